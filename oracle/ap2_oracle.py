@@ -1,0 +1,592 @@
+"""CPU ORACLE for the AP2 collocation evaluator -- TEST INFRASTRUCTURE ONLY.
+
+This module is the independent CPU restatement of the reference's hot path that the HIP
+evaluator is checked against.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import it; the product (``awebox_amd``) never does.
+
+Parity status: the reference evaluates this math inside CasADi 3.6.4's SX virtual machine, which
+cannot be imported or built in this environment.  The restatement is
+therefore pinned by the reference's own analytic known-answer tests restated in
+``tests/test_oracle_known_answers.py`` (pendulum / pseudo-Atwood Lagrangian residuals,
+``test/units/test_model.py:438-832``; frame conversions ``frames.py:206-417``; Radau constants),
+not by CasADi output ("parity partially pinned").
+
+Design: plain PyTorch float64 on the CPU.  The Lagrangian derivatives are taken exactly the way
+the reference takes them -- automatic differentiation of L with respect to the *scaled*
+generalised coordinates, followed by ``time_derivative`` as a Jacobian-vector product over the
+(variable, derivative) pairs -- so the hand-derived expressions inside the HIP kernel are checked
+against machine-differentiated ones rather than against a second copy of themselves.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+from torch.func import grad, jacfwd, jvp, vmap
+
+torch.set_default_dtype(torch.float64)
+
+# ----------------------------------------------------------------------------------------
+# layout of the 59 node variables (awebox/mdl/system.py:42-230; order x, xdot, u, z, theta)
+# ----------------------------------------------------------------------------------------
+_X = [("q10", 3), ("dq10", 3), ("omega10", 3), ("r10", 9), ("delta10", 3), ("l_t", 1), ("dl_t", 1)]
+_XD = [("d" + n, s) for n, s in _X]
+_U = [("f_fict10", 3), ("m_fict10", 3), ("ddelta10", 3), ("ddl_t", 1)]
+_Z = [("lambda10", 1)]
+_TH = [("diam_t", 1), ("t_f", 1)]
+
+
+def _build_index():
+    idx, pos = {}, 0
+    for vt, ents in (("x", _X), ("xdot", _XD), ("u", _U), ("z", _Z), ("theta", _TH)):
+        for n, s in ents:
+            idx[(vt, n)] = slice(pos, pos + s)
+            pos += s
+    return idx, pos
+
+
+IDX, NW = _build_index()
+
+# time_derivative pairs (awebox/mdl/lagr_dyn_dir/tools.py:13-73): for every xdot name 'd<v>',
+# the variable v and the first non-xdot container holding 'd<v>' (struct_op.get_variable_type
+# prefers x/u/z/theta over xdot, struct_operations.py:737-761).
+_PAIRS = [(("x", "q10"), ("x", "dq10")), (("x", "dq10"), ("xdot", "ddq10")),
+          (("x", "omega10"), ("xdot", "domega10")), (("x", "r10"), ("xdot", "dr10")),
+          (("x", "delta10"), ("u", "ddelta10")), (("x", "l_t"), ("x", "dl_t")),
+          (("x", "dl_t"), ("u", "ddl_t"))]
+
+
+def get(w, vt, name):
+    return w[IDX[(vt, name)]]
+
+
+def skew(a):
+    z = torch.zeros((), dtype=a.dtype)
+    return torch.stack([torch.stack([z, -a[2], a[1]]), torch.stack([a[2], z, -a[0]]),
+                        torch.stack([-a[1], a[0], z])])
+
+
+def cross(a, b):
+    # vect_op.cross (vector_operations.py:47-54)
+    return torch.stack([a[1] * b[2] - a[2] * b[1], -(a[0] * b[2] - a[2] * b[0]), a[0] * b[1] - a[1] * b[0]])
+
+
+def smooth_sqrt(arg, eps):
+    return (arg + eps) ** 0.5
+
+
+def norm(a):
+    return smooth_sqrt(torch.dot(a, a), 0.0)
+
+
+def smooth_norm(a, eps=1e-8):
+    return smooth_sqrt(torch.dot(a, a), eps ** 2)
+
+
+def smooth_abs(x, eps=1e-8):
+    return smooth_sqrt(x ** 2, eps ** 2)
+
+
+def reshape33(v):
+    # casadi reshape is column-major
+    return v.reshape(3, 3).T
+
+
+def vec_col(m):
+    return m.T.reshape(9)
+
+
+class Ap2Oracle:
+    """Restated awebox AP2 model + NLP assembly.
+
+    ``scaling`` [59], ``consts`` (dict of option-derived scalars), ``theta0`` (dict name ->
+    tensor) follow the reference option pipeline; see ``awebox_amd/problem.py`` for how they are
+    produced and ``tests/test_problem.py`` for their checks.
+    """
+
+    def __init__(self, scaling, consts: dict, sd_len, n_k=40, d=4):
+        self.s = torch.as_tensor(np.asarray(scaling, dtype=np.float64))
+        self.c = dict(consts)
+        self.sd_len = np.asarray(sd_len, dtype=np.int64).reshape(6, 9)
+        self.n_k, self.d = n_k, d
+        self.tau, self.C, self.D, self.w = self._radau(d)
+
+    # ------------------------------------------------------------------ collocation ---------
+    @staticmethod
+    def _radau(d):
+        """Radau IIA nodes + Lagrange coefficients (collocation.py:67-200), numpy Polynomial."""
+        from numpy.polynomial import legendre as L, polynomial as P
+        # roots of P_d(x) - P_{d-1}(x) on [-1, 1], mapped to (0, 1]
+        coeffs = np.zeros(d + 1)
+        coeffs[d] = 1.0
+        coeffs[d - 1] = -1.0
+        r = np.sort(np.real(L.legroots(coeffs)))
+        # pin the right end point exactly (Radau IIA)
+        tau_c = (r + 1.0) / 2.0
+        tau_c[-1] = 1.0
+        tau = np.concatenate([[0.0], tau_c])
+        n = d + 1
+        C = np.zeros((n, n))
+        D = np.zeros(n)
+        for j in range(n):
+            # Lagrange basis in the reference's product form (collocation.py:99-102); its value
+            # at tau=1 is exact (the factor (1 - tau_d) = 0 for j < d)
+            others = [tau[m] for m in range(n) if m != j]
+            val = 1.0
+            for r in others:
+                val *= (1.0 - r) / (tau[j] - r)
+            D[j] = val
+            # derivative from the expanded monomial form (a different evaluation path than the
+            # product rule used by awebox_amd.collocation)
+            lj = P.Polynomial.fromroots(others)
+            lj = lj / lj(tau[j])
+            dl = lj.deriv()
+            for m in range(n):
+                C[j, m] = dl(tau[m])
+        w = np.linalg.solve(C[1:, 1:], D[1:])
+        return tau, C, D, w
+
+    # ------------------------------------------------------------------ environment ---------
+    @staticmethod
+    def density(th, zz):
+        # Atmosphere.get_density, isa (atmosphere.py:42-78)
+        t = th["atmosphere.t_ref"] - th["atmosphere.gamma_air"] * zz
+        return th["atmosphere.rho_ref"] * (t / th["atmosphere.t_ref"]) ** (
+            th["atmosphere.g"] / th["atmosphere.gamma_air"] / th["atmosphere.r"] - 1.0)
+
+    @staticmethod
+    def wind_velocity(th, zz):
+        # Wind.get_velocity + get_speed 'power' (wind.py:50-89, 184-208)
+        z_cropped = smooth_abs(zz, 1.0)
+        u = th["wind.u_ref"] * (z_cropped / th["wind.z_ref"]) ** th["wind.power_wind.exp_ref"]
+        z = torch.zeros((), dtype=u.dtype)
+        return torch.stack([u, z, z])
+
+    # ------------------------------------------------------------------ time derivative -----
+    def tangent(self, w_sc):
+        """Direction vector t(w) such that time_derivative(f) = J_f(w) t(w) (tools.py:13-73)."""
+        s = self.s
+        seg = {}
+        for (vt, vn), (dt, dn) in _PAIRS:
+            iv, idv = IDX[(vt, vn)], IDX[(dt, dn)]
+            # the scaled chain rule: d f/d v_sc diag(s_v)^-1 diag(s_dv) dv_sc
+            seg[(vt, vn)] = s[idv] / s[iv] * w_sc[idv]
+        # kite rotation matrix term: d expr/d r (skew(omega_scaled) inv(R^T)) with the SCALED
+        # omega of vars_scaled (tools.py:60-71)
+        r = reshape33(get(w_sc, "x", "r10"))
+        omega_sc = get(w_sc, "x", "omega10")
+        seg[("x", "r10")] = seg[("x", "r10")] + vec_col(skew(omega_sc) @ torch.linalg.inv(r.T))
+        parts = []
+        for key, sl in sorted(IDX.items(), key=lambda kv: kv[1].start):
+            parts.append(seg[key] if key in seg else torch.zeros(sl.stop - sl.start, dtype=w_sc.dtype))
+        return torch.cat(parts)
+
+    def time_derivative(self, f):
+        def df(w_sc, *args):
+            _, out = jvp(lambda ww: f(ww, *args), (w_sc,), (self.tangent(w_sc),))
+            return out
+        return df
+
+    # ------------------------------------------------------------------ model pieces --------
+    def si(self, w_sc):
+        return w_sc * self.s
+
+    def seg_mass(self, w_sc, th):
+        # tether_aero.get_tether_segment_properties (tether_aero.py:178-267)
+        w = self.si(w_sc)
+        q = get(w, "x", "q10")
+        diam = get(w, "theta", "diam_t")[0]
+        area = math.pi * (diam / 2.) ** 2.
+        return area * th["tether.rho"] * norm(q)
+
+    def lagrangian(self, w_sc, th):
+        """L = e_kinetic - e_potential - lambda c (lagr_dyn.py:39-55, energy.py:43-144)."""
+        w = self.si(w_sc)
+        q, dq = get(w, "x", "q10"), get(w, "x", "dq10")
+        omega = get(w, "x", "omega10")
+        m_t = self.seg_mass(w_sc, th)
+        ehat = q / norm(q)
+        reelout = torch.dot(dq, ehat)
+        dq_parent = reelout * ehat
+        e_kin_tether = 0.5 * m_t / 3 * (torch.dot(dq, dq) + torch.dot(dq_parent, dq_parent)
+                                        + torch.dot(dq, dq_parent))
+        m_k = th["geometry.m_k"]
+        e_kin_kite = 0.5 * m_k * torch.dot(dq, dq)
+        J = reshape33(th["geometry.j"])
+        e_kin_rot = 0.5 * omega @ J @ omega
+        g = th["atmosphere.g"]
+        q_mean = q / 2.
+        e_pot = g * m_t * q_mean[2] + g * m_k * q[2]
+        c = self.holonomic(w_sc, th)
+        lam = get(w, "z", "lambda10")[0]
+        return (e_kin_tether + e_kin_kite + e_kin_rot) - e_pot - lam * c
+
+    def holonomic(self, w_sc, th):
+        # holonomics.get_tether_length_constraint (holonomics.py:204-264)
+        w = self.si(w_sc)
+        q = get(w, "x", "q10")
+        l_t = get(w, "x", "l_t")[0]
+        return 0.5 * (torch.dot(q, q) - l_t ** 2.0)
+
+    def element_drag(self, q_upper, q_lower, dq_upper, dq_lower, diam, th):
+        # element.get_element_drag_fun (element.py:60-104); cd 'constant'
+        q_average = (q_upper + q_lower) / 2.
+        zz = q_average[2]
+        uw = self.wind_velocity(th, zz)
+        ua = uw - (dq_upper + dq_lower) / 2.
+        eps = 1.e-6
+        ua_norm = smooth_norm(ua, eps)
+        ehat_ua = ua / smooth_norm(ua, eps)
+        tether = q_upper - q_lower
+        length_sq = torch.dot(tether, tether)
+        length_par = torch.dot(tether, ehat_ua)
+        length_perp = smooth_sqrt(length_sq - length_par ** 2., eps ** 2.)
+        cd = th["tether.cd"]
+        return cd * 0.5 * self.density(th, zz) * ua_norm * diam * length_perp * ua
+
+    def tether_drag_upper(self, w, th):
+        # segment.get_distributed_segment_forces 'multi' (segment.py:38-65); main tether: the
+        # lower node is the ground (q = dq = 0)
+        q, dq = get(w, "x", "q10"), get(w, "x", "dq10")
+        diam = get(w, "theta", "diam_t")[0]
+        n = int(self.c["n_elements"])
+        total = torch.zeros(3, dtype=q.dtype)
+        ds = 1.0 / n
+        s_grid = np.linspace(0.5 * ds, 1 - 0.5 * ds, n)
+        for e in range(n):
+            lo, up = float(e) / float(n), float(e + 1) / float(n)
+            drag = self.element_drag(q * up, q * lo, dq * up, dq * lo, diam, th)
+            total = total + s_grid[e] * drag
+        return total
+
+    def aero(self, w, th):
+        """6-DOF stability-derivative force/moment (six_dof_kite.py:165-201, kite_aero.py:63-117)."""
+        q, dq = get(w, "x", "q10"), get(w, "x", "dq10")
+        omega = get(w, "x", "omega10")
+        R = reshape33(get(w, "x", "r10"))
+        delta = get(w, "x", "delta10")
+        u = self.wind_velocity(th, q[2]) - dq                    # kite_dir/tools.py:162-215
+        rho = self.density(th, q[2])
+        e1, e2, e3 = R[:, 0], R[:, 1], R[:, 2]
+        alpha = torch.dot(u, e3) / smooth_abs(torch.dot(u, e1))  # indicators.py:435-463
+        beta = torch.dot(u, e2) / smooth_abs(torch.dot(u, e1))
+        airspeed = norm(u)
+        # stability_derivatives.collect_inputs / get_p_q_r, frame 'control'
+        om_c = omega * torch.tensor([-1., 1., -1.])
+        om_hat = om_c / (2. * airspeed)
+        b, cr = th["geometry.b_ref"], th["geometry.c_ref"]
+        p, qq, r = om_hat[0] * b, om_hat[1] * cr, om_hat[2] * b
+        inputs = [torch.ones((), dtype=u.dtype), alpha, -beta, p, qq, r, delta[0], delta[1], delta[2]]
+        sd = th["aero.stab_derivs"].reshape(6, 9, 3)
+        coeffs = []
+        for ci in range(6):
+            acc = torch.zeros((), dtype=u.dtype)
+            for ii in range(9):
+                n = int(self.sd_len[ci, ii])
+                if n == 0:
+                    continue
+                stack = torch.stack([inputs[ii] * alpha ** l for l in range(n)])
+                weight = th["aero.moment_factor"] if (ci >= 3 and ii >= 6) else 1.0
+                acc = acc + weight * torch.dot(sd[ci, ii, :n], stack)
+            coeffs.append(acc)
+        CF = torch.stack(coeffs[:3])
+        CM = torch.stack(coeffs[3:])
+        dyn = 0.5 * rho * torch.dot(u, u)
+        s_ref = th["geometry.s_ref"]
+        F_ctrl = CF * dyn * s_ref
+        M_ctrl = dyn * s_ref * (torch.stack([b, cr, b]) * CM)
+        flip = torch.tensor([-1., 1., -1.])
+        F_earth = R @ (flip * F_ctrl)                            # frames.from_control_to_earth
+        M_body = flip * M_ctrl                                   # frames.from_control_to_body
+        return dict(u=u, rho=rho, alpha=alpha, beta=beta, airspeed=airspeed, F_earth=F_earth,
+                    M_body=M_body, R=R)
+
+    # ------------------------------------------------------------------ residuals -----------
+    def node(self, w_sc, gamma, th):
+        """Model equalities [24], inequalities [9], power integrand, beta at one node."""
+        s, c = self.s, self.c
+        w = self.si(w_sc)
+        q, dq = get(w, "x", "q10"), get(w, "x", "dq10")
+        l_t, dl_t = get(w, "x", "l_t")[0], get(w, "x", "dl_t")[0]
+        lam = get(w, "z", "lambda10")[0]
+        aero = self.aero(w, th)
+
+        # translational dynamics (lagr_dyn.py:68-109)
+        iq, idq = IDX[("x", "q10")], IDX[("x", "dq10")]
+
+        def dL(w_):
+            return grad(lambda ww: self.lagrangian(ww, th))(w_)
+
+        def dL_ddq(w_):
+            return dL(w_)[idq]
+
+        dlagr_dqdot_dt = self.time_derivative(dL_ddq)(w_sc)
+        dlagr_dq = dL(w_sc)[iq]
+        lhs = dlagr_dqdot_dt / s[idq] - dlagr_dq / s[iq]
+        # momentum correction (lagr_dyn.py:174-204)
+        mass_flow = self.time_derivative(lambda ww: self.seg_mass(ww, th))(w_sc)
+        correction = mass_flow * dq
+        # generalised forces (forces.py:47-80, 148-171)
+        f_fict = get(w, "u", "f_fict10")
+        F = self.tether_drag_upper(w, th) + (gamma * f_fict + aero["F_earth"])
+        rhs = F + correction
+        scaling_mass = math.pi * (c["scaling_diam"] / 2.) ** 2. * th["tether.rho"] * c["scaling_length"]
+        node_mass = scaling_mass / 2. + th["geometry.m_k"]                     # mass.py:62-93
+        force_scaling = node_mass * c["g_scaling"] * 10.
+        trans = (lhs - rhs) / force_scaling
+
+        # holonomic constraint with Baumgarte (holonomics.py:17-123, 267-312)
+        cfun = lambda ww: self.holonomic(ww, th)  # noqa: E731
+        g0 = cfun(w_sc)
+        g1 = self.time_derivative(cfun)(w_sc)
+        g2 = self.time_derivative(self.time_derivative(cfun))(w_sc)
+        kappa = th["tether.kappa"]
+        hol_lhs = g2 + 2. * kappa * g1 + kappa ** 2. * g0
+        hol_scale = kappa ** 2. * (c["scaling_length"] * c["q_scaling_mean"])
+        hol = (hol_lhs / hol_scale).reshape(1)
+
+        # rotational dynamics + DCM (lagr_dyn.py:207-254), tether moment (forces.py:174-190)
+        omega = get(w, "x", "omega10")
+        domega = get(w, "xdot", "domega10")
+        R = aero["R"]
+        dR = reshape33(get(w, "xdot", "dr10"))
+        J = reshape33(th["geometry.j"])
+        lam_c = lambda ww: self.si(ww)[IDX[("z", "lambda10")]][0] * self.holonomic(ww, th)  # noqa: E731
+        dW_dr = grad(lam_c)(w_sc)[IDX[("x", "r10")]]
+        n_tether = 2. * self.unskew(R.T @ reshape33(dW_dr))  # jacobian_dcm(...).T
+        M = gamma * get(w, "u", "m_fict10") + aero["M_body"]
+        omega_derivative = M - (J @ domega + cross(omega, J @ omega) + n_tether)
+        rot = omega_derivative / c["m_aero_scaling"]
+        kappa_r = th["kappa_r"]
+        ortho = kappa_r / 2. * (torch.eye(3) - R.T @ R)
+        dcm = vec_col(dR - R @ (ortho + skew(omega)))
+
+        # trivial kinematics, sorted xdot names (lagr_dyn.py:141-169)
+        triv = []
+        for xd_name, (ut, un) in (("ddelta10", ("u", "ddelta10")), ("ddl_t", ("u", "ddl_t")),
+                                  ("dl_t", ("x", "dl_t")), ("dq10", ("x", "dq10"))):
+            si_diff = get(w, "xdot", xd_name) - get(w, ut, un)
+            mean = (s[IDX[(ut, un)]] * s[IDX[("xdot", xd_name)]]) ** 0.5
+            triv.append(si_diff / mean)
+        eq = torch.cat([trans, hol, rot, dcm] + triv)
+
+        # inequalities (dynamics.py:655-821, 1022-1117; indicators.py:286-338)
+        tension = lam * norm(q)
+        f_lim = th["model_bounds.tether_force_limits"]
+        force_scaling_t = c["lambda_scaling"] * c["scaling_length"]
+        u = aero["u"]
+        airspeed = norm(u)
+        a_lim = th["model_bounds.airspeed_limits"]
+        u_ref = th["wind.u_ref"]
+        e1, e2, e3 = R[:, 0], R[:, 1], R[:, 2]
+        tight, a_ref = c["aero_tightness"], c["airspeed_ref"]
+        amax, amin, bmax, bmin = c["alpha_max"], c["alpha_min"], c["beta_max"], c["beta_min"]
+        sabs = lambda v: math.sqrt(v ** 2 + 1e-16)  # noqa: E731  smooth_abs of a constant
+        alpha_ub = (torch.dot(u, e3) - torch.dot(u, e1) * amax) * tight / a_ref / sabs(amax)
+        alpha_lb = (-torch.dot(u, e3) + torch.dot(u, e1) * amin) * tight / a_ref / sabs(amin)
+        beta_ub = (torch.dot(u, e2) - torch.dot(u, e1) * bmax) * tight / a_ref / sabs(bmax)
+        beta_lb = (-torch.dot(u, e2) + torch.dot(u, e1) * bmin) * tight / a_ref / sabs(bmin)
+        gamma_max = th["model_bounds.rot_angles"][2]
+        yaw = (torch.dot(q, R[:, 2]) - torch.cos(gamma_max) * norm(q)) / c["scaling_length"]
+        ineq = torch.stack([(tension - f_lim[1]) / force_scaling_t, (f_lim[0] - tension) / force_scaling_t,
+                            (airspeed - a_lim[1]) / u_ref, (a_lim[0] - airspeed) / u_ref,
+                            alpha_ub, alpha_lb, beta_ub, beta_lb, -1. * yaw])
+
+        power = lam * l_t * dl_t / c["energy_scaling"]            # dynamics.py:318-330
+        beta_out = torch.dot(u, e2) / smooth_abs(torch.dot(u, e1))
+        return eq, ineq, power, beta_out
+
+    @staticmethod
+    def unskew(A):
+        return 0.5 * torch.stack([A[2, 1] - A[1, 2], A[0, 2] - A[2, 0], A[1, 0] - A[0, 1]])
+
+    # ------------------------------------------------------------------ NLP assembly --------
+    def unpack_theta0(self, theta0_vec, offsets: dict) -> dict:
+        th = {}
+        for name, (o, sz) in offsets.items():
+            v = theta0_vec[o:o + sz]
+            th[name] = v[0] if sz == 1 else v
+        return th
+
+    def _node_vmap(self, W, gamma, th):
+        return vmap(self.node, in_dims=(0, None, None))(W, gamma, th)
+
+    def interval_rows(self, wloc, th):
+        """All g rows of one shooting interval as a function of its local V slice.
+
+        ``wloc = [theta(2), phi(7), x[k], u[k], xdot[k], z[k], coll_var[k, 0..d-1], x[k+1]]``
+        (ocp/constraints.py:210-373; collocation.py:202-258, 319-336)
+        """
+        d = self.d
+        nx, nu = 23, 10
+        theta, phi = wloc[0:2], wloc[2:9]
+        o = 9
+        xk = wloc[o:o + nx]; o += nx
+        uk = wloc[o:o + nu]; o += nu
+        xdk = wloc[o:o + nx]; o += nx
+        zk = wloc[o:o + 1]; o += 1
+        coll_x, coll_z = [], []
+        for _ in range(d):
+            coll_x.append(wloc[o:o + nx]); o += nx
+            coll_z.append(wloc[o:o + 1]); o += 1
+        xk1 = wloc[o:o + nx]
+        gamma = phi[0]
+        tf = theta[1]
+        h = 1.0 / self.n_k
+        C = torch.as_tensor(self.C)
+        X = [xk] + coll_x
+        W = [torch.cat([xk, xdk, uk, zk, theta])]
+        for j in range(d):
+            xp = sum(C[r, j + 1] * X[r] for r in range(d + 1))
+            W.append(torch.cat([coll_x[j], xp / h / tf, uk, coll_z[j], theta]))
+        W = torch.stack(W)
+        eq, ineq, power, beta = vmap(self.node, in_dims=(0, None, None))(W, gamma, th)
+        Dc = torch.as_tensor(self.D)
+        xf = sum(Dc[r] * X[r] for r in range(d + 1))
+        cont = xk1 - xf
+        rows = [eq[0], ineq[0]] + [eq[j + 1] for j in range(d)] + [cont]
+        return torch.cat(rows)
+
+    def local_index(self, layout, k):
+        glob = np.arange(0, 9)
+        base = layout.v_intervals + k * layout.interval_stride
+        return np.concatenate([glob, np.arange(base, base + layout.interval_stride + 23)])
+
+    def nlp_g(self, V, P, layout, theta0_offsets):
+        V = torch.as_tensor(V)
+        P = torch.as_tensor(P)
+        th = self.unpack_theta0(P[layout.p_theta0:], theta0_offsets)
+        locs = torch.stack([V[torch.as_tensor(self.local_index(layout, k))] for k in range(self.n_k)])
+        rows = vmap(self.interval_rows, in_dims=(0, None))(locs, th)
+        g = [rows.reshape(-1), self.periodic(V, layout)]
+        return torch.cat(g)
+
+    def periodic(self, V, layout):
+        # operation.make_periodicity_equality with sorted x names (operation.py:245-266)
+        order = torch.as_tensor(_periodic_order())
+        x0 = V[torch.as_tensor(layout.x(0))]
+        xT = V[torch.as_tensor(layout.coll_x(self.n_k - 1, self.d - 1))]
+        return x0[order] - xT[order]
+
+    def nlp_jac_g(self, V, P, layout, theta0_offsets):
+        """Sparse J_g as a scipy CSC matrix (exact zeros dropped)."""
+        import scipy.sparse as sp
+        V = torch.as_tensor(V)
+        P = torch.as_tensor(P)
+        th = self.unpack_theta0(P[layout.p_theta0:], theta0_offsets)
+        idx = np.stack([self.local_index(layout, k) for k in range(self.n_k)])
+        locs = V[torch.as_tensor(idx)]
+        J = vmap(jacfwd(self.interval_rows), in_dims=(0, None))(locs, th).numpy()  # [n_k, 152, 185]
+        rows, cols, vals = [], [], []
+        R = layout.rows_per_interval
+        for k in range(self.n_k):
+            r, c = np.nonzero(J[k])
+            rows.append(k * R + r)
+            cols.append(idx[k][c])
+            vals.append(J[k][r, c])
+        order = _periodic_order()
+        pr = layout.g_periodic + np.arange(23)
+        rows += [pr, pr]
+        cols += [layout.x(0)[order], layout.coll_x(self.n_k - 1, self.d - 1)[order]]
+        vals += [np.ones(23), -np.ones(23)]
+        return sp.csc_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                             shape=(layout.n_g, layout.n_v))
+
+    def nlp_f(self, V, P, layout, theta0_offsets, cost_names, phi_names):
+        """Objective (ocp/objective.py:45-544) for a power_cycle trajectory."""
+        V = torch.as_tensor(V)
+        P = torch.as_tensor(P)
+        th = self.unpack_theta0(P[layout.p_theta0:], theta0_offsets)
+        cost = {n: P[layout.p_cost + i] for i, n in enumerate(cost_names)}
+        weights = P[layout.p_weights:layout.p_weights + NW]
+        vref = P[layout.p_ref:layout.p_ref + layout.n_v]
+        c = self.c
+        d, n_k = self.d, self.n_k
+        h = 1.0 / n_k
+        C = torch.as_tensor(self.C)
+        tf = V[layout.theta()[1]]
+        phi = V[torch.as_tensor(layout.phi())]
+        psi = phi[phi_names.index("psi")]
+        gamma = phi[phi_names.index("gamma")]
+
+        # category masks and weight factors (objective.py:147-170)
+        cats = {"tracking": [], "xdot_regularisation": [], "u_regularisation": [], "fictitious": [],
+                "theta_regularisation": []}
+        for (vt, n), sl in IDX.items():
+            if vt in ("x", "z"):
+                cat = "tracking"
+            elif vt == "xdot":
+                cat = "xdot_regularisation"
+            elif vt == "u":
+                cat = "fictitious" if n in ("f_fict10", "m_fict10") else "u_regularisation"
+            else:
+                cat = None if n == "t_f" else "theta_regularisation"
+            if cat is not None:
+                cats[cat].extend(range(sl.start, sl.stop))
+        norm_of = {"tracking": c["norm_tracking"], "xdot_regularisation": c["norm_xdot_reg"],
+                   "u_regularisation": c["norm_u_reg"], "fictitious": c["norm_fictitious"],
+                   "theta_regularisation": c["norm_theta_reg"]}
+        w_eff = weights.clone()
+        for cat, ids in cats.items():
+            ids_t = torch.as_tensor(ids)
+            w_eff = w_eff.index_put((ids_t,), weights[ids_t] * cost[cat[:-5] if cat.endswith("_cost") else cat] / norm_of[cat])
+
+        Wn, Rn, wj = [], [], []
+        for k in range(n_k):
+            X = [V[torch.as_tensor(layout.x(k))]] + [V[torch.as_tensor(layout.coll_x(k, j))] for j in range(d)]
+            for j in range(d):
+                xp = sum(C[r, j + 1] * X[r] for r in range(d + 1))
+                Wn.append(torch.cat([X[j + 1], xp / h / tf, V[torch.as_tensor(layout.u(k))],
+                                     V[torch.as_tensor(layout.coll_z(k, j))], V[torch.as_tensor(layout.theta())]]))
+                Rn.append(torch.cat([vref[torch.as_tensor(layout.coll_x(k, j))], torch.zeros(23),
+                                     vref[torch.as_tensor(layout.u(k))], vref[torch.as_tensor(layout.coll_z(k, j))],
+                                     vref[torch.as_tensor(layout.theta())]]))
+                wj.append(self.w[j])
+        Wn, Rn = torch.stack(Wn), torch.stack(Rn)
+        wj = torch.as_tensor(np.array(wj))
+        reg = wj[:, None] * w_eff[None, :] * (Wn - Rn) ** 2
+        comp = {cat: reg[:, torch.as_tensor(ids)].sum() for cat, ids in cats.items()}
+
+        eq, ineq, power, beta = vmap(self.node, in_dims=(0, None, None))(Wn, gamma, th)
+        # integral outputs (collocation.py:272-316): tf/N Lambda^T p, then the D-weighted end value
+        Lam = torch.as_tensor(np.linalg.solve(self.C[1:, 1:], np.eye(d)))
+        Dc = torch.as_tensor(self.D)
+        e_end = torch.zeros(())
+        pw = power.reshape(n_k, d)
+        for k in range(n_k):
+            io = tf / n_k * (Lam.T @ pw[k])
+            e_end = e_end + sum(Dc[j + 1] * io[j] for j in range(d))
+        power_cost = cost["power"] * (-1.) * e_end / tf
+        beta_cost = cost["beta"] * (wj * beta ** 2).sum() / c["norm_beta"]
+        tf_ref = vref[layout.theta()[1]]
+        time_cost = cost["t_f"] * (tf - tf_ref) * (tf - tf_ref)
+        homotopy = sum(cost[n] * phi[i] for i, n in enumerate(phi_names))
+        general = (comp["fictitious"] + comp["u_regularisation"] + comp["xdot_regularisation"]
+                   + comp["theta_regularisation"] + beta_cost + time_cost)
+        return psi * comp["tracking"] + (1. - psi) * power_cost + general + homotopy
+
+    def nlp_grad_f(self, V, P, layout, theta0_offsets, cost_names, phi_names):
+        V = torch.as_tensor(V)
+        return grad(lambda v: self.nlp_f(v, P, layout, theta0_offsets, cost_names, phi_names))(V)
+
+
+def _periodic_order():
+    off, pos = {}, 0
+    for n, s in _X:
+        off[n] = (pos, s)
+        pos += s
+    out = []
+    for name in sorted(off):
+        o, s = off[name]
+        out.extend(range(o, o + s))
+    return np.array(out)
+
+
+def from_problem(consts, n_k=40, d=4):
+    """Build the oracle from an ``awebox_amd.problem.Ap2Constants`` (inputs only)."""
+    from awebox_amd import problem as pb
+    names = pb.CONST_NAMES
+    import re
+    cd = {n: float(consts.consts[i]) for i, n in enumerate(names) if not re.match(r"(scaling|sd_len)\d+$", n)}
+    return Ap2Oracle(consts.scaling, cd, consts.sd_len, n_k=n_k, d=d)
