@@ -1,0 +1,98 @@
+// Scalar types the AP2 node model is instantiated with.
+//
+//   double  -- value only (f/g evaluation)
+//   Dual    -- forward-mode derivative along ONE direction; on the GPU every lane of a
+//              wavefront carries a different direction, so one wavefront produces a full
+//              node Jacobian block
+//   Dep     -- structural dependency bitmask over <= 64 node inputs; used once on the host to
+//              derive the fixed CCS sparsity of the constraint Jacobian (what CasADi's
+//              symbolic sparsity propagation provides in the reference, preparation.py:366-400)
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define AWE_HD __host__ __device__ __forceinline__
+#else
+#define AWE_HD inline
+#endif
+
+namespace awe {
+
+// ------------------------------------------------------------------------------------------
+struct Dual {
+    double v, d;
+    AWE_HD Dual() : v(0.0), d(0.0) {}
+    AWE_HD Dual(double a) : v(a), d(0.0) {}
+    AWE_HD Dual(double a, double b) : v(a), d(b) {}
+};
+
+AWE_HD Dual operator+(Dual a, Dual b) { return Dual(a.v + b.v, a.d + b.d); }
+AWE_HD Dual operator-(Dual a, Dual b) { return Dual(a.v - b.v, a.d - b.d); }
+AWE_HD Dual operator-(Dual a) { return Dual(-a.v, -a.d); }
+AWE_HD Dual operator*(Dual a, Dual b) { return Dual(a.v * b.v, a.d * b.v + a.v * b.d); }
+AWE_HD Dual operator/(Dual a, Dual b) {
+    double q = a.v / b.v;
+    return Dual(q, (a.d - q * b.d) / b.v);
+}
+AWE_HD Dual operator+(Dual a, double b) { return Dual(a.v + b, a.d); }
+AWE_HD Dual operator+(double a, Dual b) { return Dual(a + b.v, b.d); }
+AWE_HD Dual operator-(Dual a, double b) { return Dual(a.v - b, a.d); }
+AWE_HD Dual operator-(double a, Dual b) { return Dual(a - b.v, -b.d); }
+AWE_HD Dual operator*(Dual a, double b) { return Dual(a.v * b, a.d * b); }
+AWE_HD Dual operator*(double a, Dual b) { return Dual(a * b.v, a * b.d); }
+AWE_HD Dual operator/(Dual a, double b) { return Dual(a.v / b, a.d / b); }
+AWE_HD Dual operator/(double a, Dual b) {
+    double q = a / b.v;
+    return Dual(q, -q * b.d / b.v);
+}
+AWE_HD Dual& operator+=(Dual& a, Dual b) { a = a + b; return a; }
+AWE_HD Dual& operator-=(Dual& a, Dual b) { a = a - b; return a; }
+AWE_HD Dual& operator*=(Dual& a, Dual b) { a = a * b; return a; }
+
+AWE_HD Dual sqrt(Dual a) {
+    double s = ::sqrt(a.v);
+    return Dual(s, a.d * 0.5 / s);
+}
+// a^p for constant exponent p (a > 0)
+AWE_HD Dual pow(Dual a, double p) {
+    double r = ::pow(a.v, p);
+    return Dual(r, a.d * p * r / a.v);
+}
+AWE_HD double value(Dual a) { return a.v; }
+AWE_HD double tangent(Dual a) { return a.d; }
+
+// ------------------------------------------------------------------------------------------
+struct Dep {
+    uint64_t m;
+    AWE_HD Dep() : m(0) {}
+    AWE_HD Dep(double) : m(0) {}
+    AWE_HD static Dep bit(int i) { Dep d; d.m = (uint64_t)1 << i; return d; }
+};
+AWE_HD Dep mk_dep(uint64_t m) { Dep d; d.m = m; return d; }
+AWE_HD Dep operator+(Dep a, Dep b) { return mk_dep(a.m | b.m); }
+AWE_HD Dep operator-(Dep a, Dep b) { return mk_dep(a.m | b.m); }
+AWE_HD Dep operator-(Dep a) { return a; }
+AWE_HD Dep operator*(Dep a, Dep b) { return mk_dep(a.m | b.m); }
+AWE_HD Dep operator/(Dep a, Dep b) { return mk_dep(a.m | b.m); }
+AWE_HD Dep operator+(Dep a, double) { return a; }
+AWE_HD Dep operator+(double, Dep b) { return b; }
+AWE_HD Dep operator-(Dep a, double) { return a; }
+AWE_HD Dep operator-(double, Dep b) { return b; }
+AWE_HD Dep operator*(Dep a, double) { return a; }
+AWE_HD Dep operator*(double, Dep b) { return b; }
+AWE_HD Dep operator/(Dep a, double) { return a; }
+AWE_HD Dep operator/(double, Dep b) { return b; }
+AWE_HD Dep& operator+=(Dep& a, Dep b) { a.m |= b.m; return a; }
+AWE_HD Dep& operator-=(Dep& a, Dep b) { a.m |= b.m; return a; }
+AWE_HD Dep& operator*=(Dep& a, Dep b) { a.m |= b.m; return a; }
+AWE_HD Dep sqrt(Dep a) { return a; }
+AWE_HD Dep pow(Dep a, double) { return a; }
+
+AWE_HD double value(double a) { return a; }
+AWE_HD double sqrt(double a) { return ::sqrt(a); }
+AWE_HD double pow(double a, double p) { return ::pow(a, p); }
+
+}  // namespace awe

@@ -1,0 +1,204 @@
+"""Python side of the drop-in boundary: ctypes binding of ``libawegpu.so`` (include/awegpu.h).
+
+``Ap2Evaluator`` exposes the NLP oracle surface IPOPT reaches through ``casadi.nlpsol`` in the
+reference (awebox/opti/preparation.py:366-400): ``nlp_f``, ``nlp_g``, ``nlp_grad_f`` and
+``nlp_jac_g`` with CasADi's argument meaning (x = V, p = P) and output convention (J_g in CCS,
+column-major).  It also provides the batched device-pointer path used by the sweep / MPC drivers
+and by ``bench.py``.
+
+There is no CPU fallback: if the shared library is missing or no HIP device is visible, every
+constructor raises ``AwegpuUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import problem as pb
+
+_LIB = None
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libawegpu.so")
+
+AWE_OK, AWE_ERR_ARG, AWE_ERR_HIP, AWE_ERR_NONFINITE, AWE_ERR_NODEVICE = 0, 1, 2, 3, 4
+
+EXPORTED_SYMBOLS = ["awe_create", "awe_destroy", "awe_last_error", "awe_sizes", "awe_sparsity_jac",
+                    "awe_sparsity_jac_static",
+                    "awe_eval_nlp", "awe_eval_g", "awe_eval_f", "awe_eval_nlp_host",
+                    "awe_last_kernel_ms", "awe_device_count"]
+
+
+class AwegpuUnavailable(RuntimeError):
+    """The HIP evaluator cannot run here (library not built or no MI355X visible)."""
+
+
+class AwegpuError(RuntimeError):
+    pass
+
+
+def load_library(path: str = _LIB_PATH):
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise AwegpuUnavailable(f"{path} not built; run `python -m awebox_amd.build`")
+    lib = ctypes.CDLL(path)
+    dp = ctypes.POINTER(ctypes.c_double)
+    ip = ctypes.POINTER(ctypes.c_int)
+    h = ctypes.c_void_p
+    lib.awe_create.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(h)]
+    lib.awe_destroy.argtypes = [h]
+    lib.awe_last_error.restype = ctypes.c_char_p
+    lib.awe_sizes.argtypes = [h, ip, ip, ip, ip]
+    lib.awe_sparsity_jac.argtypes = [h, ip, ip]
+    lib.awe_eval_nlp.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.awe_eval_g.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.awe_eval_f.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.awe_eval_nlp_host.argtypes = [h, dp, dp, dp, dp, dp, dp]
+    lib.awe_last_kernel_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.awe_device_count.restype = ctypes.c_int
+    lib.awe_sparsity_jac_static.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip]
+    _LIB = lib
+    return lib
+
+
+def sparsity_jac_static(consts: pb.Ap2Constants):
+    """CCS pattern (colind, row) of J_g derived on the CPU -- no device needed."""
+    lib = load_library()
+    cfg = consts.cfg
+    c = np.ascontiguousarray(consts.consts, dtype=np.float64)
+    nnz = ctypes.c_int()
+    ip = ctypes.POINTER(ctypes.c_int)
+    rc = lib.awe_sparsity_jac_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz), None, None)
+    if rc != AWE_OK:
+        raise AwegpuError(lib.awe_last_error().decode())
+    lay = pb.NlpLayout(cfg.n_k, cfg.d)
+    colind = np.zeros(lay.n_v + 1, dtype=np.int32)
+    row = np.zeros(nnz.value, dtype=np.int32)
+    rc = lib.awe_sparsity_jac_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
+                                     colind.ctypes.data_as(ip), row.ctypes.data_as(ip))
+    if rc != AWE_OK:
+        raise AwegpuError(lib.awe_last_error().decode())
+    return colind, row
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class Ap2Evaluator:
+    """HIP evaluator of the AP2 direct-collocation NLP for ``batch`` (V, P) instances."""
+
+    def __init__(self, consts: pb.Ap2Constants | None = None, batch: int = 1):
+        self.consts = consts or pb.build_constants()
+        cfg = self.consts.cfg
+        self.layout = pb.NlpLayout(cfg.n_k, cfg.d)
+        self.batch = int(batch)
+        self._lib = load_library()
+        if self._lib.awe_device_count() <= 0:
+            raise AwegpuUnavailable("no HIP device visible: the evaluator has no CPU fallback")
+        c = np.ascontiguousarray(self.consts.consts, dtype=np.float64)
+        handle = ctypes.c_void_p()
+        self._check(self._lib.awe_create(cfg.n_k, cfg.d, _dptr(c), c.size, self.batch, ctypes.byref(handle)))
+        self._h = handle
+        n_v, n_g, n_p, nnz = (ctypes.c_int() for _ in range(4))
+        self._check(self._lib.awe_sizes(self._h, ctypes.byref(n_v), ctypes.byref(n_g), ctypes.byref(n_p),
+                                        ctypes.byref(nnz)))
+        self.n_v, self.n_g, self.n_p, self.nnz = n_v.value, n_g.value, n_p.value, nnz.value
+        assert (self.n_v, self.n_g, self.n_p) == (self.layout.n_v, self.layout.n_g, self.layout.n_p)
+        self._colind = np.zeros(self.n_v + 1, dtype=np.int32)
+        self._row = np.zeros(self.nnz, dtype=np.int32)
+        ip = ctypes.POINTER(ctypes.c_int)
+        self._check(self._lib.awe_sparsity_jac(self._h, self._colind.ctypes.data_as(ip),
+                                               self._row.ctypes.data_as(ip)))
+
+    # -------------------------------------------------------------------------------
+    def _check(self, rc):
+        if rc != AWE_OK:
+            msg = self._lib.awe_last_error().decode()
+            if rc == AWE_ERR_NODEVICE:
+                raise AwegpuUnavailable(msg)
+            raise AwegpuError(f"awegpu error {rc}: {msg}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.awe_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sparsity_jac(self):
+        """CCS pattern of J_g: (colind[n_v+1], row[nnz]) -- nlp_jac_g's output sparsity."""
+        return self._colind.copy(), self._row.copy()
+
+    # ---------------------------------------------- device path (torch CUDA tensors) ---
+    def eval_nlp_device(self, V, P, f, g, grad_f, jac, stream=None):
+        """f, g, grad f, J_g values for all batch members; tensors must be contiguous fp64 on
+        the GPU with shapes [B, n_v], [B, n_p], [B], [B, n_g], [B, n_v], [B, nnz]."""
+        import torch
+        for t, n in ((V, self.n_v), (P, self.n_p), (g, self.n_g), (grad_f, self.n_v), (jac, self.nnz)):
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
+                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+        if f.numel() != self.batch:
+            raise ValueError("f must hold one value per batch member")
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.awe_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
+                                           grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
+
+    def eval_g_device(self, V, P, g, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.awe_eval_g(self._h, V.data_ptr(), P.data_ptr(), g.data_ptr(), ctypes.c_void_p(s)))
+
+    def eval_f_device(self, V, P, f, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.awe_eval_f(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), ctypes.c_void_p(s)))
+
+    def last_kernel_ms(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        self._check(self._lib.awe_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    # ---------------------------------------------- host path (numpy) ----------------
+    def eval_nlp(self, V, P):
+        """Host arrays in, host arrays out: dict(f [B], g [B, n_g], grad_f [B, n_v], jac [B, nnz])."""
+        V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))
+        P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(self.batch, self.n_p))
+        f = np.zeros(self.batch)
+        g = np.zeros((self.batch, self.n_g))
+        grad = np.zeros((self.batch, self.n_v))
+        jac = np.zeros((self.batch, self.nnz))
+        self._check(self._lib.awe_eval_nlp_host(self._h, _dptr(V), _dptr(P), _dptr(f), _dptr(g), _dptr(grad),
+                                                _dptr(jac)))
+        return {"f": f, "g": g, "grad_f": grad, "jac": jac}
+
+    def jac_csc(self, values):
+        import scipy.sparse as sp
+        return sp.csc_matrix((np.asarray(values), self._row, self._colind), shape=(self.n_g, self.n_v))
+
+    # ---- CasADi nlpsol oracle names (batch member 0) --------------------------------
+    def _single(self, x, p):
+        if self.batch != 1:
+            raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
+        return self.eval_nlp(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1))
+
+    def nlp_f(self, x, p):
+        return float(self._single(x, p)["f"][0])
+
+    def nlp_g(self, x, p):
+        return self._single(x, p)["g"][0]
+
+    def nlp_grad_f(self, x, p):
+        out = self._single(x, p)
+        return float(out["f"][0]), out["grad_f"][0]
+
+    def nlp_jac_g(self, x, p):
+        out = self._single(x, p)
+        return out["g"][0], self.jac_csc(out["jac"][0])

@@ -1,0 +1,140 @@
+"""Parity of the HIP evaluator (through the C ABI) with the CPU oracle, on an MI355X.
+
+Tolerances (fp64; the two implementations differ only in evaluation order -- the oracle
+differentiates the Lagrangian automatically, the kernel evaluates hand-derived expressions):
+  g, grad f : |a - b| <= 1e-9 |b| + 1e-11 * max|b|
+  J_g       : |a - b| <= 1e-9 |b| + 1e-11 * max|column of b|  (values compared on the union pattern)
+  f         : relative 1e-12
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from awebox_amd import problem as pb
+from awebox_amd.initial_guess import batch_member, initial_guess
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL_REL = 1e-9, 1e-11
+
+
+def _close(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    tol = RTOL * np.abs(b) + ATOL_REL * max(np.abs(b).max(), 1e-300)
+    bad = np.abs(a - b) > tol
+    assert not bad.any(), f"{what}: {bad.sum()} entries off, worst {np.abs(a - b)[bad].max():.3e} at {np.argmax(np.abs(a - b) - tol)}"
+
+
+def _close_jac(Jk, Jo, what="J_g"):
+    Jk, Jo = sp.csc_matrix(Jk), sp.csc_matrix(Jo)
+    D = (Jk - Jo).tocsc()
+    colmax = np.maximum(abs(Jo).max(axis=0).toarray().ravel(), 1e-300)
+    D.data = np.abs(D.data)
+    Jo_on_D = abs(Jo).tocsc()
+    worst = 0.0
+    for c in range(D.shape[1]):
+        s, e = D.indptr[c], D.indptr[c + 1]
+        if s == e:
+            continue
+        rows = D.indices[s:e]
+        ref = np.asarray(Jo_on_D[rows, c].todense()).ravel()
+        tol = RTOL * ref + ATOL_REL * colmax[c]
+        excess = D.data[s:e] - tol
+        worst = max(worst, excess.max())
+        assert (excess <= 0).all(), f"{what}: column {c} rows {rows[excess > 0]} off by {D.data[s:e][excess > 0]}"
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test on a machine without a visible GPU")
+    from awebox_amd.build import build
+    build()
+    return torch
+
+
+def _setup(n_k=40, d=4):
+    from oracle.ap2_oracle import from_problem
+    consts = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+    lay = pb.NlpLayout(n_k, d)
+    v0 = initial_guess(consts, lay)
+    return consts, lay, v0, from_problem(consts, n_k=n_k, d=d)
+
+
+def _oracle_all(orc, lay, V, P):
+    g = orc.nlp_g(V, P, lay, pb.THETA0_OFF).numpy()
+    f = float(orc.nlp_f(V, P, lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES))
+    grad = orc.nlp_grad_f(V, P, lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES).numpy()
+    J = orc.nlp_jac_g(V, P, lay, pb.THETA0_OFF)
+    return f, g, grad, J
+
+
+@pytest.mark.parametrize("n_k,d,member", [(40, 4, None), (40, 4, 0), (40, 4, 7), (5, 3, 1), (3, 2, 2)])
+def test_nlp_eval_matches_oracle(gpu, n_k, d, member):
+    from awebox_amd.evaluator import Ap2Evaluator
+    consts, lay, v0, orc = _setup(n_k, d)
+    V = v0 if member is None else batch_member(v0, lay, member)
+    P = pb.pack_p(lay, consts, v0)
+    ev = Ap2Evaluator(consts, batch=1)
+    out = ev.eval_nlp(V, P)
+    f, g, grad, J = _oracle_all(orc, lay, V, P)
+    _close(out["g"][0], g, "g")
+    assert out["f"][0] == pytest.approx(f, rel=1e-12)
+    _close(out["grad_f"][0], grad, "grad_f")
+    _close_jac(ev.jac_csc(out["jac"][0]), J)
+
+
+def test_batched_sweep_members_match_oracle(gpu):
+    """8 instances per launch with different V and different u_ref (the sweep parameter)."""
+    from awebox_amd.evaluator import Ap2Evaluator
+    consts, lay, v0, orc = _setup()
+    B = 8
+    u_refs = np.linspace(5, 8, B)                      # dual_kites_power_curve sweep range
+    Vs = np.stack([batch_member(v0, lay, b) for b in range(B)])
+    Ps = np.stack([pb.pack_p(lay, consts, v0, u_ref=u) for u in u_refs])
+    ev = Ap2Evaluator(consts, batch=B)
+    out = ev.eval_nlp(Vs, Ps)
+    for b in (0, 3, 7):
+        f, g, grad, J = _oracle_all(orc, lay, Vs[b], Ps[b])
+        _close(out["g"][b], g, f"g[{b}]")
+        assert out["f"][b] == pytest.approx(f, rel=1e-12)
+        _close(out["grad_f"][b], grad, f"grad_f[{b}]")
+        _close_jac(ev.jac_csc(out["jac"][b]), J, f"J[{b}]")
+
+
+def test_device_path_value_kernels_and_determinism(gpu):
+    torch = gpu
+    from awebox_amd.evaluator import Ap2Evaluator
+    consts, lay, v0, _ = _setup()
+    B = 4
+    ev = Ap2Evaluator(consts, batch=B)
+    V = torch.tensor(np.stack([batch_member(v0, lay, b) for b in range(B)]), device="cuda")
+    P = torch.tensor(np.stack([pb.pack_p(lay, consts, v0)] * B), device="cuda")
+    f = torch.zeros(B, dtype=torch.float64, device="cuda")
+    g = torch.zeros(B, ev.n_g, dtype=torch.float64, device="cuda")
+    gr = torch.zeros(B, ev.n_v, dtype=torch.float64, device="cuda")
+    jac = torch.zeros(B, ev.nnz, dtype=torch.float64, device="cuda")
+    ev.eval_nlp_device(V, P, f, g, gr, jac)
+    f1, g1, gr1, j1 = f.clone(), g.clone(), gr.clone(), jac.clone()
+    ev.eval_nlp_device(V, P, f, g, gr, jac)
+    torch.cuda.synchronize()
+    assert torch.equal(f, f1) and torch.equal(g, g1) and torch.equal(gr, gr1) and torch.equal(jac, j1)
+    g2 = torch.zeros_like(g)
+    f2 = torch.zeros_like(f)
+    ev.eval_g_device(V, P, g2)
+    ev.eval_f_device(V, P, f2)
+    torch.cuda.synchronize()
+    assert torch.equal(g2, g1) and torch.equal(f2, f1)
+    ms_main, ms_fin = ev.last_kernel_ms()
+    assert ms_main > 0 and ms_fin > 0
+
+
+def test_nonfinite_is_an_evaluation_error(gpu):
+    from awebox_amd.evaluator import Ap2Evaluator, AwegpuError
+    consts, lay, v0, _ = _setup()
+    V = v0.copy()
+    V[lay.x(3)[0:3]] = 0.0                              # |q| = 0 -> division by zero
+    ev = Ap2Evaluator(consts, batch=1)
+    with pytest.raises(AwegpuError, match="non-finite"):
+        ev.eval_nlp(V, pb.pack_p(lay, consts, v0))

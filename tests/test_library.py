@@ -1,0 +1,58 @@
+"""The C-ABI library: builds, loads, exports every symbol of include/awegpu.h, and its CPU-side
+sparsity derivation is a superset of the oracle's non-zero pattern (no compute on a GPU here)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from awebox_amd import problem as pb
+from awebox_amd.build import LIB, build
+from awebox_amd.evaluator import EXPORTED_SYMBOLS, load_library, sparsity_jac_static
+from awebox_amd.initial_guess import batch_member, initial_guess
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "awegpu.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build()
+    return load_library()
+
+
+def test_exports_every_header_symbol(lib):
+    declared = set(re.findall(r"^(?:int|const char\*)\s+(awe_\w+)\(", open(HEADER).read(), re.M))
+    assert declared == set(EXPORTED_SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (awe_\w+)", out))
+    assert declared <= exported
+
+
+@pytest.mark.parametrize("n_k,d", [(40, 4), (5, 3)])
+def test_static_sparsity_covers_oracle_pattern(lib, n_k, d):
+    from oracle.ap2_oracle import from_problem
+    consts = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+    lay = pb.NlpLayout(n_k, d)
+    colind, row = sparsity_jac_static(consts)
+    assert colind[-1] == row.size and np.all(np.diff(colind) >= 0)
+    for c in range(lay.n_v):                       # CCS rows sorted within each column
+        r = row[colind[c]:colind[c + 1]]
+        assert np.all(np.diff(r) > 0)
+    v0 = initial_guess(consts, lay)
+    V = batch_member(v0, lay, 0)
+    P = pb.pack_p(lay, consts, v0)
+    orc = from_problem(consts, n_k=n_k, d=d)
+    J = orc.nlp_jac_g(V, P, lay, pb.THETA0_OFF)
+    pat = sp.csc_matrix((np.ones(row.size), row, colind), shape=J.shape)
+    nz = (J != 0).astype(float)
+    assert (nz - nz.multiply(pat)).nnz == 0, "oracle non-zero outside the evaluator's CCS pattern"
+
+
+def test_no_device_means_no_fallback(lib):
+    from awebox_amd.evaluator import Ap2Evaluator, AwegpuUnavailable
+    if lib.awe_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(AwegpuUnavailable):
+        Ap2Evaluator()

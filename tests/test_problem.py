@@ -1,0 +1,102 @@
+"""Host-side problem description: sizes, header/Python layout contract, derived constants.
+
+Expected values restate the reference formulas (awebox/opts/model_funcs.py).
+"""
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+from awebox_amd import problem as pb
+from awebox_amd.initial_guess import batch_member, initial_guess
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "awegpu.h")
+
+
+def _defines():
+    out = {}
+    for line in open(HEADER):
+        m = re.match(r"#define (AWE_\w+) (\d+)", line)
+        if m:
+            out[m.group(1)] = int(m.group(2))
+    return out
+
+
+def test_sizes_match_survey():
+    lay = pb.NlpLayout(40, 4)
+    assert (lay.n_v, lay.n_g) == (6154, 6103)
+    assert pb.NW == 59 and pb.N_EQ == 24 and pb.N_INEQ == 9
+    assert lay.interval_stride == 153 and lay.rows_per_interval == 152
+
+
+def test_header_layout_contract():
+    d = _defines()
+    assert d["AWE_NW"] == pb.NW and d["AWE_NTHETA0"] == pb.NTHETA0 and d["AWE_NCONST"] == pb.NCONST
+    th = {"AWE_TH_G": "atmosphere.g", "AWE_TH_R": "atmosphere.r", "AWE_TH_T_REF": "atmosphere.t_ref",
+          "AWE_TH_RHO_REF": "atmosphere.rho_ref", "AWE_TH_GAMMA_AIR": "atmosphere.gamma_air",
+          "AWE_TH_Z_REF": "wind.z_ref", "AWE_TH_EXP_REF": "wind.power_wind.exp_ref", "AWE_TH_U_REF": "wind.u_ref",
+          "AWE_TH_KAPPA": "tether.kappa", "AWE_TH_RHO_TETHER": "tether.rho", "AWE_TH_CD_TETHER": "tether.cd",
+          "AWE_TH_FORCE_LIMITS": "model_bounds.tether_force_limits",
+          "AWE_TH_AIRSPEED_LIMITS": "model_bounds.airspeed_limits", "AWE_TH_ROT_ANGLES": "model_bounds.rot_angles",
+          "AWE_TH_KAPPA_R": "kappa_r", "AWE_TH_B_REF": "geometry.b_ref", "AWE_TH_C_REF": "geometry.c_ref",
+          "AWE_TH_S_REF": "geometry.s_ref", "AWE_TH_M_K": "geometry.m_k", "AWE_TH_J": "geometry.j",
+          "AWE_TH_MOMENT_FACTOR": "aero.moment_factor", "AWE_TH_STAB_DERIVS": "aero.stab_derivs"}
+    for macro, name in th.items():
+        assert d[macro] == pb.THETA0_OFF[name][0], macro
+    for macro, val in d.items():
+        if macro.startswith("AWE_C_") and macro not in ("AWE_C_SCALING", "AWE_C_SD_LEN"):
+            assert pb.CONST_NAMES[val] == macro[len("AWE_C_"):].lower(), macro
+    assert d["AWE_C_SCALING"] == pb.CONST_IDX["scaling0"] and d["AWE_C_SD_LEN"] == pb.CONST_IDX["sd_len0"]
+
+
+def test_derived_scaling_constants():
+    c = pb.build_constants()
+    det = c.details
+    # model_funcs.estimate_flight_radius 'centripetal': groundspeed^2 / (acc_max g)
+    assert det["flight_radius"] == pytest.approx(15.0 ** 2 / (12.0 * 9.81), rel=1e-15)
+    # estimate_time_period: 2 pi windings radius / groundspeed; omega = 2 pi / period
+    assert det["t_f_guess"] == pytest.approx(2 * math.pi * det["flight_radius"] / 15.0, rel=1e-15)
+    assert det["omega_guess"] == pytest.approx(2 * math.pi / det["t_f_guess"], rel=1e-15)
+    # wind at 200 sin(45 deg) with the power law (model_funcs.get_u_at_altitude)
+    zz = 200 * math.sin(math.pi / 4)
+    assert det["u_alt"] == pytest.approx(10 * (math.sqrt(zz ** 2 + 1) / 100) ** 0.15, rel=1e-15)
+    # lambda scaling 'average_force' tension / l_t
+    assert det["lambda_scaling"] == pytest.approx((50 + 1800) / 2 / 200, rel=1e-15)
+    s = c.scaling
+    assert np.all(s[0:3] == det["flight_radius"]) and np.all(s[3:6] == 15.0)
+    assert np.all(s[23:26] == s[0:3])       # xdot scaling = scaling of the integral variable
+    assert np.all(s[26:29] == 15.0)
+    assert s[21] == 200.0 and s[22] == pytest.approx(det["u_alt"] / 3)
+    assert s[55] == pytest.approx(1.2)      # u.ddl_t = max(ddl_t bounds)/2
+    assert s[57] == 5e-3 and s[58] == 1.0
+    # power cost = time period estimate (model_funcs.py:1116-1123)
+    assert c.cost_steps["power1"][pb.COST_NAMES.index("power")] == pytest.approx(det["t_f_guess"], rel=1e-12)
+
+
+def test_cost_schedule_and_weights():
+    c = pb.build_constants()
+    cost = dict(zip(pb.COST_NAMES, c.cost_steps["power1"]))
+    assert cost["tracking"] == 1e-3 and cost["psi"] == 1e-3 and cost["gamma"] == 1e-3
+    assert cost["fictitious"] == 1e-3 and cost["beta"] == 1e3 and cost["theta_regularisation"] == 1.0
+    init = dict(zip(pb.COST_NAMES, c.cost_steps["initial0"]))
+    assert init["tracking"] == 1e-1 and init["fictitious"] == 1e3 and init["power"] == 0.0
+    w = c.weights
+    assert w[pb.W_OFF[("x", "q10")][0]] == 1e-1 and w[pb.W_OFF[("xdot", "domega10")][0]] == 5e7
+    assert w[pb.W_OFF[("u", "f_fict10")][0]] == 1.0 and w[pb.W_OFF[("xdot", "dr10")][0]] == 1.0
+
+
+def test_initial_guess_is_a_closed_circular_orbit():
+    c = pb.build_constants()
+    lay = pb.NlpLayout()
+    v0 = initial_guess(c, lay)
+    s = c.scaling
+    q0 = v0[lay.x(0)][0:3] * s[0:3]
+    assert np.linalg.norm(q0) == pytest.approx(200.0, rel=1e-12)        # |q| = l_t
+    qN = v0[lay.x(40)][0:3] * s[0:3]
+    np.testing.assert_allclose(q0, qN, atol=1e-9)                        # one winding
+    R = v0[lay.x(0)][9:18].reshape(3, 3, order="F")
+    np.testing.assert_allclose(R.T @ R, np.eye(3), atol=1e-12)
+    vb = batch_member(v0, lay, 3)
+    assert vb[0] == v0[0] and not np.allclose(vb[20:], v0[20:])
