@@ -24,6 +24,12 @@ for s in $STAGES; do
     prof)  run 600 rocprof.log rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS} ;;
     pmc)   run 600 rocprof_pmc.log rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} && \
            run 600 rocprof_pmc2.log rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} ;;
+    sq)    i=0; IFS=';' read -ra GROUPS_ARR <<< "${PMC_GROUPS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY}"
+           for grp in "${GROUPS_ARR[@]}"; do
+             i=$((i+1))
+             run 600 rocprof_sq$i.log rocprofv3 --pmc $grp -d $OUT/sq$i -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS}
+           done ;;
+    listc) run 120 counters.log rocprofv3 -L ;;
   esac
 done
 echo ALL_DONE
