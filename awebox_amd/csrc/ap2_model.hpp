@@ -47,19 +47,22 @@ struct NodeResult {
 template <class T>
 AWE_HD T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
-// ISA density (atmosphere.py:60-78)
+// ISA density (atmosphere.py:60-78): rho_ref ((T_ref - gamma_air zz) / T_ref)^(g/(gamma_air R) - 1),
+// evaluated as exp(expo log(.)) -- two short transcendental kernels instead of a full pow
 template <class T>
 AWE_HD T isa_density(const T& zz, const double* th) {
-    T t = th[AWE_TH_T_REF] - th[AWE_TH_GAMMA_AIR] * zz;
-    double expo = th[AWE_TH_G] / th[AWE_TH_GAMMA_AIR] / th[AWE_TH_R] - 1.0;
-    return th[AWE_TH_RHO_REF] * pow(t / th[AWE_TH_T_REF], expo);
+    const double expo = th[AWE_TH_G] / th[AWE_TH_GAMMA_AIR] / th[AWE_TH_R] - 1.0;
+    T ratio = 1.0 - zz * (th[AWE_TH_GAMMA_AIR] / th[AWE_TH_T_REF]);
+    return th[AWE_TH_RHO_REF] * exp(expo * log(ratio));
 }
 
-// power-law wind speed with smooth_abs(zz, eps=1) altitude (wind.py:184-208)
+// power-law wind speed u_ref (smooth_abs(zz, eps=1) / z_ref)^c_f (wind.py:184-208), with
+// smooth_abs(zz) = sqrt(zz^2 + 1) folded into the logarithm
 template <class T>
 AWE_HD T wind_speed(const T& zz, const double* th) {
-    T z_cropped = sqrt(zz * zz + 1.0);
-    return th[AWE_TH_U_REF] * pow(z_cropped / th[AWE_TH_Z_REF], th[AWE_TH_EXP_REF]);
+    const double p = th[AWE_TH_EXP_REF];
+    const double scale = th[AWE_TH_U_REF] * ::exp(-p * ::log(th[AWE_TH_Z_REF]));
+    return scale * exp((0.5 * p) * log(zz * zz + 1.0));
 }
 
 // Rows are emitted phase by phase (DCM, trivial, aero -> rotation -> path constraints, tether

@@ -3,20 +3,25 @@
 // Replaces, for the AP2 configuration, the CasADi-expanded SX evaluation that IPOPT calls
 // through nlpsol (awebox/opti/preparation.py:366-400): f, g, grad f and the CCS values of J_g.
 //
-// Execution model (SURVEY.md section 7 step 4):
-//   * one 64-lane wavefront (one workgroup) per shooting interval k of one NLP instance b;
+// Execution model:
+//   * one workgroup per (NLP instance, shooting interval); W = ceil((d+1)/2) wavefronts;
 //   * the interval's slice of V is staged in LDS with coalesced loads;
-//   * the wave walks the interval's d+1 nodes (shooting node + d Radau nodes); at each node every
-//     lane evaluates the hand-written model in forward-mode dual arithmetic along its own
-//     direction, so the 64 lanes together produce the node's Jacobian block in one pass;
-//   * directions are chosen in V-space where that is free: at a collocation node the lane of
-//     state i seeds x_i AND the matching polynomial derivative xdot_i = C[jj,jj]/(h tf), and one
-//     lane seeds the full d/d t_f (t_f and every xdot_i = -xdot_i/t_f), so the chain rule through
-//     the collocation polynomial (collocation.py:202-258) costs no extra pass;
-//   * J values are written straight into their fixed CCS slots (positions derived on the host
-//     from a structural-dependency instantiation of the same model), g rows and the interval's
-//     grad f entries are written directly, and the few global gradient entries are reduced
-//     deterministically by a small finalize kernel (no float atomics).
+//   * model pass: every half-wavefront (32 lanes) evaluates ONE node (the shooting node or one
+//     Radau node) of the hand-written model in forward-mode dual arithmetic.  The node's
+//     Jacobian block is obtained by *compressed* forward mode: the 61 seed directions are
+//     grouped into <= 32 colours whose row sets are disjoint (greedy Curtis-Powell-Reid
+//     colouring computed on the host from the structural dependencies of the same model), so
+//     32 lanes recover the whole block and one wavefront evaluates two nodes at once;
+//   * seed directions live in V-space where that is free: at a Radau node the direction of
+//     state i seeds x_i AND xdot_i = C[jj,jj]/(h tf); the direction of xdot_i feeds the other
+//     d columns of the collocation polynomial; one direction carries d/d t_f of every xdot_i
+//     (collocation.py:202-258).  The chain rule through xdot = C X / (h tf) costs no extra pass;
+//   * scatter pass (one lane per direction): tangents are moved from the compressed LDS buffer
+//     into an LDS image of this interval's part of the CCS value array, and the objective's
+//     directional derivatives are formed (objective.py);
+//   * write-out: the interval's g rows, grad f columns and CCS runs leave LDS as contiguous,
+//     coalesced stores; the few global gradient entries are reduced deterministically by a small
+//     finalize kernel (no float atomics anywhere).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,10 +51,14 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 constexpr int kMaxD = 9;
-constexpr int kLanes = 64;
-constexpr int kTargets = 4;     // max V columns one lane direction feeds at one node
-constexpr int kLaneGamma = 59;  // direction d/d phi.gamma
-constexpr int kLanePsi = 60;    // direction d/d phi.psi (objective only)
+constexpr int kHalf = 32;        // lanes per node in the model pass (compressed directions)
+constexpr int kDirs = 64;        // seed directions (lane = direction in the scatter pass)
+constexpr int kDirZ = 56, kDirDiam = 57, kDirTf = 58, kDirGamma = 59, kDirPsi = 60;
+constexpr int kRowPower = AWE_N_EQ + AWE_N_INEQ;       // 33: power integrand (objective)
+constexpr int kRowBeta = kRowPower + 1;                // 34: side slip (objective)
+constexpr int kGvalStride = 36;
+constexpr unsigned long long kJRows = (1ull << kRowPower) - 1ull;
+constexpr int kSegs = 4;         // CCS runs per interval: local columns, diam_t, t_f, gamma
 constexpr int kPhiGamma = 0, kPhiPsi = 3;
 constexpr int kCostTracking = 0, kCostURegularisation = 1, kCostXdotRegularisation = 2,
               kCostGamma = 3, kCostPsi = 5, kCostFictitious = 10, kCostPower = 11, kCostTf = 13,
@@ -177,77 +186,112 @@ struct Layout {
 const int kPeriodicOrder[AWE_NX] = {18, 19, 20, 22, 3, 4, 5, 21, 6, 7, 8, 0, 1, 2,
                                      9, 10, 11, 12, 13, 14, 15, 16, 17};
 
+
 // ---------------------------------------------------------------------------------------
 // device side
 // ---------------------------------------------------------------------------------------
+
+// Compressed-direction tables (host colouring, see build_tables).  kind 0 = shooting node,
+// kind 1 = Radau node.  Direction numbering (lane of the scatter pass): 0..58 node variables
+// (at a Radau node: 0..22 state x_i with its own xdot_i, 23..45 xdot_i into the other
+// polynomial columns, 58 = t_f through every xdot_i), 59 phi.gamma, 60 phi.psi (objective only).
+struct ColorTabs {
+    unsigned long long seedA[2][kHalf];   // colour seeds node variable i (bit i) / gamma (bit 59)
+    unsigned int seedXD[2][kHalf];        // colour carries the xdot-direction of state i
+    unsigned long long cmask[2][kHalf];   // rows (0..34) the colour produces
+    int off[2][kHalf];                    // colour's first entry in the node's tangent buffer
+    int tf_color[2];
+    unsigned long long dmask[2][kDirs];   // rows of each direction
+    int dcolor[2][kDirs];                 // colour of each direction, -1 if it has no rows
+    int tsize[2];                         // tangent-buffer entries per node
+};
+
 struct KArgs {
     const double* V;
     const double* P;
     const double* cst;
     const DevColl* coll;
-    const int* pos;                    // [n_k][d+1][64][kTargets]
-    const unsigned long long* rowmask; // [d+1][64]
-    const int* cont_pos;               // [n_k][23][2]  (x[k+1] col, coll_x[k][d-1] col)
-    const int* per_pos;                // [23][2]
+    const ColorTabs* ct;
+    const unsigned short* pos;   // [n_k][d+1][64][max(d,1)] LDS index of a direction's first row
+    const int* seg;              // [n_k][kSegs][3] global CCS slot, length, LDS offset
+    const int* cidx_off;         // [n_k + 1] constant-entry ranges
+    const int* cidx;             // LDS index of constant entries (continuity, periodicity)
+    const double* cval;
     double* g;
     double* jac;
     double* grad;
-    double* partial;                   // [batch][n_k][kNPartial]
+    double* partial;             // [batch][n_k][kNPartial]
     double* f;
     int n_k, d, n_v, n_g, n_p, nnz, batch;
     int stride, rows, v_int0;
+    int tang_total, jst_size;
     int want_derivs;
 };
 
+// node variable i of one lane's colour: value from LDS, tangent from the colour's seeds
 struct LaneIn {
-    const double* w;   // LDS: 59 node values (scaled)
-    int lane;
-    int coll;          // 0 shooting node, 1 collocation node
-    double cxx;        // C[jj][jj] / (h tf): xdot_i sensitivity to the node's own state
-    double inv_tf;
+    const double* w;             // LDS: 59 node values (scaled)
+    unsigned long long seedA;
+    unsigned int seedXD;
+    double cxx;                  // C[jj][jj] / (h tf) at a Radau node, 0 at the shooting node
+    double tfs;                  // -1/tf for the t_f colour at a Radau node, else 0
     __device__ __forceinline__ awe::Dual operator()(int i) const {
-        double t = (i == lane) ? 1.0 : 0.0;
-        if (coll) {
-            if (i >= AWE_NX && i < 2 * AWE_NX) {
-                if (lane == i - AWE_NX) t = cxx;
-                if (lane == AWE_NW - 1) t = -w[i] * inv_tf;   // d/d t_f of xdot = C X/(h tf)
-            }
+        double t = ((seedA >> i) & 1ull) ? 1.0 : 0.0;
+        if (i >= AWE_NX && i < 2 * AWE_NX) {
+            const int j = i - AWE_NX;
+            if ((seedA >> j) & 1ull) t += cxx;
+            if ((seedXD >> j) & 1u) t += 1.0;
+            t += tfs * w[i];
         }
         return awe::Dual(w[i], t);
     }
 };
 
-// streams one node's rows: g value (lane r writes row r) and the lane's Jacobian entries
-struct KernelSink {
-    double* g;
-    double* jac;
-    int g_eq0, g_ineq0, lane;
-    bool derivs;
-    unsigned long long m;
-    int p[kTargets];
-    double sc[kTargets];
-    awe::Dual pw, bt;
-    __device__ __forceinline__ void emit(int r, const awe::Dual& v, int g_row) {
-        if (lane == r) g[g_row] = v.v;
-        if (derivs && ((m >> r) & 1ull)) {
-            const int c = __popcll(m & ((1ull << r) - 1ull));
-#pragma unroll
-            for (int t = 0; t < kTargets; ++t)
-                if (p[t] >= 0) jac[p[t] + c] = sc[t] * v.d;
-        }
+// streams one node's rows into the compressed LDS tangent buffer (and values into gval)
+struct NodeSink {
+    double* tp;
+    double* gv;
+    unsigned long long cm;
+    bool c0;
+    __device__ __forceinline__ void emit(int r, const awe::Dual& v) {
+        if (c0) gv[r] = v.v;
+        if ((cm >> r) & 1ull) tp[__popcll(cm & ((1ull << r) - 1ull))] = v.d;
     }
-    __device__ __forceinline__ void eq_row(int r, const awe::Dual& v) { emit(r, v, g_eq0 + r); }
-    __device__ __forceinline__ void ineq_row(int r, const awe::Dual& v) {
-        emit(AWE_N_EQ + r, v, g_ineq0 + r);
-    }
-    __device__ __forceinline__ void power(const awe::Dual& v) { pw = v; }
-    __device__ __forceinline__ void beta(const awe::Dual& v) { bt = v; }
+    __device__ __forceinline__ void eq_row(int r, const awe::Dual& v) { emit(r, v); }
+    __device__ __forceinline__ void ineq_row(int r, const awe::Dual& v) { emit(AWE_N_EQ + r, v); }
+    __device__ __forceinline__ void power(const awe::Dual& v) { emit(kRowPower, v); }
+    __device__ __forceinline__ void beta(const awe::Dual& v) { emit(kRowBeta, v); }
 };
 
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
 template <int D>
-__global__ __launch_bounds__(64) void ap2_interval_kernel(KArgs a) {
+constexpr int waves_for() { return (D + 2) / 2; }
+
+template <int D>
+constexpr int nloc_pad() {
+    return ((9 + AWE_NX + AWE_NU + AWE_NX + AWE_NZ + D * (AWE_NX + AWE_NZ) + AWE_NX) + 1) & ~1;
+}
+
+// LDS layout (doubles): vloc | wn[NN][64] | gval[NN][36] | dfl[NN][64] | fnode[NN pad] |
+//                       tang[tang_total] | jst[jst_size]
+template <int D>
+constexpr int lds_fixed_doubles() {
+    return nloc_pad<D>() + (D + 1) * (64 + kGvalStride + 64) + ((D + 2) & ~1);
+}
+
+template <int D>
+__global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs a) {
     constexpr int NN = D + 1;
-    const int lane = threadIdx.x;
+    constexpr int W = waves_for<D>();
+    constexpr int NT = 64 * W;
+    constexpr int NTG = D > 1 ? D : 1;      // CCS targets per direction
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
     const int k = blockIdx.x % a.n_k;
     const int b = blockIdx.x / a.n_k;
     const double* V = a.V + (size_t)b * a.n_v;
@@ -259,15 +303,25 @@ __global__ __launch_bounds__(64) void ap2_interval_kernel(KArgs a) {
     double* g = a.g + (size_t)b * a.n_g;
     double* jac = a.jac + (size_t)b * a.nnz;
     double* grad = a.grad + (size_t)b * a.n_v;
+    const ColorTabs* ct = a.ct;
+    const double* C = a.coll->C;
 
-    // ---- stage the interval's V slice: [theta, phi, x[k], u, xdot, z, coll..., x[k+1]] ---
-    constexpr int NLOC_MAX = 9 + AWE_NX + AWE_NU + AWE_NX + AWE_NZ + 9 * (AWE_NX + AWE_NZ) + AWE_NX;
-    __shared__ double vloc[NLOC_MAX];
-    __shared__ double wn[AWE_NW];
-    const int nloc_int = a.stride + AWE_NX;
+    extern __shared__ double smem[];
+    double* vloc = smem;
+    double* wn = vloc + nloc_pad<D>();
+    double* gval = wn + NN * 64;
+    double* dfl = gval + NN * kGvalStride;
+    double* fnode = dfl + NN * 64;
+    double* tang = fnode + ((D + 2) & ~1);
+    double* jst = tang + a.tang_total;
+    auto toff = [&](int n) { return n == 0 ? 0 : ct->tsize[0] + (n - 1) * ct->tsize[1]; };
+
+    // ---- phase 0: stage [theta, phi, x[k], u, xdot, z, coll..., x[k+1]]; constant J entries
     const int base = a.v_int0 + k * a.stride;
-    for (int i = lane; i < 9; i += kLanes) vloc[i] = V[i];
-    for (int i = lane; i < nloc_int; i += kLanes) vloc[9 + i] = V[base + i];
+    for (int i = tid; i < 9; i += NT) vloc[i] = V[i];
+    for (int i = tid; i < a.stride + AWE_NX; i += NT) vloc[9 + i] = V[base + i];
+    if (a.want_derivs)
+        for (int e = a.cidx_off[k] + tid; e < a.cidx_off[k + 1]; e += NT) jst[a.cidx[e]] = a.cval[e];
     __syncthreads();
     const double* vt = vloc;                       // theta at 0, phi at 2
     const double* vx = vloc + 9;                   // x[k]
@@ -276,200 +330,228 @@ __global__ __launch_bounds__(64) void ap2_interval_kernel(KArgs a) {
     const double* vz = vxd + AWE_NX;
     const double* vcoll = vz + AWE_NZ;             // coll_var[j] = vcoll + j*24
     const double* vx1 = vcoll + D * (AWE_NX + AWE_NZ);
-
     const double tf = vt[1];
     const double h = 1.0 / a.n_k;
     const double inv_h_tf = 1.0 / h / tf;
-    const double* C = a.coll->C;
+    const double inv_tf = 1.0 / tf;
 
-    awe::Dual gamma(vt[2 + kPhiGamma], lane == kLaneGamma ? 1.0 : 0.0);
-    awe::Dual psi(vt[2 + kPhiPsi], lane == kLanePsi ? 1.0 : 0.0);
-    awe::Dual tfd(tf, lane == AWE_NW - 1 ? 1.0 : 0.0);
+    // node values (scaled, AWE_NW layout); xdot at Radau nodes from the polynomial
+    for (int t = tid; t < NN * 64; t += NT) {
+        const int n = t >> 6, i = t & 63;
+        double val = 0.0;
+        if (i < AWE_NX) {
+            val = n == 0 ? vx[i] : vcoll[(n - 1) * (AWE_NX + AWE_NZ) + i];
+        } else if (i < 2 * AWE_NX) {
+            const int s = i - AWE_NX;
+            if (n == 0) {
+                val = vxd[s];
+            } else {
+                double xp = 0.0;
+#pragma unroll
+                for (int r = 0; r < NN; ++r) {
+                    const double Xr = (r == 0) ? vx[s] : vcoll[(r - 1) * (AWE_NX + AWE_NZ) + s];
+                    xp += C[r * NN + n] * Xr;
+                }
+                val = xp / h / tf;
+            }
+        } else if (i < 2 * AWE_NX + AWE_NU) {
+            val = vu[i - 2 * AWE_NX];
+        } else if (i < 2 * AWE_NX + AWE_NU + AWE_NZ) {
+            val = n == 0 ? vz[0] : vcoll[(n - 1) * (AWE_NX + AWE_NZ) + AWE_NX];
+        } else if (i < AWE_NW) {
+            val = vt[i - (2 * AWE_NX + AWE_NU + AWE_NZ)];
+        }
+        wn[t] = val;
+    }
+    __syncthreads();
 
-    // effective regularisation weights (objective.py:147-170)
+    // ---- phase 1: model, one node per half-wavefront, one colour per lane ------------------
+    {
+        const int n = wave * 2 + (lane >> 5);
+        const int c = lane & (kHalf - 1);
+        if (n < NN) {
+            const int kind = n > 0 ? 1 : 0;
+            LaneIn in;
+            in.w = wn + n * 64;
+            in.seedA = ct->seedA[kind][c];
+            in.seedXD = ct->seedXD[kind][c];
+            in.cxx = n > 0 ? C[n * NN + n] * inv_h_tf : 0.0;
+            in.tfs = (c == ct->tf_color[kind]) ? -inv_tf : 0.0;
+            NodeSink sink;
+            sink.tp = tang + toff(n) + ct->off[kind][c];
+            sink.gv = gval + n * kGvalStride;
+            sink.cm = ct->cmask[kind][c];
+            sink.c0 = c == 0;
+            awe::Dual gamma(vt[2 + kPhiGamma], ((in.seedA >> kDirGamma) & 1ull) ? 1.0 : 0.0);
+            awe::ap2_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0);
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 2: scatter tangents into the CCS image; objective directional derivatives --
+    const double psi = vt[2 + kPhiPsi];
     const double w_track = cost[kCostTracking] / a.cst[AWE_C_NORM_TRACKING];
     const double w_xdot = cost[kCostXdotRegularisation] / a.cst[AWE_C_NORM_XDOT_REG];
     const double w_ureg = cost[kCostURegularisation] / a.cst[AWE_C_NORM_U_REG];
     const double w_fict = cost[kCostFictitious] / a.cst[AWE_C_NORM_FICTITIOUS];
     const double w_theta = cost[kCostThetaRegularisation] / a.cst[AWE_C_NORM_THETA_REG];
-
-    // gradient accumulators (lane = direction)
-    double gx[NN], gxd[NN];
-    for (int r = 0; r < NN; ++r) { gx[r] = 0.0; gxd[r] = 0.0; }
-    double gu = 0.0, gglob = 0.0;
-    double gz[NN];
-    for (int r = 0; r < NN; ++r) gz[r] = 0.0;
-    double fsum = 0.0;
-
-    const unsigned long long* rmask = a.rowmask;
-    const int* pos_k = a.pos + (size_t)k * NN * kLanes * kTargets;
-
-#pragma unroll 1
-    for (int node = 0; node < NN; ++node) {
-        // ---- node variables into LDS --------------------------------------------------
-        __syncthreads();
-        if (node == 0) {
-            if (lane < AWE_NX) wn[lane] = vx[lane];
-            else if (lane < 2 * AWE_NX) wn[lane] = vxd[lane - AWE_NX];
-            else if (lane < 2 * AWE_NX + AWE_NU) wn[lane] = vu[lane - 2 * AWE_NX];
-            else if (lane < 2 * AWE_NX + AWE_NU + AWE_NZ) wn[lane] = vz[0];
-            else if (lane < AWE_NW) wn[lane] = vt[lane - (2 * AWE_NX + AWE_NU + AWE_NZ)];
-        } else {
-            const double* cx = vcoll + (node - 1) * (AWE_NX + AWE_NZ);
-            if (lane < AWE_NX) {
-                wn[lane] = cx[lane];
-            } else if (lane < 2 * AWE_NX) {
-                const int i = lane - AWE_NX;
-                double xp = 0.0;
+    for (int n = wave; n < NN; n += W) {
+        const int kind = n > 0 ? 1 : 0;
+        const int dir = lane;
+        const unsigned long long m = ct->dmask[kind][dir];
+        const int c = ct->dcolor[kind][dir];
+        const unsigned long long cm = c >= 0 ? ct->cmask[kind][c] : 0ull;
+        const double* tp = tang + toff(n) + (c >= 0 ? ct->off[kind][c] : 0);
+        if (a.want_derivs) {
+            const unsigned short* pl = a.pos + (((size_t)k * NN + n) * kDirs + dir) * NTG;
+            const bool xd = n > 0 && dir >= AWE_NX && dir < 2 * AWE_NX;
+            int p[NTG];
+            double sc[NTG];
+            {
+                int t = 0;
 #pragma unroll
-                for (int r = 0; r < NN; ++r) {
-                    const double Xr = (r == 0) ? vx[i] : vcoll[(r - 1) * (AWE_NX + AWE_NZ) + i];
-                    xp += C[r * NN + node] * Xr;
-                }
-                wn[lane] = xp / h / tf;
-            } else if (lane < 2 * AWE_NX + AWE_NU) {
-                wn[lane] = vu[lane - 2 * AWE_NX];
-            } else if (lane < 2 * AWE_NX + AWE_NU + AWE_NZ) {
-                wn[lane] = cx[AWE_NX];
-            } else if (lane < AWE_NW) {
-                wn[lane] = vt[lane - (2 * AWE_NX + AWE_NU + AWE_NZ)];
-            }
-        }
-        __syncthreads();
-
-        LaneIn in{wn, lane, node > 0 ? 1 : 0, C[node * NN + node] * inv_h_tf, 1.0 / tf};
-        KernelSink sink;
-        sink.g = g;
-        sink.jac = jac;
-        sink.lane = lane;
-        sink.derivs = a.want_derivs != 0 && lane <= kLaneGamma;
-        sink.g_eq0 = node == 0 ? k * a.rows : k * a.rows + AWE_N_EQ + AWE_N_INEQ + (node - 1) * AWE_N_EQ;
-        sink.g_ineq0 = k * a.rows + AWE_N_EQ;
-        sink.m = (lane <= kLaneGamma) ? rmask[node * kLanes + lane] : 0ull;
-        {
-            const int* pl = pos_k + ((size_t)node * kLanes + (lane & 63)) * kTargets;
-            const bool xd_lane = node > 0 && lane >= AWE_NX && lane < 2 * AWE_NX;
-            int t = 0;
-#pragma unroll
-            for (int rr = 0; rr < NN; ++rr) {
-                if (xd_lane && rr != node && t < kTargets) {
-                    sink.p[t] = pl[t];
-                    sink.sc[t] = C[rr * NN + node] * inv_h_tf;
+                for (int rr = 0; rr < NN; ++rr) {
+                    if (rr == n || t >= NTG) continue;
+                    p[t] = pl[t];
+                    sc[t] = C[rr * NN + n] * inv_h_tf;
                     ++t;
                 }
+                for (; t < NTG; ++t) { p[t] = 0; sc[t] = 0.0; }
             }
-            if (!xd_lane) {
-                sink.p[0] = pl[0];
-                sink.sc[0] = 1.0;
-                t = 1;
+            if (!xd) p[0] = pl[0];
+            int rank = 0;
+            for (unsigned long long mm = m & kJRows; mm; mm &= mm - 1ull) {
+                const int r = __builtin_ctzll(mm);
+                const double v = tp[__popcll(cm & ((1ull << r) - 1ull))];
+                if (xd) {
+#pragma unroll
+                    for (int t = 0; t < NTG; ++t) jst[p[t] + rank] = sc[t] * v;
+                } else {
+                    jst[p[0] + rank] = v;
+                }
+                ++rank;
             }
-            for (; t < kTargets; ++t) { sink.p[t] = -1; sink.sc[t] = 0.0; }
         }
-        awe::ap2_node<awe::Dual>(in, gamma, th, a.cst, sink, node == 0);
-
-        // ---- objective (collocation nodes only; objective.py:45-544) ----------------------
-        if (node > 0) {
-            const int j = node - 1;
+        if (n > 0) {
+            // objective at Radau node j (objective.py:45-544): w_j [psi tracking + xdot, u,
+            // fictitious and theta regularisation] + beta cost + (1 - psi) power cost
+            const int j = n - 1;
             const double wj = a.coll->w[j];
-            // refs: coll x/z from P.p.ref, xdot ref 0, u ref u[k], theta ref
-            const double* rb = vref + base;  // ref V slice of this interval
+            const double* w = wn + n * 64;
+            const double* rb = vref + base;
             const double* rcx = rb + 2 * AWE_NX + AWE_NU + AWE_NZ + j * (AWE_NX + AWE_NZ);
-            awe::Dual track(0.0), xdreg(0.0), ureg(0.0), fict(0.0), threg(0.0);
-            for (int i = 0; i < AWE_NX; ++i) {
-                awe::Dual dv = in(i) - rcx[i];
-                track += (wts[i] * w_track) * (dv * dv);
-            }
-            {
-                awe::Dual dz = in(2 * AWE_NX + AWE_NU) - rcx[AWE_NX];
-                track += (wts[2 * AWE_NX + AWE_NU] * w_track) * (dz * dz);
-            }
-            for (int i = 0; i < AWE_NX; ++i) {
-                awe::Dual dv = in(AWE_NX + i);
-                xdreg += (wts[AWE_NX + i] * w_xdot) * (dv * dv);
-            }
             const double* ru = rb + AWE_NX;
-            for (int i = 0; i < AWE_NU; ++i) {
-                awe::Dual dv = in(2 * AWE_NX + i) - ru[i];
-                const double wi = wts[2 * AWE_NX + i];
-                if (i < 6) fict += (wi * w_fict) * (dv * dv);
-                else ureg += (wi * w_ureg) * (dv * dv);
+            const double cxx = C[n * NN + n] * inv_h_tf;
+            double trk = 0.0, xdr = 0.0, oth = 0.0, dfd = 0.0;
+            if (dir < AWE_NX) {
+                const double e = w[dir] - rcx[dir], ww = wts[dir] * w_track;
+                const double xdv = w[AWE_NX + dir], wx = wts[AWE_NX + dir] * w_xdot;
+                trk = ww * (e * e);
+                dfd = wj * (psi * (2.0 * ww * e) + cxx * (2.0 * wx * xdv));
+            } else if (dir < 2 * AWE_NX) {
+                const double xdv = w[dir], wx = wts[dir] * w_xdot;
+                xdr = wx * (xdv * xdv);
+                dfd = wj * (2.0 * wx * xdv);
+            } else if (dir < 2 * AWE_NX + AWE_NU) {
+                const int i = dir - 2 * AWE_NX;
+                const double e = w[dir] - ru[i], wu = wts[dir] * (i < 6 ? w_fict : w_ureg);
+                oth = wu * (e * e);
+                dfd = wj * (2.0 * wu * e);
+            } else if (dir == kDirZ) {
+                const double e = w[dir] - rcx[AWE_NX], ww = wts[dir] * w_track;
+                trk = ww * (e * e);
+                dfd = wj * psi * (2.0 * ww * e);
+            } else if (dir == kDirDiam) {
+                const double e = w[dir] - vref[0], wt = wts[dir] * w_theta;
+                oth = wt * (e * e);
+                dfd = wj * (2.0 * wt * e);
             }
-            {
-                awe::Dual dv = in(2 * AWE_NX + AWE_NU + AWE_NZ) - vref[0];
-                threg += (wts[2 * AWE_NX + AWE_NU + AWE_NZ] * w_theta) * (dv * dv);
-            }
-            awe::Dual regs = wj * (psi * track + xdreg + ureg + fict + threg);
-            awe::Dual beta_c = (cost[kCostBeta] * wj / a.cst[AWE_C_NORM_BETA]) * (sink.bt * sink.bt);
-            // power: -c_p * (tf/N) w_j p / tf  (collocation.py:272-316, objective.py:279-298)
-            awe::Dual pw = (-cost[kCostPower]) * ((tfd / (double)a.n_k) * (wj * sink.pw)) / tfd;
-            awe::Dual fn = regs + beta_c + (1.0 - psi) * pw;
-            fsum += fn.v;
-            const double dfn = fn.d;
-            if (lane < AWE_NX) {
-                gx[node] += dfn;
-            } else if (lane < 2 * AWE_NX) {
-#pragma unroll
-                for (int rr = 0; rr < NN; ++rr)
-                    if (rr != node) gxd[rr] += C[rr * NN + node] * inv_h_tf * dfn;
-            } else if (lane < 2 * AWE_NX + AWE_NU) {
-                gu += dfn;
-            } else if (lane == 2 * AWE_NX + AWE_NU) {
-                gz[node] += dfn;
-            } else {
-                gglob += dfn;   // diam_t (57), t_f (58), gamma (59), psi (60)
-            }
+            trk = wave_sum(trk);
+            xdr = wave_sum(xdr);
+            oth = wave_sum(oth);
+            const double bv = gval[n * kGvalStride + kRowBeta];
+            const double pv = gval[n * kGvalStride + kRowPower];
+            const double cb = cost[kCostBeta] * wj / a.cst[AWE_C_NORM_BETA];
+            const double cp = -cost[kCostPower] * wj / (double)a.n_k;   // (-c_p)(tf/N) w_j p / tf
+            if (dir == kDirTf) dfd = -2.0 * wj * xdr * inv_tf;
+            if (dir == kDirPsi) dfd = wj * trk - cp * pv;
+            if ((m >> kRowBeta) & 1ull)
+                dfd += (2.0 * cb * bv) * tp[__popcll(cm & ((1ull << kRowBeta) - 1ull))];
+            if ((m >> kRowPower) & 1ull)
+                dfd += ((1.0 - psi) * cp) * tp[__popcll(cm & ((1ull << kRowPower) - 1ull))];
+            dfl[n * 64 + dir] = dfd;
+            if (dir == 0) fnode[n] = wj * (psi * trk + xdr + oth) + cb * (bv * bv) + (1.0 - psi) * (cp * pv);
         }
     }
+    __syncthreads();
 
-    // ---- continuity rows (collocation.py:319-336) ---------------------------------------
+    // ---- phase 3: write-out ---------------------------------------------------------------
     const DevColl* cc = a.coll;
-    if (lane < AWE_NX) {
-        double xf = 0.0;
+    for (int r = tid; r < a.rows; r += NT) {
+        double val;
+        if (r < AWE_N_EQ + AWE_N_INEQ) {
+            val = gval[r];
+        } else if (r < AWE_N_EQ + AWE_N_INEQ + D * AWE_N_EQ) {
+            const int q = r - (AWE_N_EQ + AWE_N_INEQ);
+            val = gval[(1 + q / AWE_N_EQ) * kGvalStride + q % AWE_N_EQ];
+        } else {
+            // continuity x[k+1] - sum_r D_r X_r (collocation.py:319-336); CasADi drops 0 * X
+            const int i = r - (AWE_N_EQ + AWE_N_INEQ + D * AWE_N_EQ);
+            double xf = 0.0;
 #pragma unroll
-        for (int r = 0; r < NN; ++r) {
-            if (cc->D[r] == 0.0) continue;   // structural zero (CasADi drops 0 * x)
-            const double Xr = (r == 0) ? vx[lane] : vcoll[(r - 1) * (AWE_NX + AWE_NZ) + lane];
-            xf += cc->D[r] * Xr;
+            for (int rr = 0; rr < NN; ++rr) {
+                if (cc->D[rr] == 0.0) continue;
+                const double Xr = (rr == 0) ? vx[i] : vcoll[(rr - 1) * (AWE_NX + AWE_NZ) + i];
+                xf += cc->D[rr] * Xr;
+            }
+            val = vx1[i] - xf;
         }
-        g[k * a.rows + AWE_N_EQ + AWE_N_INEQ + D * AWE_N_EQ + lane] = vx1[lane] - xf;
-        if (a.want_derivs) {
-            const int* cp = a.cont_pos + ((size_t)k * AWE_NX + lane) * 2;
-            jac[cp[0]] = 1.0;
-            jac[cp[1]] = -cc->D[D];
-        }
-    }
-
-    if (!a.want_derivs) {
-        if (lane == 0) a.partial[((size_t)b * a.n_k + k) * kNPartial] = fsum;
-        return;
-    }
-
-    // ---- gradient of the interval's local columns --------------------------------------
-    // X_{k,r} columns: xdot-lane i holds sum over nodes of the polynomial path, x-lane i the
-    // direct path of node r.
-    double gx_from_x[NN];
-#pragma unroll
-    for (int r = 0; r < NN; ++r) gx_from_x[r] = __shfl(gx[r], lane - AWE_NX);
-    if (lane >= AWE_NX && lane < 2 * AWE_NX) {
-        const int i = lane - AWE_NX;
-        grad[base + i] = gxd[0];                                       // x[k]
-#pragma unroll
-        for (int r = 1; r < NN; ++r)
-            grad[base + 2 * AWE_NX + AWE_NU + AWE_NZ + (r - 1) * (AWE_NX + AWE_NZ) + i] = gxd[r] + gx_from_x[r];
-        grad[base + AWE_NX + AWE_NU + i] = 0.0;                         // xdot[k] (shooting)
-    } else if (lane >= 2 * AWE_NX && lane < 2 * AWE_NX + AWE_NU) {
-        grad[base + AWE_NX + (lane - 2 * AWE_NX)] = gu;                 // u[k]
-    } else if (lane == 2 * AWE_NX + AWE_NU) {
-        grad[base + 2 * AWE_NX + AWE_NU] = 0.0;                         // z[k] (shooting)
-#pragma unroll
-        for (int r = 1; r < NN; ++r)
-            grad[base + 2 * AWE_NX + AWE_NU + AWE_NZ + (r - 1) * (AWE_NX + AWE_NZ) + AWE_NX] = gz[r];
+        g[k * a.rows + r] = val;
     }
     double* part = a.partial + ((size_t)b * a.n_k + k) * kNPartial;
-    if (lane == 0) part[0] = fsum;
-    if (lane == AWE_NW - 2) part[1] = gglob;   // diam_t
-    if (lane == AWE_NW - 1) part[2] = gglob;   // t_f
-    if (lane == kLanePsi) part[3] = gglob;     // psi
+    if (tid == 0) {
+        double s = 0.0;
+        for (int n = 1; n < NN; ++n) s += fnode[n];
+        part[0] = s;
+    }
+    if (!a.want_derivs) return;
+    if (tid >= 1 && tid <= 3) {
+        const int dcol = tid == 1 ? kDirDiam : (tid == 2 ? kDirTf : kDirPsi);
+        double s = 0.0;
+        for (int n = 1; n < NN; ++n) s += dfl[n * 64 + dcol];
+        part[tid] = s;
+    }
+    // gradient of the interval's local columns: x[k], u[k], xdot[k], z[k], coll_var[k]
+    for (int col = tid; col < a.stride; col += NT) {
+        double gsum = 0.0;
+        if (col < AWE_NX) {                                   // x[k]: polynomial path only
+#pragma unroll
+            for (int n = 1; n < NN; ++n) gsum += C[n] * inv_h_tf * dfl[n * 64 + AWE_NX + col];
+        } else if (col < AWE_NX + AWE_NU) {                   // u[k] (zero-order hold)
+            const int i = col - AWE_NX;
+#pragma unroll
+            for (int n = 1; n < NN; ++n) gsum += dfl[n * 64 + 2 * AWE_NX + i];
+        } else if (col >= 2 * AWE_NX + AWE_NU + AWE_NZ) {     // coll_var[k][j]
+            const int q = col - (2 * AWE_NX + AWE_NU + AWE_NZ);
+            const int r = 1 + q / (AWE_NX + AWE_NZ), e = q % (AWE_NX + AWE_NZ);
+            if (e < AWE_NX) {
+                gsum = dfl[r * 64 + e];
+#pragma unroll
+                for (int n = 1; n < NN; ++n)
+                    if (n != r) gsum += C[r * NN + n] * inv_h_tf * dfl[n * 64 + AWE_NX + e];
+            } else {
+                gsum = dfl[r * 64 + kDirZ];
+            }
+        }                                                     // xdot[k], z[k]: 0
+        grad[base + col] = gsum;
+    }
+    // the interval's CCS runs, contiguous in the value array
+    const int* sg = a.seg + (size_t)k * kSegs * 3;
+#pragma unroll
+    for (int s = 0; s < kSegs; ++s) {
+        const int g0 = sg[3 * s], len = sg[3 * s + 1], lo = sg[3 * s + 2];
+        for (int i = tid; i < len; i += NT) jac[g0 + i] = jst[lo + i];
+    }
 }
 
 // one wave per instance: reduce interval partials, add global costs, periodic rows
@@ -481,36 +563,30 @@ __global__ __launch_bounds__(64) void ap2_finalize_kernel(KArgs a) {
     const double* cost = P + a.n_v + AWE_NW;
     const double* vref = P;
     double* g = a.g + (size_t)b * a.n_g;
-    double* jac = a.jac + (size_t)b * a.nnz;
     double* grad = a.grad + (size_t)b * a.n_v;
     const double* part = a.partial + (size_t)b * a.n_k * kNPartial;
 
     double s[kNPartial] = {0.0, 0.0, 0.0, 0.0};
-    for (int k = lane; k < a.n_k; k += kLanes)
+    for (int k = lane; k < a.n_k; k += 64)
         for (int c = 0; c < kNPartial; ++c) s[c] += part[k * kNPartial + c];
     for (int off = 32; off > 0; off >>= 1)
         for (int c = 0; c < kNPartial; ++c) s[c] += __shfl_xor(s[c], off);
 
     const double tf = V[1], tf_ref = vref[1];
-    // periodic rows: x_0 - x_terminal in sorted-name order
+    // periodic rows: x_0 - x_terminal in sorted-name order (operation.py:245-266); their J
+    // entries are constants written by the interval kernel
     const int last = a.v_int0 + (a.n_k - 1) * a.stride + 2 * AWE_NX + AWE_NU + AWE_NZ +
                      (a.d - 1) * (AWE_NX + AWE_NZ);
     if (lane < AWE_NX) {
         const int i = kPeriodicOrder[lane];
         g[a.n_k * a.rows + lane] = V[a.v_int0 + i] - V[last + i];
-        if (a.want_derivs) {
-            jac[a.per_pos[lane * 2 + 0]] = 1.0;
-            jac[a.per_pos[lane * 2 + 1]] = -1.0;
-        }
     }
+    // phi order gamma, tau, iota, psi, eta, nu, upsilon (system.py:435-450); cost order
+    // gamma, iota, psi, tau, eta, nu, upsilon (discretization.py:129-152)
+    constexpr int phi_cost_map[AWE_NPHI] = {3, 6, 4, 5, 7, 8, 9};
     if (lane == 0) {
         double fh = 0.0;
-        for (int i = 0; i < AWE_NPHI; ++i) {
-            // phi order gamma, tau, iota, psi, eta, nu, upsilon (system.py:435-450); cost
-            // order gamma, iota, psi, tau, eta, nu, upsilon (discretization.py:129-152)
-            static const int phi_cost_map[AWE_NPHI] = {3, 6, 4, 5, 7, 8, 9};
-            fh += cost[phi_cost_map[i]] * V[AWE_NTH + i];
-        }
+        for (int i = 0; i < AWE_NPHI; ++i) fh += cost[phi_cost_map[i]] * V[AWE_NTH + i];
         const double time_cost = cost[kCostTf] * (tf - tf_ref) * (tf - tf_ref);
         a.f[b] = s[0] + time_cost + fh;
     }
@@ -518,7 +594,6 @@ __global__ __launch_bounds__(64) void ap2_finalize_kernel(KArgs a) {
         if (lane == 0) grad[0] = s[1];
         if (lane == 1) grad[1] = s[2] + cost[kCostTf] * 2.0 * (tf - tf_ref);
         if (lane >= 2 && lane < 2 + AWE_NPHI) {
-            static const int phi_cost_map[AWE_NPHI] = {3, 6, 4, 5, 7, 8, 9};
             const int i = lane - 2;
             double gphi = cost[phi_cost_map[i]];
             if (i == kPhiPsi) gphi += s[3];
@@ -541,13 +616,17 @@ struct awe_handle_s {
     std::vector<double> cst;
     std::vector<int> colind, row;
     int nnz = 0;
+    int tang_total = 0, jst_size = 0;
+    size_t lds_bytes = 0;
     // device
     double* d_cst = nullptr;
     DevColl* d_coll = nullptr;
-    int* d_pos = nullptr;
-    unsigned long long* d_rowmask = nullptr;
-    int* d_cont = nullptr;
-    int* d_per = nullptr;
+    ColorTabs* d_ct = nullptr;
+    unsigned short* d_pos = nullptr;
+    int* d_seg = nullptr;
+    int* d_cidx_off = nullptr;
+    int* d_cidx = nullptr;
+    double* d_cval = nullptr;
     double* d_partial = nullptr;
     // scratch for value-only calls and host wrappers
     double* d_scr_jac = nullptr;
@@ -567,53 +646,76 @@ struct DepIn {
     __host__ awe::Dep operator()(int i) const { return awe::Dep::bit(i); }
 };
 
-void model_masks(const double* cst, unsigned long long eqm[AWE_N_EQ], unsigned long long ineqm[AWE_N_INEQ]) {
+struct ModelMasks {
+    unsigned long long eq[AWE_N_EQ], ineq[AWE_N_INEQ], pw, bt;
+};
+
+void model_masks(const double* cst, ModelMasks& mm) {
     std::vector<double> th(AWE_NTHETA0, 1.0);   // values are irrelevant for the structure
     DepIn in;
     awe::NodeResult<awe::Dep> res;
-    awe::ap2_node<awe::Dep>(in, awe::Dep::bit(kLaneGamma), th.data(), cst, res, true);
-    for (int r = 0; r < AWE_N_EQ; ++r) eqm[r] = res.eq[r].m;
-    for (int r = 0; r < AWE_N_INEQ; ++r) ineqm[r] = res.ineq[r].m;
+    awe::ap2_node<awe::Dep>(in, awe::Dep::bit(kDirGamma), th.data(), cst, res, true);
+    for (int r = 0; r < AWE_N_EQ; ++r) mm.eq[r] = res.eq[r].m;
+    for (int r = 0; r < AWE_N_INEQ; ++r) mm.ineq[r] = res.ineq[r].m;
+    mm.pw = res.pw.m;
+    mm.bt = res.bt.m;
+}
+
+template <int D>
+int launch_interval(awe_handle h, const KArgs& a, hipStream_t stream) {
+    constexpr int W = waves_for<D>();
+    hipLaunchKernelGGL(ap2_interval_kernel<D>, dim3(h->batch * h->n_k), dim3(64 * W), h->lds_bytes,
+                       stream, a);
+    return AWE_OK;
 }
 
 int launch(awe_handle h, const double* V, const double* P, double* f, double* g, double* grad,
            double* jac, int want_derivs, hipStream_t stream) {
     KArgs a{};
-    a.V = V; a.P = P; a.cst = h->d_cst; a.coll = h->d_coll; a.pos = h->d_pos;
-    a.rowmask = h->d_rowmask; a.cont_pos = h->d_cont; a.per_pos = h->d_per;
+    a.V = V; a.P = P; a.cst = h->d_cst; a.coll = h->d_coll; a.ct = h->d_ct; a.pos = h->d_pos;
+    a.seg = h->d_seg; a.cidx_off = h->d_cidx_off; a.cidx = h->d_cidx; a.cval = h->d_cval;
     a.g = g; a.jac = jac; a.grad = grad; a.partial = h->d_partial; a.f = f;
     a.n_k = h->n_k; a.d = h->d; a.n_v = h->lay.n_v; a.n_g = h->lay.n_g; a.n_p = h->lay.n_p;
     a.nnz = h->nnz; a.batch = h->batch; a.stride = h->lay.stride; a.rows = h->lay.rows;
-    a.v_int0 = h->lay.v_int0; a.want_derivs = want_derivs;
-    dim3 grid(h->batch * h->n_k), block(kLanes);
+    a.v_int0 = h->lay.v_int0; a.tang_total = h->tang_total; a.jst_size = h->jst_size;
+    a.want_derivs = want_derivs;
     HIP_TRY(hipEventRecord(h->ev[0], stream));
     switch (h->d) {
-        case 1: hipLaunchKernelGGL(ap2_interval_kernel<1>, grid, block, 0, stream, a); break;
-        case 2: hipLaunchKernelGGL(ap2_interval_kernel<2>, grid, block, 0, stream, a); break;
-        case 3: hipLaunchKernelGGL(ap2_interval_kernel<3>, grid, block, 0, stream, a); break;
-        case 4: hipLaunchKernelGGL(ap2_interval_kernel<4>, grid, block, 0, stream, a); break;
-        case 5: hipLaunchKernelGGL(ap2_interval_kernel<5>, grid, block, 0, stream, a); break;
+        case 1: launch_interval<1>(h, a, stream); break;
+        case 2: launch_interval<2>(h, a, stream); break;
+        case 3: launch_interval<3>(h, a, stream); break;
+        case 4: launch_interval<4>(h, a, stream); break;
+        case 5: launch_interval<5>(h, a, stream); break;
         default: return fail(AWE_ERR_ARG, "unsupported collocation degree");
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev[1], stream));
-    hipLaunchKernelGGL(ap2_finalize_kernel, dim3(h->batch), block, 0, stream, a);
+    hipLaunchKernelGGL(ap2_finalize_kernel, dim3(h->batch), dim3(64), 0, stream, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev[2], stream));
     h->timed = true;
     return AWE_OK;
 }
 
-}  // namespace
+size_t lds_fixed_bytes(int d) {
+    switch (d) {
+        case 1: return sizeof(double) * lds_fixed_doubles<1>();
+        case 2: return sizeof(double) * lds_fixed_doubles<2>();
+        case 3: return sizeof(double) * lds_fixed_doubles<3>();
+        case 4: return sizeof(double) * lds_fixed_doubles<4>();
+        default: return sizeof(double) * lds_fixed_doubles<5>();
+    }
+}
 
-namespace {
 struct HostTables {
-    std::vector<int> pos, cont, per;
-    std::vector<unsigned long long> rowmask;
+    ColorTabs ct{};
+    std::vector<unsigned short> pos;
+    std::vector<int> seg, cidx_off, cidx;
+    std::vector<double> cval;
 };
 
-// CPU-only: collocation coefficients, structural masks of the node model, the CCS pattern of
-// J_g and the kernel's slot tables.
+// CPU-only: collocation coefficients, structural masks of the node model, the colouring of the
+// seed directions, the CCS pattern of J_g and the kernel's LDS/CCS index tables.
 int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_consts, HostTables& T) {
     h->n_k = n_k; h->d = d;
     h->lay = Layout(n_k, d);
@@ -622,69 +724,112 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
     const Layout& L = h->lay;
     const Coll& cl = h->coll;
     const int NN = d + 1;
+    const int NTG = d > 1 ? d : 1;
 
-    // ---- structural masks of the node model --------------------------------------------
-    unsigned long long eqm[AWE_N_EQ], ineqm[AWE_N_INEQ];
-    model_masks(h->cst.data(), eqm, ineqm);
-    auto rows_on = [&](int var, bool with_ineq) {   // bitmask of rows depending on node var
+    // ---- direction row masks ------------------------------------------------------------
+    ModelMasks mm;
+    model_masks(h->cst.data(), mm);
+    auto rows_of = [&](int var, int kind) {
         unsigned long long m = 0;
-        for (int r = 0; r < AWE_N_EQ; ++r) if ((eqm[r] >> var) & 1ull) m |= 1ull << r;
-        if (with_ineq)
-            for (int r = 0; r < AWE_N_INEQ; ++r) if ((ineqm[r] >> var) & 1ull) m |= 1ull << (AWE_N_EQ + r);
+        for (int r = 0; r < AWE_N_EQ; ++r) if ((mm.eq[r] >> var) & 1ull) m |= 1ull << r;
+        if (kind == 0) {
+            for (int r = 0; r < AWE_N_INEQ; ++r)
+                if ((mm.ineq[r] >> var) & 1ull) m |= 1ull << (AWE_N_EQ + r);
+        } else {
+            if ((mm.pw >> var) & 1ull) m |= 1ull << kRowPower;
+            if ((mm.bt >> var) & 1ull) m |= 1ull << kRowBeta;
+        }
         return m;
     };
-    // lane row masks: [node][lane]
-    std::vector<unsigned long long> rowmask((size_t)NN * kLanes, 0ull);
-    for (int lane = 0; lane <= kLaneGamma; ++lane) rowmask[lane] = rows_on(lane, true);
-    for (int node = 1; node < NN; ++node) {
-        for (int lane = 0; lane <= kLaneGamma; ++lane) {
-            unsigned long long m = rows_on(lane, false);
-            if (lane < AWE_NX) m |= rows_on(AWE_NX + lane, false);
-            if (lane == AWE_NW - 1)
-                for (int i = 0; i < AWE_NX; ++i) m |= rows_on(AWE_NX + i, false);
-            rowmask[(size_t)node * kLanes + lane] = m;
-        }
+    ColorTabs& ct = T.ct;
+    std::memset(&ct, 0, sizeof(ct));
+    for (int dir = 0; dir <= kDirGamma; ++dir) ct.dmask[0][dir] = rows_of(dir, 0);
+    for (int dir = 0; dir <= kDirGamma; ++dir) {
+        unsigned long long m = rows_of(dir, 1);
+        if (dir < AWE_NX) m |= rows_of(AWE_NX + dir, 1);
+        if (dir == kDirTf)
+            for (int i = 0; i < AWE_NX; ++i) m |= rows_of(AWE_NX + i, 1);
+        ct.dmask[1][dir] = m;
     }
 
-    // ---- target columns of each (k, node, lane) -----------------------------------------
-    auto lane_col_shoot = [&](int k, int lane) -> int {
-        if (lane < AWE_NX) return L.x(k, lane);
-        if (lane < 2 * AWE_NX) return L.xdot(k, lane - AWE_NX);
-        if (lane < 2 * AWE_NX + AWE_NU) return L.u(k, lane - 2 * AWE_NX);
-        if (lane < 2 * AWE_NX + AWE_NU + AWE_NZ) return L.z(k);
-        if (lane < AWE_NW) return L.theta(lane - (2 * AWE_NX + AWE_NU + AWE_NZ));
-        return L.phi(kPhiGamma);
-    };
-    auto lane_cols_coll = [&](int k, int node, int lane, std::vector<int>& cols) {
+    // ---- greedy colouring: directions with disjoint row sets share a lane ----------------
+    for (int kind = 0; kind < 2; ++kind) {
+        std::vector<int> order;
+        for (int dir = 0; dir < kDirs; ++dir) {
+            ct.dcolor[kind][dir] = -1;
+            if (ct.dmask[kind][dir]) order.push_back(dir);
+        }
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+            return __builtin_popcountll(ct.dmask[kind][x]) > __builtin_popcountll(ct.dmask[kind][y]);
+        });
+        std::vector<unsigned long long> cm;
+        for (int dir : order) {
+            const unsigned long long m = ct.dmask[kind][dir];
+            size_t c = 0;
+            while (c < cm.size() && (cm[c] & m)) ++c;
+            if (c == cm.size()) cm.push_back(0ull);
+            cm[c] |= m;
+            ct.dcolor[kind][dir] = (int)c;
+        }
+        if (cm.size() > (size_t)kHalf) return fail(AWE_ERR_ARG, "internal: more than 32 colours");
+        ct.tf_color[kind] = -1;
+        int off = 0;
+        for (int c = 0; c < kHalf; ++c) {
+            ct.cmask[kind][c] = c < (int)cm.size() ? cm[c] : 0ull;
+            ct.off[kind][c] = off;
+            off += __builtin_popcountll(ct.cmask[kind][c]);
+        }
+        ct.tsize[kind] = off;
+        for (int dir = 0; dir < kDirs; ++dir) {
+            const int c = ct.dcolor[kind][dir];
+            if (c < 0) continue;
+            if (kind == 1 && dir >= AWE_NX && dir < 2 * AWE_NX) {
+                ct.seedXD[kind][c] |= 1u << (dir - AWE_NX);
+            } else {
+                ct.seedA[kind][c] |= 1ull << dir;
+                if (kind == 1 && dir == kDirTf) ct.tf_color[kind] = c;
+            }
+        }
+    }
+    h->tang_total = ct.tsize[0] + d * ct.tsize[1];
+
+    // ---- target columns of each (k, node, direction) ------------------------------------
+    auto dir_cols = [&](int k, int node, int dir, std::vector<int>& cols) {
         cols.clear();
-        if (lane < AWE_NX) { cols.push_back(L.coll_x(k, node - 1, lane)); return; }
-        if (lane < 2 * AWE_NX) {
-            for (int r = 0; r < NN; ++r) if (r != node) cols.push_back(L.X(k, r, lane - AWE_NX));
+        if (dir == kDirGamma) { cols.push_back(L.phi(kPhiGamma)); return; }
+        if (dir >= 2 * AWE_NX + AWE_NU + AWE_NZ) {
+            cols.push_back(L.theta(dir - (2 * AWE_NX + AWE_NU + AWE_NZ)));
             return;
         }
-        if (lane < 2 * AWE_NX + AWE_NU) { cols.push_back(L.u(k, lane - 2 * AWE_NX)); return; }
-        if (lane < 2 * AWE_NX + AWE_NU + AWE_NZ) { cols.push_back(L.coll_z(k, node - 1)); return; }
-        if (lane < AWE_NW) { cols.push_back(L.theta(lane - (2 * AWE_NX + AWE_NU + AWE_NZ))); return; }
-        cols.push_back(L.phi(kPhiGamma));
+        if (dir >= 2 * AWE_NX && dir < 2 * AWE_NX + AWE_NU) { cols.push_back(L.u(k, dir - 2 * AWE_NX)); return; }
+        if (node == 0) {
+            if (dir < AWE_NX) cols.push_back(L.x(k, dir));
+            else if (dir < 2 * AWE_NX) cols.push_back(L.xdot(k, dir - AWE_NX));
+            else cols.push_back(L.z(k));
+            return;
+        }
+        if (dir < AWE_NX) { cols.push_back(L.coll_x(k, node - 1, dir)); return; }
+        if (dir < 2 * AWE_NX) {
+            for (int r = 0; r < NN; ++r) if (r != node) cols.push_back(L.X(k, r, dir - AWE_NX));
+            return;
+        }
+        cols.push_back(L.coll_z(k, node - 1));
     };
+    auto node_row0 = [&](int k, int node) { return node == 0 ? L.g_shoot(k) : L.g_coll(k, node - 1); };
 
     // ---- triplets -----------------------------------------------------------------------
     std::vector<std::pair<int, int>> trip;   // (col, row)
     trip.reserve(200000);
     std::vector<int> cols;
     for (int k = 0; k < n_k; ++k) {
-        for (int lane = 0; lane <= kLaneGamma; ++lane) {
-            unsigned long long m = rowmask[lane];
-            for (int r = 0; r < AWE_N_EQ + AWE_N_INEQ; ++r)
-                if ((m >> r) & 1ull) trip.emplace_back(lane_col_shoot(k, lane), L.g_shoot(k) + r);
-        }
-        for (int node = 1; node < NN; ++node)
-            for (int lane = 0; lane <= kLaneGamma; ++lane) {
-                unsigned long long m = rowmask[(size_t)node * kLanes + lane];
-                lane_cols_coll(k, node, lane, cols);
+        for (int node = 0; node < NN; ++node)
+            for (int dir = 0; dir < kDirs; ++dir) {
+                const unsigned long long m = ct.dmask[node > 0][dir] & kJRows;
+                if (!m) continue;
+                dir_cols(k, node, dir, cols);
                 for (int c : cols)
-                    for (int r = 0; r < AWE_N_EQ; ++r)
-                        if ((m >> r) & 1ull) trip.emplace_back(c, L.g_coll(k, node - 1) + r);
+                    for (int r = 0; r < kRowPower; ++r)
+                        if ((m >> r) & 1ull) trip.emplace_back(c, node_row0(k, node) + r);
             }
         for (int i = 0; i < AWE_NX; ++i) {
             trip.emplace_back(L.x(k + 1, i), L.g_cont(k) + i);
@@ -714,52 +859,109 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
         return (int)(it - h->row.begin());
     };
 
-    // ---- kernel position tables ---------------------------------------------------------
-    std::vector<int> pos((size_t)n_k * NN * kLanes * kTargets, -1);
+    // ---- per-interval CCS runs and their LDS image ---------------------------------------
+    // run 0: every entry of the interval's own columns x[k] .. coll_var[k] (the last interval
+    // also owns the terminal x[n_k] columns); runs 1-3: the interval's rows of the global
+    // columns diam_t, t_f and phi.gamma
+    std::vector<int> seg((size_t)n_k * kSegs * 3, 0);
+    int jst_max = 0;
+    const int gcols[kSegs - 1] = {L.theta(0), L.theta(1), L.phi(kPhiGamma)};
+    for (int k = 0; k < n_k; ++k) {
+        int* s = &seg[(size_t)k * kSegs * 3];
+        const int lo = h->colind[L.x(k, 0)];
+        const int hi = (k == n_k - 1) ? h->nnz : h->colind[L.x(k + 1, 0)];
+        s[0] = lo; s[1] = hi - lo; s[2] = 0;
+        int off = hi - lo;
+        for (int q = 0; q < kSegs - 1; ++q) {
+            const int col = gcols[q];
+            auto b = h->row.begin() + h->colind[col], e = h->row.begin() + h->colind[col + 1];
+            const int a0 = (int)(std::lower_bound(b, e, k * L.rows) - h->row.begin());
+            const int a1 = (int)(std::lower_bound(b, e, (k + 1) * L.rows) - h->row.begin());
+            s[3 * (q + 1)] = a0; s[3 * (q + 1) + 1] = a1 - a0; s[3 * (q + 1) + 2] = off;
+            off += a1 - a0;
+        }
+        jst_max = std::max(jst_max, off);
+    }
+    h->jst_size = jst_max;
+    auto lds_of = [&](int k, int slot) -> int {
+        const int* s = &seg[(size_t)k * kSegs * 3];
+        for (int q = 0; q < kSegs; ++q)
+            if (slot >= s[3 * q] && slot < s[3 * q] + s[3 * q + 1]) return s[3 * q + 2] + slot - s[3 * q];
+        return -1;
+    };
     int bad = 0;
+    {   // every CCS slot belongs to exactly one interval run
+        std::vector<int> cover(h->nnz, 0);
+        for (int k = 0; k < n_k; ++k)
+            for (int q = 0; q < kSegs; ++q) {
+                const int* s = &seg[((size_t)k * kSegs + q) * 3];
+                for (int i = 0; i < s[1]; ++i) cover[s[0] + i]++;
+            }
+        for (int i = 0; i < h->nnz; ++i) if (cover[i] != 1) ++bad;
+    }
+
+    // ---- LDS index of each direction's first row in each target column -------------------
+    std::vector<unsigned short> pos((size_t)n_k * NN * kDirs * NTG, 0xffff);
+    std::vector<std::vector<int>> written(n_k);
+    for (int k = 0; k < n_k; ++k) written[k].assign(jst_max, 0);
     for (int k = 0; k < n_k; ++k)
         for (int node = 0; node < NN; ++node)
-            for (int lane = 0; lane <= kLaneGamma; ++lane) {
-                unsigned long long m = rowmask[(size_t)node * kLanes + lane];
+            for (int dir = 0; dir < kDirs; ++dir) {
+                const unsigned long long m = ct.dmask[node > 0][dir] & kJRows;
                 if (!m) continue;
-                if (node == 0) cols.assign(1, lane_col_shoot(k, lane));
-                else lane_cols_coll(k, node, lane, cols);
-                const int g0 = node == 0 ? L.g_shoot(k) : L.g_coll(k, node - 1);
-                const int first = __builtin_ctzll(m);
+                dir_cols(k, node, dir, cols);
+                const int g0 = node_row0(k, node);
                 for (size_t t = 0; t < cols.size(); ++t) {
-                    int p = find(cols[t], g0 + first);
-                    // the node's rows must be consecutive entries of the column
-                    int cnt = 0;
-                    for (int r = 0; r < 64; ++r)
+                    const int p = lds_of(k, find(cols[t], g0 + __builtin_ctzll(m)));
+                    if (p < 0) { ++bad; continue; }
+                    int cnt = 0;   // the node's rows must be consecutive entries of the column
+                    for (int r = 0; r < kRowPower; ++r)
                         if ((m >> r) & 1ull) {
-                            if (find(cols[t], g0 + r) != p + cnt) ++bad;
+                            const int q = lds_of(k, find(cols[t], g0 + r));
+                            if (q != p + cnt) ++bad; else written[k][q]++;
                             ++cnt;
                         }
-                    pos[(((size_t)k * NN + node) * kLanes + lane) * kTargets + t] = p;
+                    pos[(((size_t)k * NN + node) * kDirs + dir) * NTG + t] = (unsigned short)p;
                 }
             }
-    std::vector<int> cont((size_t)n_k * AWE_NX * 2, -1);
+    // ---- constant entries: continuity (+1, -D_r) and periodicity (+1, -1) ------------------
+    std::vector<std::vector<std::pair<int, double>>> cent(n_k);
+    auto add_const = [&](int col, int rw, double val) {
+        const int slot = find(col, rw);
+        for (int k = 0; k < n_k; ++k) {
+            const int q = lds_of(k, slot);
+            if (q >= 0) { cent[k].emplace_back(q, val); written[k][q]++; return; }
+        }
+        ++bad;
+    };
     for (int k = 0; k < n_k; ++k)
         for (int i = 0; i < AWE_NX; ++i) {
-            cont[((size_t)k * AWE_NX + i) * 2 + 0] = find(L.x(k + 1, i), L.g_cont(k) + i);
-            cont[((size_t)k * AWE_NX + i) * 2 + 1] = find(L.X(k, d, i), L.g_cont(k) + i);
+            add_const(L.x(k + 1, i), L.g_cont(k) + i, 1.0);
+            for (int r = 0; r < NN; ++r)
+                if (cl.D[r] != 0.0) add_const(L.X(k, r, i), L.g_cont(k) + i, -cl.D[r]);
         }
-    std::vector<int> per(AWE_NX * 2);
     for (int i = 0; i < AWE_NX; ++i) {
-        per[i * 2 + 0] = find(L.x(0, kPeriodicOrder[i]), L.g_periodic() + i);
-        per[i * 2 + 1] = find(last + kPeriodicOrder[i], L.g_periodic() + i);
+        add_const(L.x(0, kPeriodicOrder[i]), L.g_periodic() + i, 1.0);
+        add_const(last + kPeriodicOrder[i], L.g_periodic() + i, -1.0);
     }
-    for (int c = 0; c < (int)cont.size(); ++c) if (cont[c] < 0) ++bad;
-    for (int c = 0; c < (int)per.size(); ++c) if (per[c] < 0) ++bad;
-    for (int r = 0; r < NN; ++r)
-        if (r < d && cl.D[r] != 0.0) ++bad;   // the kernel assumes D = e_d (Radau)
+    // every slot of every interval image is written exactly once
+    for (int k = 0; k < n_k; ++k) {
+        const int* s = &seg[(size_t)k * kSegs * 3];
+        int total = 0;
+        for (int q = 0; q < kSegs; ++q) total += s[3 * q + 1];
+        for (int i = 0; i < jst_max; ++i) if (written[k][i] != (i < total ? 1 : 0)) ++bad;
+    }
     if (bad) return fail(AWE_ERR_ARG, "internal: inconsistent sparsity tables");
+    T.cidx_off.assign(n_k + 1, 0);
+    for (int k = 0; k < n_k; ++k) {
+        T.cidx_off[k + 1] = T.cidx_off[k] + (int)cent[k].size();
+        for (auto& e : cent[k]) { T.cidx.push_back(e.first); T.cval.push_back(e.second); }
+    }
     T.pos.swap(pos);
-    T.rowmask.swap(rowmask);
-    T.cont.swap(cont);
-    T.per.swap(per);
+    T.seg.swap(seg);
+    h->lds_bytes = lds_fixed_bytes(d) + sizeof(double) * (size_t)(h->tang_total + h->jst_size);
+    if (h->lds_bytes > 65536) return fail(AWE_ERR_ARG, "internal: LDS image exceeds 64 KiB");
     return AWE_OK;
-
 }
 }  // namespace
 
@@ -789,10 +991,6 @@ int awe_create(int n_k, int d, const double* consts, int n_consts, int batch, aw
     if (rc) { delete h; return rc; }
     const Coll& cl = h->coll;
     const int NN = d + 1;
-    std::vector<int>& pos = T.pos;
-    std::vector<unsigned long long>& rowmask = T.rowmask;
-    std::vector<int>& cont = T.cont;
-    std::vector<int>& per = T.per;
     DevColl dc{};
     for (int j = 0; j < NN; ++j)
         for (int r = 0; r < NN; ++r) dc.C[j * NN + r] = cl.C[j][r];
@@ -804,10 +1002,12 @@ int awe_create(int n_k, int d, const double* consts, int n_consts, int batch, aw
     HIP_TRY(hipMemcpy(dst, src, sizeof(*dst) * (n), hipMemcpyHostToDevice))
     ALLOC_COPY(h->d_cst, h->cst.data(), h->cst.size());
     ALLOC_COPY(h->d_coll, &dc, 1);
-    ALLOC_COPY(h->d_pos, pos.data(), pos.size());
-    ALLOC_COPY(h->d_rowmask, rowmask.data(), rowmask.size());
-    ALLOC_COPY(h->d_cont, cont.data(), cont.size());
-    ALLOC_COPY(h->d_per, per.data(), per.size());
+    ALLOC_COPY(h->d_ct, &T.ct, 1);
+    ALLOC_COPY(h->d_pos, T.pos.data(), T.pos.size());
+    ALLOC_COPY(h->d_seg, T.seg.data(), T.seg.size());
+    ALLOC_COPY(h->d_cidx_off, T.cidx_off.data(), T.cidx_off.size());
+    ALLOC_COPY(h->d_cidx, T.cidx.data(), T.cidx.size());
+    ALLOC_COPY(h->d_cval, T.cval.data(), T.cval.size());
 #undef ALLOC_COPY
     HIP_TRY(hipMalloc((void**)&h->d_partial, sizeof(double) * (size_t)batch * n_k * kNPartial));
     for (int i = 0; i < 3; ++i) HIP_TRY(hipEventCreate(&h->ev[i]));
@@ -834,8 +1034,8 @@ int awe_sparsity_jac_static(int n_k, int d, const double* consts, int n_consts, 
 
 int awe_destroy(awe_handle h) {
     if (!h) return AWE_OK;
-    hipFree(h->d_cst); hipFree(h->d_coll); hipFree(h->d_pos); hipFree(h->d_rowmask);
-    hipFree(h->d_cont); hipFree(h->d_per); hipFree(h->d_partial);
+    hipFree(h->d_cst); hipFree(h->d_coll); hipFree(h->d_ct); hipFree(h->d_pos); hipFree(h->d_seg);
+    hipFree(h->d_cidx_off); hipFree(h->d_cidx); hipFree(h->d_cval); hipFree(h->d_partial);
     hipFree(h->d_scr_jac); hipFree(h->d_scr_grad); hipFree(h->d_scr_g); hipFree(h->d_scr_f);
     hipFree(h->d_in_V); hipFree(h->d_in_P);
     for (int i = 0; i < 3; ++i) if (h->ev[i]) hipEventDestroy(h->ev[i]);

@@ -33,9 +33,24 @@ AWE_HD Dual operator+(Dual a, Dual b) { return Dual(a.v + b.v, a.d + b.d); }
 AWE_HD Dual operator-(Dual a, Dual b) { return Dual(a.v - b.v, a.d - b.d); }
 AWE_HD Dual operator-(Dual a) { return Dual(-a.v, -a.d); }
 AWE_HD Dual operator*(Dual a, Dual b) { return Dual(a.v * b.v, a.d * b.v + a.v * b.d); }
+// 1/x: hardware v_rcp_f64 (~2^-23 relative) refined by two Newton steps to ~1 ulp.  The dual
+// quotient rules below use one reciprocal each instead of two IEEE division sequences.
+AWE_HD double rcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
+
 AWE_HD Dual operator/(Dual a, Dual b) {
-    double q = a.v / b.v;
-    return Dual(q, (a.d - q * b.d) / b.v);
+    double r = rcp(b.v);
+    double q = a.v * r;
+    return Dual(q, (a.d - q * b.d) * r);
 }
 AWE_HD Dual operator+(Dual a, double b) { return Dual(a.v + b, a.d); }
 AWE_HD Dual operator+(double a, Dual b) { return Dual(a + b.v, b.d); }
@@ -43,10 +58,14 @@ AWE_HD Dual operator-(Dual a, double b) { return Dual(a.v - b, a.d); }
 AWE_HD Dual operator-(double a, Dual b) { return Dual(a - b.v, -b.d); }
 AWE_HD Dual operator*(Dual a, double b) { return Dual(a.v * b, a.d * b); }
 AWE_HD Dual operator*(double a, Dual b) { return Dual(a * b.v, a * b.d); }
-AWE_HD Dual operator/(Dual a, double b) { return Dual(a.v / b, a.d / b); }
+AWE_HD Dual operator/(Dual a, double b) {
+    double r = 1.0 / b;   // b is a model constant: folded, or one division per call site
+    return Dual(a.v * r, a.d * r);
+}
 AWE_HD Dual operator/(double a, Dual b) {
-    double q = a / b.v;
-    return Dual(q, -q * b.d / b.v);
+    double r = rcp(b.v);
+    double q = a * r;
+    return Dual(q, -q * b.d * r);
 }
 AWE_HD Dual& operator+=(Dual& a, Dual b) { a = a + b; return a; }
 AWE_HD Dual& operator-=(Dual& a, Dual b) { a = a - b; return a; }
@@ -54,13 +73,13 @@ AWE_HD Dual& operator*=(Dual& a, Dual b) { a = a * b; return a; }
 
 AWE_HD Dual sqrt(Dual a) {
     double s = ::sqrt(a.v);
-    return Dual(s, a.d * 0.5 / s);
+    return Dual(s, a.d * 0.5 * rcp(s));
 }
-// a^p for constant exponent p (a > 0)
-AWE_HD Dual pow(Dual a, double p) {
-    double r = ::pow(a.v, p);
-    return Dual(r, a.d * p * r / a.v);
+AWE_HD Dual exp(Dual a) {
+    double e = ::exp(a.v);
+    return Dual(e, e * a.d);
 }
+AWE_HD Dual log(Dual a) { return Dual(::log(a.v), a.d * rcp(a.v)); }
 AWE_HD double value(Dual a) { return a.v; }
 AWE_HD double tangent(Dual a) { return a.d; }
 
@@ -89,10 +108,12 @@ AWE_HD Dep& operator+=(Dep& a, Dep b) { a.m |= b.m; return a; }
 AWE_HD Dep& operator-=(Dep& a, Dep b) { a.m |= b.m; return a; }
 AWE_HD Dep& operator*=(Dep& a, Dep b) { a.m |= b.m; return a; }
 AWE_HD Dep sqrt(Dep a) { return a; }
-AWE_HD Dep pow(Dep a, double) { return a; }
+AWE_HD Dep exp(Dep a) { return a; }
+AWE_HD Dep log(Dep a) { return a; }
 
 AWE_HD double value(double a) { return a; }
 AWE_HD double sqrt(double a) { return ::sqrt(a); }
-AWE_HD double pow(double a, double p) { return ::pow(a, p); }
+AWE_HD double exp(double a) { return ::exp(a); }
+AWE_HD double log(double a) { return ::log(a); }
 
 }  // namespace awe
