@@ -65,12 +65,61 @@ AWE_HD T wind_speed(const T& zz, const double* th) {
     return scale * exp((0.5 * p) * log(zz * zz + 1.0));
 }
 
+// One element of the 'multi' tether drag model (element.py:60-104, segment.py:38-65): the drag
+// of element e of n_el on the main tether, lumped onto the kite node with the reference's shape
+// factor.  The tether's lower end is the ground (q = dq = 0); its share of the drag is dropped.
+template <class T>
+AWE_HD void tether_element(int e, int n_el, const T* q, const T* v, const T& diam, const double* th,
+                           T out[3]) {
+    const double ds = 1.0 / n_el;
+    const double s0 = 0.5 * ds, step = ((1.0 - 0.5 * ds) - s0) / (n_el - 1);
+    const double cd = th[AWE_TH_CD_TETHER];
+    const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
+    T zz = (q[2] * up + q[2] * lo) / 2.0;
+    T uw = wind_speed(zz, th);
+    T ue[3];
+    ue[0] = uw - (v[0] * up + v[0] * lo) / 2.0;
+    ue[1] = -((v[1] * up + v[1] * lo) / 2.0);
+    ue[2] = -((v[2] * up + v[2] * lo) / 2.0);
+    T un = sqrt(dot3(ue, ue) + 1e-12);
+    T tv[3];
+    for (int i = 0; i < 3; ++i) tv[i] = q[i] * up - q[i] * lo;
+    T lpar = dot3(tv, ue) / un;
+    T lperp = sqrt(dot3(tv, tv) - lpar * lpar + 1e-12);
+    T fac = cd * 0.5 * isa_density(zz, th) * un * diam * lperp;
+    const double sg = (e == n_el - 1) ? (1.0 - 0.5 * ds) : (s0 + e * step);
+    for (int i = 0; i < 3; ++i) out[i] = sg * (fac * ue[i]);
+}
+
+// Sub-models that depend on very few node variables (kite-height wind and density on q_z; the
+// tether drag on q, dq and diam_t).  The default provider evaluates them inline; the GPU kernel
+// substitutes a provider that returns values and partial derivatives preaccumulated once per
+// node, lane-parallel, so that the per-direction model pass does not repeat them.
+struct InlineSubmodels {
+    template <class T>
+    AWE_HD void kite_atmosphere(const T& qz, const double* th, T& uw, T& rho) const {
+        uw = wind_speed(qz, th);
+        rho = isa_density(qz, th);
+    }
+    template <class T>
+    AWE_HD void tether_drag(const T* q, const T* v, const T& diam, const double* th, const double* cst,
+                            T D[3]) const {
+        const int n_el = (int)cst[AWE_C_N_ELEMENTS];
+        for (int i = 0; i < 3; ++i) D[i] = T(0.0);
+        for (int e = 0; e < n_el; ++e) {
+            T c[3];
+            tether_element(e, n_el, q, v, diam, th, c);
+            for (int i = 0; i < 3; ++i) D[i] = D[i] + c[i];
+        }
+    }
+};
+
 // Rows are emitted phase by phase (DCM, trivial, aero -> rotation -> path constraints, tether
 // drag -> translation -> holonomic) and every phase re-reads its inputs through `in`, so that
 // short live ranges keep the dual-number working set inside the register file of one lane.
-template <class T, class In, class Sink>
+template <class T, class In, class Sink, class Sub = InlineSubmodels>
 AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const double* cst,
-                     Sink& out, bool want_ineq) {
+                     Sink& out, bool want_ineq, const Sub& sub = Sub()) {
     const double* s = cst + AWE_C_SCALING;
     // SI value of node variable i (dynamics.py:924-934)
     auto SI = [&](int i) -> T { return in(i) * s[i]; };
@@ -110,12 +159,11 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
     {
         T ua[3], ua_e1, ua_e2, ua_e3, uu, airspeed, rho_k;
         {
-            T qz = SI(2);
-            T uw = wind_speed(qz, th);
+            T uw;
+            sub.kite_atmosphere(SI(2), th, uw, rho_k);
             ua[0] = uw - SI(3);
             ua[1] = -SI(4);
             ua[2] = -SI(5);
-            rho_k = isa_density(qz, th);
         }
         ua_e1 = ua[0] * SI(9) + ua[1] * SI(10) + ua[2] * SI(11);
         ua_e2 = ua[0] * SI(12) + ua[1] * SI(13) + ua[2] * SI(14);
@@ -223,32 +271,8 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
     for (int i = 0; i < 3; ++i) q[i] = SI(i);
     for (int i = 0; i < 3; ++i) v[i] = SI(3 + i);
     T diam = SI(57);
-    // tether drag, 'multi' with n elements (element.py:60-104, segment.py:38-65); the main
-    // tether's lower end is the ground (q = dq = 0), its share of the drag is dropped
-    T D_tether[3] = {T(0.0), T(0.0), T(0.0)};
-    {
-        const int n_el = (int)cst[AWE_C_N_ELEMENTS];
-        const double ds = 1.0 / n_el;
-        const double s0 = 0.5 * ds, step = ((1.0 - 0.5 * ds) - s0) / (n_el - 1);
-        const double cd = th[AWE_TH_CD_TETHER];
-        for (int e = 0; e < n_el; ++e) {
-            const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
-            T zz = (q[2] * up + q[2] * lo) / 2.0;
-            T uw = wind_speed(zz, th);
-            T ue[3];
-            ue[0] = uw - (v[0] * up + v[0] * lo) / 2.0;
-            ue[1] = -((v[1] * up + v[1] * lo) / 2.0);
-            ue[2] = -((v[2] * up + v[2] * lo) / 2.0);
-            T un = sqrt(dot3(ue, ue) + 1e-12);
-            T tv[3];
-            for (int i = 0; i < 3; ++i) tv[i] = q[i] * up - q[i] * lo;
-            T lpar = dot3(tv, ue) / un;
-            T lperp = sqrt(dot3(tv, tv) - lpar * lpar + 1e-12);
-            T fac = cd * 0.5 * isa_density(zz, th) * un * diam * lperp;
-            const double sg = (e == n_el - 1) ? (1.0 - 0.5 * ds) : (s0 + e * step);
-            for (int i = 0; i < 3; ++i) D_tether[i] = D_tether[i] + sg * (fac * ue[i]);
-        }
-    }
+    T D_tether[3];
+    sub.tether_drag(q, v, diam, th, cst, D_tether);
     {
         T qq = dot3(q, q);
         T nq = sqrt(qq);                                      // vect_op.norm (eps = 0)

@@ -263,6 +263,36 @@ struct NodeSink {
     __device__ __forceinline__ void beta(const awe::Dual& v) { emit(kRowBeta, v); }
 };
 
+// Preaccumulated sub-models (InlineSubmodels in ap2_model.hpp): values and partial derivatives
+// w.r.t. the scaled node variables, computed once per node; a lane forms its tangent from the
+// seeds of its colour.  pr layout: D_tether[3], dD/d(q0,q1,q2,dq0,dq1,dq2,diam_t)[7][3],
+// u_wind, du_wind/dq_z, rho, drho/dq_z.
+constexpr int kPreStride = 28;
+constexpr int kPreDirs = 7;
+__device__ __forceinline__ int pre_var(int j) { return j < 6 ? j : kDirDiam; }
+
+struct LdsSubmodels {
+    const double* pr;
+    unsigned long long seedA;
+    __device__ __forceinline__ void kite_atmosphere(const awe::Dual&, const double*, awe::Dual& uw,
+                                                    awe::Dual& rho) const {
+        const double sd = ((seedA >> 2) & 1ull) ? 1.0 : 0.0;
+        uw = awe::Dual(pr[24], sd * pr[25]);
+        rho = awe::Dual(pr[26], sd * pr[27]);
+    }
+    __device__ __forceinline__ void tether_drag(const awe::Dual*, const awe::Dual*, const awe::Dual&,
+                                                const double*, const double*, awe::Dual D[3]) const {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < kPreDirs; ++j)
+                if ((seedA >> pre_var(j)) & 1ull) t += pr[3 + 3 * j + i];
+            D[i] = awe::Dual(pr[i], t);
+        }
+    }
+};
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -277,11 +307,12 @@ constexpr int nloc_pad() {
     return ((9 + AWE_NX + AWE_NU + AWE_NX + AWE_NZ + D * (AWE_NX + AWE_NZ) + AWE_NX) + 1) & ~1;
 }
 
-// LDS layout (doubles): vloc | wn[NN][64] | gval[NN][36] | dfl[NN][64] | fnode[NN pad] |
-//                       tang[tang_total] | jst[jst_size]
+// LDS layout (doubles): vloc | wn[NN][64] | gval[NN][36] | dfl[NN][64] | pre[NN][28] |
+//                       fnode[NN pad] | tang[tang_total] | jst[jst_size]
+// (the sub-model scratch of phase 0 aliases tang, which is written only from phase 1 on)
 template <int D>
 constexpr int lds_fixed_doubles() {
-    return nloc_pad<D>() + (D + 1) * (64 + kGvalStride + 64) + ((D + 2) & ~1);
+    return nloc_pad<D>() + (D + 1) * (64 + kGvalStride + 64 + kPreStride) + ((D + 2) & ~1);
 }
 
 template <int D>
@@ -311,7 +342,8 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
     double* wn = vloc + nloc_pad<D>();
     double* gval = wn + NN * 64;
     double* dfl = gval + NN * kGvalStride;
-    double* fnode = dfl + NN * 64;
+    double* pre = dfl + NN * 64;
+    double* fnode = pre + NN * kPreStride;
     double* tang = fnode + ((D + 2) & ~1);
     double* jst = tang + a.tang_total;
     auto toff = [&](int n) { return n == 0 ? 0 : ct->tsize[0] + (n - 1) * ct->tsize[1]; };
@@ -365,6 +397,53 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
     }
     __syncthreads();
 
+    // ---- phase 0b: sub-models, one (node, tether element, direction) per thread -----------
+    {
+        const double* s = a.cst + AWE_C_SCALING;
+        const int n_el = (int)a.cst[AWE_C_N_ELEMENTS];
+        const int ntask = n_el * kPreDirs + 1;
+        double* scr = tang;   // [NN][n_el][7][6]
+        for (int t = tid; t < NN * ntask; t += NT) {
+            const int n = t / ntask, q = t - n * ntask;
+            const double* w = wn + n * 64;
+            if (q < n_el * kPreDirs) {
+                const int e = q / kPreDirs, j = q - e * kPreDirs;
+                const int vj = pre_var(j);
+                awe::Dual qv[3], vv[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    qv[i] = awe::Dual(w[i], vj == i ? 1.0 : 0.0) * s[i];
+                    vv[i] = awe::Dual(w[3 + i], vj == 3 + i ? 1.0 : 0.0) * s[3 + i];
+                }
+                awe::Dual diam = awe::Dual(w[kDirDiam], vj == kDirDiam ? 1.0 : 0.0) * s[kDirDiam];
+                awe::Dual c[3];
+                awe::tether_element(e, n_el, qv, vv, diam, th, c);
+                double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) { o[i] = c[i].v; o[3 + i] = c[i].d; }
+            } else {
+                awe::Dual uw, rho;
+                awe::InlineSubmodels().kite_atmosphere(awe::Dual(w[2], 1.0) * s[2], th, uw, rho);
+                double* o = pre + n * kPreStride;
+                o[24] = uw.v; o[25] = uw.d; o[26] = rho.v; o[27] = rho.d;
+            }
+        }
+        __syncthreads();
+        // element sums in element order (the order of the inline model)
+        for (int t = tid; t < NN * kPreDirs * 3; t += NT) {
+            const int n = t / (kPreDirs * 3), j = (t / 3) % kPreDirs, i = t % 3;
+            double val = 0.0, tan = 0.0;
+            for (int e = 0; e < n_el; ++e) {
+                const double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
+                val = val + o[i];
+                tan = tan + o[3 + i];
+            }
+            if (j == 0) pre[n * kPreStride + i] = val;
+            pre[n * kPreStride + 3 + 3 * j + i] = tan;
+        }
+        __syncthreads();
+    }
+
     // ---- phase 1: model, one node per half-wavefront, one colour per lane ------------------
     {
         const int n = wave * 2 + (lane >> 5);
@@ -383,7 +462,8 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
             sink.cm = ct->cmask[kind][c];
             sink.c0 = c == 0;
             awe::Dual gamma(vt[2 + kPhiGamma], ((in.seedA >> kDirGamma) & 1ull) ? 1.0 : 0.0);
-            awe::ap2_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0);
+            LdsSubmodels sub{pre + n * kPreStride, in.seedA};
+            awe::ap2_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0, sub);
         }
     }
     __syncthreads();
@@ -792,6 +872,11 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
         }
     }
     h->tang_total = ct.tsize[0] + d * ct.tsize[1];
+    {   // the tangent buffer doubles as sub-model scratch [NN][n_el][7][6] in phase 0
+        const int n_el = (int)h->cst[AWE_C_N_ELEMENTS];
+        if (n_el < 1 || n_el > 64) return fail(AWE_ERR_ARG, "tether elements must be in 1..64");
+        h->tang_total = std::max(h->tang_total, NN * n_el * 7 * 6);
+    }
 
     // ---- target columns of each (k, node, direction) ------------------------------------
     auto dir_cols = [&](int k, int node, int dir, std::vector<int>& cols) {
