@@ -16,11 +16,15 @@
 //     state i seeds x_i AND xdot_i = C[jj,jj]/(h tf); the direction of xdot_i feeds the other
 //     d columns of the collocation polynomial; one direction carries d/d t_f of every xdot_i
 //     (collocation.py:202-258).  The chain rule through xdot = C X / (h tf) costs no extra pass;
-//   * scatter pass (one lane per direction): tangents are moved from the compressed LDS buffer
-//     into an LDS image of this interval's part of the CCS value array, and the objective's
-//     directional derivatives are formed (objective.py);
-//   * write-out: the interval's g rows, grad f columns and CCS runs leave LDS as contiguous,
-//     coalesced stores; the few global gradient entries are reduced deterministically by a small
+//   * the sub-models that depend on very few variables (tether drag: q, dq, diam_t; kite-height
+//     wind and density: q_z) are preaccumulated once per node, one (element, direction) per
+//     thread, and enter the model pass as values plus partial derivatives;
+//   * objective pass (one lane per direction): directional derivatives of the objective terms
+//     of each Radau node (objective.py), summed per V column in a fixed order;
+//   * write-out: the interval's g rows and grad f columns are contiguous stores; the CCS values
+//     of J_g are produced by a host-built gather list with one entry per CCS slot of the
+//     interval (tangent-buffer index, polynomial scale), so the J stores are contiguous and
+//     coalesced; the few global gradient entries are reduced deterministically by a small
 //     finalize kernel (no float atomics anywhere).
 #include <hip/hip_runtime.h>
 
@@ -58,7 +62,8 @@ constexpr int kRowPower = AWE_N_EQ + AWE_N_INEQ;       // 33: power integrand (o
 constexpr int kRowBeta = kRowPower + 1;                // 34: side slip (objective)
 constexpr int kGvalStride = 36;
 constexpr unsigned long long kJRows = (1ull << kRowPower) - 1ull;
-constexpr int kSegs = 4;         // CCS runs per interval: local columns, diam_t, t_f, gamma
+constexpr int kSegs = 4;
+constexpr int kMaxConst = 8;         // CCS runs per interval: local columns, diam_t, t_f, gamma
 constexpr int kPhiGamma = 0, kPhiPsi = 3;
 constexpr int kCostTracking = 0, kCostURegularisation = 1, kCostXdotRegularisation = 2,
               kCostGamma = 3, kCostPsi = 5, kCostFictitious = 10, kCostPower = 11, kCostTf = 13,
@@ -212,11 +217,9 @@ struct KArgs {
     const double* cst;
     const DevColl* coll;
     const ColorTabs* ct;
-    const unsigned short* pos;   // [n_k][d+1][64][max(d,1)] LDS index of a direction's first row
-    const int* seg;              // [n_k][kSegs][3] global CCS slot, length, LDS offset
-    const int* cidx_off;         // [n_k + 1] constant-entry ranges
-    const int* cidx;             // LDS index of constant entries (continuity, periodicity)
-    const double* cval;
+    const int* seg;              // [n_k][kSegs][3] global CCS slot, length, offset in the list
+    const unsigned* glist;       // per CCS slot: tangent index | scale index << 16
+    const int* glist_off;        // [n_k] first list entry of each interval
     double* g;
     double* jac;
     double* grad;
@@ -224,7 +227,10 @@ struct KArgs {
     double* f;
     int n_k, d, n_v, n_g, n_p, nnz, batch;
     int stride, rows, v_int0;
-    int tang_total, jst_size;
+    int tang_total;              // tangent buffer entries; tang[tang_total] holds 1.0
+    int nscale;                  // 1 + (d+1)^2 polynomial scales + constant entries
+    double kconst[kMaxConst];    // values of constant J entries (continuity, periodicity)
+    int nconst;
     int want_derivs;
 };
 
@@ -308,19 +314,25 @@ constexpr int nloc_pad() {
 }
 
 // LDS layout (doubles): vloc | wn[NN][64] | gval[NN][36] | dfl[NN][64] | pre[NN][28] |
-//                       fnode[NN pad] | tang[tang_total] | jst[jst_size]
+//                       fnode[NN pad] | scale[64] | tang[tang_total + 1]
 // (the sub-model scratch of phase 0 aliases tang, which is written only from phase 1 on)
 template <int D>
 constexpr int lds_fixed_doubles() {
-    return nloc_pad<D>() + (D + 1) * (64 + kGvalStride + 64 + kPreStride) + ((D + 2) & ~1);
+    return nloc_pad<D>() + (D + 1) * (64 + kGvalStride + 64 + kPreStride) + ((D + 2) & ~1) + 64 + 2;
 }
 
+// occupancy target (waves per SIMD) for the register allocator; build-time tunable
+#ifndef AWE_WAVES_PER_EU
+#define AWE_WAVES_PER_EU 3
+#endif
+
 template <int D>
-__global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs a) {
+__global__ __launch_bounds__(64 * waves_for<D>())
+__attribute__((amdgpu_waves_per_eu(AWE_WAVES_PER_EU, AWE_WAVES_PER_EU)))
+void ap2_interval_kernel(KArgs a) {
     constexpr int NN = D + 1;
     constexpr int W = waves_for<D>();
     constexpr int NT = 64 * W;
-    constexpr int NTG = D > 1 ? D : 1;      // CCS targets per direction
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int k = blockIdx.x % a.n_k;
@@ -344,16 +356,14 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
     double* dfl = gval + NN * kGvalStride;
     double* pre = dfl + NN * 64;
     double* fnode = pre + NN * kPreStride;
-    double* tang = fnode + ((D + 2) & ~1);
-    double* jst = tang + a.tang_total;
+    double* scl = fnode + ((D + 2) & ~1);
+    double* tang = scl + 64;
     auto toff = [&](int n) { return n == 0 ? 0 : ct->tsize[0] + (n - 1) * ct->tsize[1]; };
 
     // ---- phase 0: stage [theta, phi, x[k], u, xdot, z, coll..., x[k+1]]; constant J entries
     const int base = a.v_int0 + k * a.stride;
     for (int i = tid; i < 9; i += NT) vloc[i] = V[i];
     for (int i = tid; i < a.stride + AWE_NX; i += NT) vloc[9 + i] = V[base + i];
-    if (a.want_derivs)
-        for (int e = a.cidx_off[k] + tid; e < a.cidx_off[k + 1]; e += NT) jst[a.cidx[e]] = a.cval[e];
     __syncthreads();
     const double* vt = vloc;                       // theta at 0, phi at 2
     const double* vx = vloc + 9;                   // x[k]
@@ -366,6 +376,14 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
     const double h = 1.0 / a.n_k;
     const double inv_h_tf = 1.0 / h / tf;
     const double inv_tf = 1.0 / tf;
+    // gather scales: 1, C[r][n] / (h tf) for the polynomial columns, constant entries
+    for (int i = tid; i < a.nscale; i += NT) {
+        double sv = 1.0;
+        if (i >= 1 && i <= NN * NN) sv = C[i - 1] * inv_h_tf;
+        else if (i > NN * NN) sv = a.kconst[i - 1 - NN * NN];
+        scl[i] = sv;
+    }
+    if (tid == 0) tang[a.tang_total] = 1.0;
 
     // node values (scaled, AWE_NW layout); xdot at Radau nodes from the polynomial
     for (int t = tid; t < NN * 64; t += NT) {
@@ -398,6 +416,7 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
     __syncthreads();
 
     // ---- phase 0b: sub-models, one (node, tether element, direction) per thread -----------
+#ifndef AWE_EXP_SKIP_PRE
     {
         const double* s = a.cst + AWE_C_SCALING;
         const int n_el = (int)a.cst[AWE_C_N_ELEMENTS];
@@ -443,12 +462,17 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
         }
         __syncthreads();
     }
+#endif
 
     // ---- phase 1: model, one node per half-wavefront, one colour per lane ------------------
     {
         const int n = wave * 2 + (lane >> 5);
         const int c = lane & (kHalf - 1);
+#ifndef AWE_EXP_SKIP_MODEL
         if (n < NN) {
+#else
+        if (n < 0) {
+#endif
             const int kind = n > 0 ? 1 : 0;
             LaneIn in;
             in.w = wn + n * 64;
@@ -482,36 +506,6 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
         const int c = ct->dcolor[kind][dir];
         const unsigned long long cm = c >= 0 ? ct->cmask[kind][c] : 0ull;
         const double* tp = tang + toff(n) + (c >= 0 ? ct->off[kind][c] : 0);
-        if (a.want_derivs) {
-            const unsigned short* pl = a.pos + (((size_t)k * NN + n) * kDirs + dir) * NTG;
-            const bool xd = n > 0 && dir >= AWE_NX && dir < 2 * AWE_NX;
-            int p[NTG];
-            double sc[NTG];
-            {
-                int t = 0;
-#pragma unroll
-                for (int rr = 0; rr < NN; ++rr) {
-                    if (rr == n || t >= NTG) continue;
-                    p[t] = pl[t];
-                    sc[t] = C[rr * NN + n] * inv_h_tf;
-                    ++t;
-                }
-                for (; t < NTG; ++t) { p[t] = 0; sc[t] = 0.0; }
-            }
-            if (!xd) p[0] = pl[0];
-            int rank = 0;
-            for (unsigned long long mm = m & kJRows; mm; mm &= mm - 1ull) {
-                const int r = __builtin_ctzll(mm);
-                const double v = tp[__popcll(cm & ((1ull << r) - 1ull))];
-                if (xd) {
-#pragma unroll
-                    for (int t = 0; t < NTG; ++t) jst[p[t] + rank] = sc[t] * v;
-                } else {
-                    jst[p[0] + rank] = v;
-                }
-                ++rank;
-            }
-        }
         if (n > 0) {
             // objective at Radau node j (objective.py:45-544): w_j [psi tracking + xdot, u,
             // fictitious and theta regularisation] + beta cost + (1 - psi) power cost
@@ -625,12 +619,16 @@ __global__ __launch_bounds__(64 * waves_for<D>()) void ap2_interval_kernel(KArgs
         }                                                     // xdot[k], z[k]: 0
         grad[base + col] = gsum;
     }
-    // the interval's CCS runs, contiguous in the value array
+    // the interval's CCS runs, contiguous in the value array: one gather entry per slot
     const int* sg = a.seg + (size_t)k * kSegs * 3;
+    const unsigned* gl = a.glist + a.glist_off[k];
 #pragma unroll
     for (int s = 0; s < kSegs; ++s) {
         const int g0 = sg[3 * s], len = sg[3 * s + 1], lo = sg[3 * s + 2];
-        for (int i = tid; i < len; i += NT) jac[g0 + i] = jst[lo + i];
+        for (int i = tid; i < len; i += NT) {
+            const unsigned e = gl[lo + i];
+            jac[g0 + i] = scl[e >> 16] * tang[e & 0xffffu];
+        }
     }
 }
 
@@ -696,17 +694,16 @@ struct awe_handle_s {
     std::vector<double> cst;
     std::vector<int> colind, row;
     int nnz = 0;
-    int tang_total = 0, jst_size = 0;
+    int tang_total = 0, nscale = 0;
+    std::vector<double> kconst;
     size_t lds_bytes = 0;
     // device
     double* d_cst = nullptr;
     DevColl* d_coll = nullptr;
     ColorTabs* d_ct = nullptr;
-    unsigned short* d_pos = nullptr;
     int* d_seg = nullptr;
-    int* d_cidx_off = nullptr;
-    int* d_cidx = nullptr;
-    double* d_cval = nullptr;
+    unsigned* d_glist = nullptr;
+    int* d_glist_off = nullptr;
     double* d_partial = nullptr;
     // scratch for value-only calls and host wrappers
     double* d_scr_jac = nullptr;
@@ -752,12 +749,14 @@ int launch_interval(awe_handle h, const KArgs& a, hipStream_t stream) {
 int launch(awe_handle h, const double* V, const double* P, double* f, double* g, double* grad,
            double* jac, int want_derivs, hipStream_t stream) {
     KArgs a{};
-    a.V = V; a.P = P; a.cst = h->d_cst; a.coll = h->d_coll; a.ct = h->d_ct; a.pos = h->d_pos;
-    a.seg = h->d_seg; a.cidx_off = h->d_cidx_off; a.cidx = h->d_cidx; a.cval = h->d_cval;
+    a.V = V; a.P = P; a.cst = h->d_cst; a.coll = h->d_coll; a.ct = h->d_ct;
+    a.seg = h->d_seg; a.glist = h->d_glist; a.glist_off = h->d_glist_off;
+    a.nscale = h->nscale; a.nconst = (int)h->kconst.size();
+    for (size_t q = 0; q < h->kconst.size(); ++q) a.kconst[q] = h->kconst[q];
     a.g = g; a.jac = jac; a.grad = grad; a.partial = h->d_partial; a.f = f;
     a.n_k = h->n_k; a.d = h->d; a.n_v = h->lay.n_v; a.n_g = h->lay.n_g; a.n_p = h->lay.n_p;
     a.nnz = h->nnz; a.batch = h->batch; a.stride = h->lay.stride; a.rows = h->lay.rows;
-    a.v_int0 = h->lay.v_int0; a.tang_total = h->tang_total; a.jst_size = h->jst_size;
+    a.v_int0 = h->lay.v_int0; a.tang_total = h->tang_total;
     a.want_derivs = want_derivs;
     HIP_TRY(hipEventRecord(h->ev[0], stream));
     switch (h->d) {
@@ -789,9 +788,8 @@ size_t lds_fixed_bytes(int d) {
 
 struct HostTables {
     ColorTabs ct{};
-    std::vector<unsigned short> pos;
-    std::vector<int> seg, cidx_off, cidx;
-    std::vector<double> cval;
+    std::vector<int> seg, glist_off;
+    std::vector<unsigned> glist;
 };
 
 // CPU-only: collocation coefficients, structural masks of the node model, the colouring of the
@@ -804,7 +802,6 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
     const Layout& L = h->lay;
     const Coll& cl = h->coll;
     const int NN = d + 1;
-    const int NTG = d > 1 ? d : 1;
 
     // ---- direction row masks ------------------------------------------------------------
     ModelMasks mm;
@@ -949,7 +946,6 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
     // also owns the terminal x[n_k] columns); runs 1-3: the interval's rows of the global
     // columns diam_t, t_f and phi.gamma
     std::vector<int> seg((size_t)n_k * kSegs * 3, 0);
-    int jst_max = 0;
     const int gcols[kSegs - 1] = {L.theta(0), L.theta(1), L.phi(kPhiGamma)};
     for (int k = 0; k < n_k; ++k) {
         int* s = &seg[(size_t)k * kSegs * 3];
@@ -965,9 +961,7 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
             s[3 * (q + 1)] = a0; s[3 * (q + 1) + 1] = a1 - a0; s[3 * (q + 1) + 2] = off;
             off += a1 - a0;
         }
-        jst_max = std::max(jst_max, off);
     }
-    h->jst_size = jst_max;
     auto lds_of = [&](int k, int slot) -> int {
         const int* s = &seg[(size_t)k * kSegs * 3];
         for (int q = 0; q < kSegs; ++q)
@@ -985,38 +979,58 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
         for (int i = 0; i < h->nnz; ++i) if (cover[i] != 1) ++bad;
     }
 
-    // ---- LDS index of each direction's first row in each target column -------------------
-    std::vector<unsigned short> pos((size_t)n_k * NN * kDirs * NTG, 0xffff);
-    std::vector<std::vector<int>> written(n_k);
-    for (int k = 0; k < n_k; ++k) written[k].assign(jst_max, 0);
+    // ---- gather list: for every CCS slot of every interval, where its value comes from -------
+    std::vector<int> list_off(n_k + 1, 0);
+    for (int k = 0; k < n_k; ++k) {
+        const int* s = &seg[(size_t)k * kSegs * 3];
+        int total = 0;
+        for (int q = 0; q < kSegs; ++q) total += s[3 * q + 1];
+        list_off[k + 1] = list_off[k] + total;
+    }
+    const unsigned kUnset = 0xffffffffu;
+    std::vector<unsigned> glist(list_off[n_k], kUnset);
+    const int nn2 = NN * NN;
+    auto put = [&](int k, int slot, int src, int scale) {
+        const int q = lds_of(k, slot);
+        if (q < 0 || src < 0 || src > 0xffff || scale > 0xffff) { ++bad; return; }
+        unsigned& e = glist[list_off[k] + q];
+        if (e != kUnset) ++bad;
+        e = (unsigned)src | ((unsigned)scale << 16);
+    };
+    auto toff = [&](int node) { return node == 0 ? 0 : ct.tsize[0] + (node - 1) * ct.tsize[1]; };
     for (int k = 0; k < n_k; ++k)
-        for (int node = 0; node < NN; ++node)
+        for (int node = 0; node < NN; ++node) {
+            const int kind = node > 0;
             for (int dir = 0; dir < kDirs; ++dir) {
-                const unsigned long long m = ct.dmask[node > 0][dir] & kJRows;
+                const unsigned long long m = ct.dmask[kind][dir] & kJRows;
                 if (!m) continue;
+                const int c = ct.dcolor[kind][dir];
+                const unsigned long long cm = ct.cmask[kind][c];
+                const bool xd = node > 0 && dir >= AWE_NX && dir < 2 * AWE_NX;
                 dir_cols(k, node, dir, cols);
+                std::vector<int> rr_of;   // polynomial node of each target (xdot directions)
+                for (int r = 0; r < NN; ++r) if (r != node) rr_of.push_back(r);
                 const int g0 = node_row0(k, node);
-                for (size_t t = 0; t < cols.size(); ++t) {
-                    const int p = lds_of(k, find(cols[t], g0 + __builtin_ctzll(m)));
-                    if (p < 0) { ++bad; continue; }
-                    int cnt = 0;   // the node's rows must be consecutive entries of the column
-                    for (int r = 0; r < kRowPower; ++r)
-                        if ((m >> r) & 1ull) {
-                            const int q = lds_of(k, find(cols[t], g0 + r));
-                            if (q != p + cnt) ++bad; else written[k][q]++;
-                            ++cnt;
-                        }
-                    pos[(((size_t)k * NN + node) * kDirs + dir) * NTG + t] = (unsigned short)p;
-                }
+                for (size_t t = 0; t < cols.size(); ++t)
+                    for (int r = 0; r < kRowPower; ++r) {
+                        if (!((m >> r) & 1ull)) continue;
+                        const int src = toff(node) + ct.off[kind][c] +
+                                        __builtin_popcountll(cm & ((1ull << r) - 1ull));
+                        const int scale = xd ? 1 + rr_of[t] * NN + node : 0;
+                        put(k, find(cols[t], g0 + r), src, scale);
+                    }
             }
+        }
     // ---- constant entries: continuity (+1, -D_r) and periodicity (+1, -1) ------------------
-    std::vector<std::vector<std::pair<int, double>>> cent(n_k);
+    std::vector<double>& kc = h->kconst;
+    kc.clear();
     auto add_const = [&](int col, int rw, double val) {
         const int slot = find(col, rw);
-        for (int k = 0; k < n_k; ++k) {
-            const int q = lds_of(k, slot);
-            if (q >= 0) { cent[k].emplace_back(q, val); written[k][q]++; return; }
-        }
+        size_t q = 0;
+        while (q < kc.size() && kc[q] != val) ++q;
+        if (q == kc.size()) kc.push_back(val);
+        for (int k = 0; k < n_k; ++k)
+            if (lds_of(k, slot) >= 0) { put(k, slot, h->tang_total, 1 + nn2 + (int)q); return; }
         ++bad;
     };
     for (int k = 0; k < n_k; ++k)
@@ -1029,22 +1043,16 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
         add_const(L.x(0, kPeriodicOrder[i]), L.g_periodic() + i, 1.0);
         add_const(last + kPeriodicOrder[i], L.g_periodic() + i, -1.0);
     }
-    // every slot of every interval image is written exactly once
-    for (int k = 0; k < n_k; ++k) {
-        const int* s = &seg[(size_t)k * kSegs * 3];
-        int total = 0;
-        for (int q = 0; q < kSegs; ++q) total += s[3 * q + 1];
-        for (int i = 0; i < jst_max; ++i) if (written[k][i] != (i < total ? 1 : 0)) ++bad;
-    }
+    if ((int)kc.size() > kMaxConst) return fail(AWE_ERR_ARG, "internal: too many constant entries");
+    h->nscale = 1 + nn2 + (int)kc.size();
+    if (h->nscale > 64) return fail(AWE_ERR_ARG, "internal: scale table exceeds 64 entries");
+    // every slot of every interval run has exactly one source
+    for (unsigned e : glist) if (e == kUnset) ++bad;
     if (bad) return fail(AWE_ERR_ARG, "internal: inconsistent sparsity tables");
-    T.cidx_off.assign(n_k + 1, 0);
-    for (int k = 0; k < n_k; ++k) {
-        T.cidx_off[k + 1] = T.cidx_off[k] + (int)cent[k].size();
-        for (auto& e : cent[k]) { T.cidx.push_back(e.first); T.cval.push_back(e.second); }
-    }
-    T.pos.swap(pos);
+    T.glist.swap(glist);
+    T.glist_off.assign(list_off.begin(), list_off.end() - 1);
     T.seg.swap(seg);
-    h->lds_bytes = lds_fixed_bytes(d) + sizeof(double) * (size_t)(h->tang_total + h->jst_size);
+    h->lds_bytes = lds_fixed_bytes(d) + sizeof(double) * (size_t)(h->tang_total + 1);
     if (h->lds_bytes > 65536) return fail(AWE_ERR_ARG, "internal: LDS image exceeds 64 KiB");
     return AWE_OK;
 }
@@ -1088,11 +1096,9 @@ int awe_create(int n_k, int d, const double* consts, int n_consts, int batch, aw
     ALLOC_COPY(h->d_cst, h->cst.data(), h->cst.size());
     ALLOC_COPY(h->d_coll, &dc, 1);
     ALLOC_COPY(h->d_ct, &T.ct, 1);
-    ALLOC_COPY(h->d_pos, T.pos.data(), T.pos.size());
     ALLOC_COPY(h->d_seg, T.seg.data(), T.seg.size());
-    ALLOC_COPY(h->d_cidx_off, T.cidx_off.data(), T.cidx_off.size());
-    ALLOC_COPY(h->d_cidx, T.cidx.data(), T.cidx.size());
-    ALLOC_COPY(h->d_cval, T.cval.data(), T.cval.size());
+    ALLOC_COPY(h->d_glist, T.glist.data(), T.glist.size());
+    ALLOC_COPY(h->d_glist_off, T.glist_off.data(), T.glist_off.size());
 #undef ALLOC_COPY
     HIP_TRY(hipMalloc((void**)&h->d_partial, sizeof(double) * (size_t)batch * n_k * kNPartial));
     for (int i = 0; i < 3; ++i) HIP_TRY(hipEventCreate(&h->ev[i]));
@@ -1119,8 +1125,8 @@ int awe_sparsity_jac_static(int n_k, int d, const double* consts, int n_consts, 
 
 int awe_destroy(awe_handle h) {
     if (!h) return AWE_OK;
-    hipFree(h->d_cst); hipFree(h->d_coll); hipFree(h->d_ct); hipFree(h->d_pos); hipFree(h->d_seg);
-    hipFree(h->d_cidx_off); hipFree(h->d_cidx); hipFree(h->d_cval); hipFree(h->d_partial);
+    hipFree(h->d_cst); hipFree(h->d_coll); hipFree(h->d_ct); hipFree(h->d_seg);
+    hipFree(h->d_glist); hipFree(h->d_glist_off); hipFree(h->d_partial);
     hipFree(h->d_scr_jac); hipFree(h->d_scr_grad); hipFree(h->d_scr_g); hipFree(h->d_scr_f);
     hipFree(h->d_in_V); hipFree(h->d_in_P);
     for (int i = 0; i < 3; ++i) if (h->ev[i]) hipEventDestroy(h->ev[i]);
