@@ -209,13 +209,15 @@ struct ColorTabs {
     unsigned long long dmask[2][kDirs];   // rows of each direction
     int dcolor[2][kDirs];                 // colour of each direction, -1 if it has no rows
     int tsize[2];                         // tangent-buffer entries per node
+    int obj_beta[kDirs];                  // Radau node: tangent-buffer index of the beta row of
+    int obj_power[kDirs];                 // each direction, and of its power row (-1: none)
 };
 
 struct KArgs {
     const double* V;
     const double* P;
     const double* cst;
-    const DevColl* coll;
+    DevColl coll;                // by value: uniform loads from the kernel-argument segment
     const ColorTabs* ct;
     const int* seg;              // [n_k][kSegs][3] global CCS slot, length, offset in the list
     const unsigned* glist;       // per CCS slot: tangent index | scale index << 16
@@ -313,12 +315,19 @@ constexpr int nloc_pad() {
     return ((9 + AWE_NX + AWE_NU + AWE_NX + AWE_NZ + D * (AWE_NX + AWE_NZ) + AWE_NX) + 1) & ~1;
 }
 
-// LDS layout (doubles): vloc | wn[NN][64] | gval[NN][36] | dfl[NN][64] | pre[NN][28] |
+// LDS layout (doubles): vloc | pst | wn[NN][64] | gval[NN][36] | dfl[NN][64] | pre[NN][28] |
 //                       fnode[NN pad] | scale[64] | tang[tang_total + 1]
 // (the sub-model scratch of phase 0 aliases tang, which is written only from phase 1 on)
+// P staged for the objective: weights[59] | cost[20] at 64 | theta ref[2] at 84 | ref V slice
+constexpr int kPstCost = 64, kPstThRef = 84, kPstRef = 86;
+template <int D>
+constexpr int pst_pad() {
+    return (kPstRef + AWE_NX + AWE_NU + AWE_NX + AWE_NZ + D * (AWE_NX + AWE_NZ) + 1) & ~1;
+}
+
 template <int D>
 constexpr int lds_fixed_doubles() {
-    return nloc_pad<D>() + (D + 1) * (64 + kGvalStride + 64 + kPreStride) + ((D + 2) & ~1) + 64 + 2;
+    return nloc_pad<D>() + pst_pad<D>() + (D + 1) * (64 + kGvalStride + 64 + kPreStride) + ((D + 2) & ~1) + 64 + 2;
 }
 
 // occupancy target (waves per SIMD) for the register allocator; build-time tunable
@@ -347,11 +356,12 @@ void ap2_interval_kernel(KArgs a) {
     double* jac = a.jac + (size_t)b * a.nnz;
     double* grad = a.grad + (size_t)b * a.n_v;
     const ColorTabs* ct = a.ct;
-    const double* C = a.coll->C;
+    const double* C = a.coll.C;
 
     extern __shared__ double smem[];
     double* vloc = smem;
-    double* wn = vloc + nloc_pad<D>();
+    double* pst = vloc + nloc_pad<D>();
+    double* wn = pst + pst_pad<D>();
     double* gval = wn + NN * 64;
     double* dfl = gval + NN * kGvalStride;
     double* pre = dfl + NN * 64;
@@ -364,6 +374,15 @@ void ap2_interval_kernel(KArgs a) {
     const int base = a.v_int0 + k * a.stride;
     for (int i = tid; i < 9; i += NT) vloc[i] = V[i];
     for (int i = tid; i < a.stride + AWE_NX; i += NT) vloc[9 + i] = V[base + i];
+    for (int i = tid; i < kPstRef + a.stride; i += NT) {
+        double pv = 0.0;
+        if (i < AWE_NW) pv = wts[i];
+        else if (i >= kPstCost && i < kPstCost + AWE_NCOST) pv = cost[i - kPstCost];
+        else if (i >= kPstThRef && i < kPstRef) pv = vref[i - kPstThRef];
+        else if (i >= kPstRef) pv = vref[base + i - kPstRef];
+        pst[i] = pv;
+    }
+    const int obj_b = ct->obj_beta[lane], obj_p = ct->obj_power[lane];
     __syncthreads();
     const double* vt = vloc;                       // theta at 0, phi at 2
     const double* vx = vloc + 9;                   // x[k]
@@ -492,51 +511,50 @@ void ap2_interval_kernel(KArgs a) {
     }
     __syncthreads();
 
-    // ---- phase 2: scatter tangents into the CCS image; objective directional derivatives --
+    // ---- phase 2: objective directional derivatives (one lane per direction) -------------
+    const double* pcost = pst + kPstCost;
+    const double* pw8 = pst;                                   // weights
     const double psi = vt[2 + kPhiPsi];
-    const double w_track = cost[kCostTracking] / a.cst[AWE_C_NORM_TRACKING];
-    const double w_xdot = cost[kCostXdotRegularisation] / a.cst[AWE_C_NORM_XDOT_REG];
-    const double w_ureg = cost[kCostURegularisation] / a.cst[AWE_C_NORM_U_REG];
-    const double w_fict = cost[kCostFictitious] / a.cst[AWE_C_NORM_FICTITIOUS];
-    const double w_theta = cost[kCostThetaRegularisation] / a.cst[AWE_C_NORM_THETA_REG];
-    for (int n = wave; n < NN; n += W) {
-        const int kind = n > 0 ? 1 : 0;
+    const double w_track = pcost[kCostTracking] / a.cst[AWE_C_NORM_TRACKING];
+    const double w_xdot = pcost[kCostXdotRegularisation] / a.cst[AWE_C_NORM_XDOT_REG];
+    const double w_ureg = pcost[kCostURegularisation] / a.cst[AWE_C_NORM_U_REG];
+    const double w_fict = pcost[kCostFictitious] / a.cst[AWE_C_NORM_FICTITIOUS];
+    const double w_theta = pcost[kCostThetaRegularisation] / a.cst[AWE_C_NORM_THETA_REG];
+#ifndef AWE_EXP_SKIP_OBJ
+    for (int n = 1 + wave; n < NN; n += W) {
         const int dir = lane;
-        const unsigned long long m = ct->dmask[kind][dir];
-        const int c = ct->dcolor[kind][dir];
-        const unsigned long long cm = c >= 0 ? ct->cmask[kind][c] : 0ull;
-        const double* tp = tang + toff(n) + (c >= 0 ? ct->off[kind][c] : 0);
-        if (n > 0) {
+        const double* tp = tang + toff(n);
+        {
             // objective at Radau node j (objective.py:45-544): w_j [psi tracking + xdot, u,
             // fictitious and theta regularisation] + beta cost + (1 - psi) power cost
             const int j = n - 1;
-            const double wj = a.coll->w[j];
+            const double wj = a.coll.w[j];
             const double* w = wn + n * 64;
-            const double* rb = vref + base;
+            const double* rb = pst + kPstRef;                  // reference V slice
             const double* rcx = rb + 2 * AWE_NX + AWE_NU + AWE_NZ + j * (AWE_NX + AWE_NZ);
             const double* ru = rb + AWE_NX;
             const double cxx = C[n * NN + n] * inv_h_tf;
             double trk = 0.0, xdr = 0.0, oth = 0.0, dfd = 0.0;
             if (dir < AWE_NX) {
-                const double e = w[dir] - rcx[dir], ww = wts[dir] * w_track;
-                const double xdv = w[AWE_NX + dir], wx = wts[AWE_NX + dir] * w_xdot;
+                const double e = w[dir] - rcx[dir], ww = pw8[dir] * w_track;
+                const double xdv = w[AWE_NX + dir], wx = pw8[AWE_NX + dir] * w_xdot;
                 trk = ww * (e * e);
                 dfd = wj * (psi * (2.0 * ww * e) + cxx * (2.0 * wx * xdv));
             } else if (dir < 2 * AWE_NX) {
-                const double xdv = w[dir], wx = wts[dir] * w_xdot;
+                const double xdv = w[dir], wx = pw8[dir] * w_xdot;
                 xdr = wx * (xdv * xdv);
                 dfd = wj * (2.0 * wx * xdv);
             } else if (dir < 2 * AWE_NX + AWE_NU) {
                 const int i = dir - 2 * AWE_NX;
-                const double e = w[dir] - ru[i], wu = wts[dir] * (i < 6 ? w_fict : w_ureg);
+                const double e = w[dir] - ru[i], wu = pw8[dir] * (i < 6 ? w_fict : w_ureg);
                 oth = wu * (e * e);
                 dfd = wj * (2.0 * wu * e);
             } else if (dir == kDirZ) {
-                const double e = w[dir] - rcx[AWE_NX], ww = wts[dir] * w_track;
+                const double e = w[dir] - rcx[AWE_NX], ww = pw8[dir] * w_track;
                 trk = ww * (e * e);
                 dfd = wj * psi * (2.0 * ww * e);
             } else if (dir == kDirDiam) {
-                const double e = w[dir] - vref[0], wt = wts[dir] * w_theta;
+                const double e = w[dir] - pst[kPstThRef], wt = pw8[dir] * w_theta;
                 oth = wt * (e * e);
                 dfd = wj * (2.0 * wt * e);
             }
@@ -545,22 +563,21 @@ void ap2_interval_kernel(KArgs a) {
             oth = wave_sum(oth);
             const double bv = gval[n * kGvalStride + kRowBeta];
             const double pv = gval[n * kGvalStride + kRowPower];
-            const double cb = cost[kCostBeta] * wj / a.cst[AWE_C_NORM_BETA];
-            const double cp = -cost[kCostPower] * wj / (double)a.n_k;   // (-c_p)(tf/N) w_j p / tf
+            const double cb = pcost[kCostBeta] * wj / a.cst[AWE_C_NORM_BETA];
+            const double cp = -pcost[kCostPower] * wj / (double)a.n_k;   // (-c_p)(tf/N) w_j p / tf
             if (dir == kDirTf) dfd = -2.0 * wj * xdr * inv_tf;
             if (dir == kDirPsi) dfd = wj * trk - cp * pv;
-            if ((m >> kRowBeta) & 1ull)
-                dfd += (2.0 * cb * bv) * tp[__popcll(cm & ((1ull << kRowBeta) - 1ull))];
-            if ((m >> kRowPower) & 1ull)
-                dfd += ((1.0 - psi) * cp) * tp[__popcll(cm & ((1ull << kRowPower) - 1ull))];
+            if (obj_b >= 0) dfd += (2.0 * cb * bv) * tp[obj_b];
+            if (obj_p >= 0) dfd += ((1.0 - psi) * cp) * tp[obj_p];
             dfl[n * 64 + dir] = dfd;
             if (dir == 0) fnode[n] = wj * (psi * trk + xdr + oth) + cb * (bv * bv) + (1.0 - psi) * (cp * pv);
         }
     }
+#endif
     __syncthreads();
 
     // ---- phase 3: write-out ---------------------------------------------------------------
-    const DevColl* cc = a.coll;
+    const DevColl* cc = &a.coll;
     for (int r = tid; r < a.rows; r += NT) {
         double val;
         if (r < AWE_N_EQ + AWE_N_INEQ) {
@@ -625,6 +642,9 @@ void ap2_interval_kernel(KArgs a) {
 #pragma unroll
     for (int s = 0; s < kSegs; ++s) {
         const int g0 = sg[3 * s], len = sg[3 * s + 1], lo = sg[3 * s + 2];
+#ifdef AWE_EXP_SKIP_GATHER
+        if (tid < 0)
+#endif
         for (int i = tid; i < len; i += NT) {
             const unsigned e = gl[lo + i];
             jac[g0 + i] = scl[e >> 16] * tang[e & 0xffffu];
@@ -699,7 +719,7 @@ struct awe_handle_s {
     size_t lds_bytes = 0;
     // device
     double* d_cst = nullptr;
-    DevColl* d_coll = nullptr;
+    DevColl dcoll{};
     ColorTabs* d_ct = nullptr;
     int* d_seg = nullptr;
     unsigned* d_glist = nullptr;
@@ -749,7 +769,7 @@ int launch_interval(awe_handle h, const KArgs& a, hipStream_t stream) {
 int launch(awe_handle h, const double* V, const double* P, double* f, double* g, double* grad,
            double* jac, int want_derivs, hipStream_t stream) {
     KArgs a{};
-    a.V = V; a.P = P; a.cst = h->d_cst; a.coll = h->d_coll; a.ct = h->d_ct;
+    a.V = V; a.P = P; a.cst = h->d_cst; a.coll = h->dcoll; a.ct = h->d_ct;
     a.seg = h->d_seg; a.glist = h->d_glist; a.glist_off = h->d_glist_off;
     a.nscale = h->nscale; a.nconst = (int)h->kconst.size();
     for (size_t q = 0; q < h->kconst.size(); ++q) a.kconst[q] = h->kconst[q];
@@ -867,6 +887,16 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
                 if (kind == 1 && dir == kDirTf) ct.tf_color[kind] = c;
             }
         }
+    }
+    for (int dir = 0; dir < kDirs; ++dir) {
+        ct.obj_beta[dir] = ct.obj_power[dir] = -1;
+        const int c = ct.dcolor[1][dir];
+        if (c < 0) continue;
+        const unsigned long long m = ct.dmask[1][dir], cm = ct.cmask[1][c];
+        if ((m >> kRowBeta) & 1ull)
+            ct.obj_beta[dir] = ct.off[1][c] + __builtin_popcountll(cm & ((1ull << kRowBeta) - 1ull));
+        if ((m >> kRowPower) & 1ull)
+            ct.obj_power[dir] = ct.off[1][c] + __builtin_popcountll(cm & ((1ull << kRowPower) - 1ull));
     }
     h->tang_total = ct.tsize[0] + d * ct.tsize[1];
     {   // the tangent buffer doubles as sub-model scratch [NN][n_el][7][6] in phase 0
@@ -1089,12 +1119,12 @@ int awe_create(int n_k, int d, const double* consts, int n_consts, int batch, aw
         for (int r = 0; r < NN; ++r) dc.C[j * NN + r] = cl.C[j][r];
     for (int j = 0; j < NN; ++j) dc.D[j] = cl.D[j];
     for (int j = 0; j < d; ++j) dc.w[j] = cl.w[j];
+    h->dcoll = dc;
 
 #define ALLOC_COPY(dst, src, n)                                                     \
     HIP_TRY(hipMalloc((void**)&dst, sizeof(*dst) * (n)));                          \
     HIP_TRY(hipMemcpy(dst, src, sizeof(*dst) * (n), hipMemcpyHostToDevice))
     ALLOC_COPY(h->d_cst, h->cst.data(), h->cst.size());
-    ALLOC_COPY(h->d_coll, &dc, 1);
     ALLOC_COPY(h->d_ct, &T.ct, 1);
     ALLOC_COPY(h->d_seg, T.seg.data(), T.seg.size());
     ALLOC_COPY(h->d_glist, T.glist.data(), T.glist.size());
@@ -1125,7 +1155,7 @@ int awe_sparsity_jac_static(int n_k, int d, const double* consts, int n_consts, 
 
 int awe_destroy(awe_handle h) {
     if (!h) return AWE_OK;
-    hipFree(h->d_cst); hipFree(h->d_coll); hipFree(h->d_ct); hipFree(h->d_seg);
+    hipFree(h->d_cst); hipFree(h->d_ct); hipFree(h->d_seg);
     hipFree(h->d_glist); hipFree(h->d_glist_off); hipFree(h->d_partial);
     hipFree(h->d_scr_jac); hipFree(h->d_scr_grad); hipFree(h->d_scr_g); hipFree(h->d_scr_f);
     hipFree(h->d_in_V); hipFree(h->d_in_P);
