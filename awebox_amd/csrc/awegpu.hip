@@ -256,14 +256,19 @@ struct LaneIn {
 };
 
 // streams one node's rows into the compressed LDS tangent buffer (and values into gval)
+// (branch-free: stores a lane does not own go to its private dump slot)
 struct NodeSink {
     double* tp;
     double* gv;
+    double* dump;
     unsigned long long cm;
     bool c0;
     __device__ __forceinline__ void emit(int r, const awe::Dual& v) {
-        if (c0) gv[r] = v.v;
-        if ((cm >> r) & 1ull) tp[__popcll(cm & ((1ull << r) - 1ull))] = v.d;
+        double* ga = c0 ? gv + r : dump;
+        *ga = v.v;
+        const bool on = (cm >> r) & 1ull;
+        double* ta = on ? tp + __popcll(cm & ((1ull << r) - 1ull)) : dump;
+        *ta = v.d;
     }
     __device__ __forceinline__ void eq_row(int r, const awe::Dual& v) { emit(r, v); }
     __device__ __forceinline__ void ineq_row(int r, const awe::Dual& v) { emit(AWE_N_EQ + r, v); }
@@ -504,6 +509,7 @@ void ap2_interval_kernel(KArgs a) {
             sink.gv = gval + n * kGvalStride;
             sink.cm = ct->cmask[kind][c];
             sink.c0 = c == 0;
+            sink.dump = dfl + tid;   // dfl is first written in phase 2
             awe::Dual gamma(vt[2 + kPhiGamma], ((in.seedA >> kDirGamma) & 1ull) ? 1.0 : 0.0);
             LdsSubmodels sub{pre + n * kPreStride, in.seedA};
             awe::ap2_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0, sub);
