@@ -65,18 +65,25 @@ AWE_HD T wind_speed(const T& zz, const double* th) {
     return scale * exp((0.5 * p) * log(zz * zz + 1.0));
 }
 
-// One element of the 'multi' tether drag model (element.py:60-104, segment.py:38-65): the drag
-// of element e of n_el on the main tether, lumped onto the kite node with the reference's shape
-// factor.  The tether's lower end is the ground (q = dq = 0); its share of the drag is dropped.
+// Height of the midpoint of tether element e of n_el (element.py:60-104): the element runs from
+// the ground anchor (s = 0) to the kite (s = 1), lo = e / n_el, up = (e + 1) / n_el
 template <class T>
-AWE_HD void tether_element(int e, int n_el, const T* q, const T* v, const T& diam, const double* th,
-                           T out[3]) {
+AWE_HD T tether_element_height(int e, int n_el, const T& qz) {
+    const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
+    return (qz * up + qz * lo) / 2.0;
+}
+
+// One element of the 'multi' tether drag model (element.py:60-104, segment.py:38-65) given the
+// wind speed and air density at the element's midpoint: the drag of element e on the main
+// tether, lumped onto the kite node with the reference's shape factor.  The tether's lower end
+// is the ground (q = dq = 0); its share of the drag is dropped.
+template <class T>
+AWE_HD void tether_element_drag(int e, int n_el, const T* q, const T* v, const T& diam, const T& uw,
+                                const T& rho, const double* th, T out[3]) {
     const double ds = 1.0 / n_el;
     const double s0 = 0.5 * ds, step = ((1.0 - 0.5 * ds) - s0) / (n_el - 1);
     const double cd = th[AWE_TH_CD_TETHER];
     const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
-    T zz = (q[2] * up + q[2] * lo) / 2.0;
-    T uw = wind_speed(zz, th);
     T ue[3];
     ue[0] = uw - (v[0] * up + v[0] * lo) / 2.0;
     ue[1] = -((v[1] * up + v[1] * lo) / 2.0);
@@ -86,9 +93,16 @@ AWE_HD void tether_element(int e, int n_el, const T* q, const T* v, const T& dia
     for (int i = 0; i < 3; ++i) tv[i] = q[i] * up - q[i] * lo;
     T lpar = dot3(tv, ue) / un;
     T lperp = sqrt(dot3(tv, tv) - lpar * lpar + 1e-12);
-    T fac = cd * 0.5 * isa_density(zz, th) * un * diam * lperp;
+    T fac = cd * 0.5 * rho * un * diam * lperp;
     const double sg = (e == n_el - 1) ? (1.0 - 0.5 * ds) : (s0 + e * step);
     for (int i = 0; i < 3; ++i) out[i] = sg * (fac * ue[i]);
+}
+
+template <class T>
+AWE_HD void tether_element(int e, int n_el, const T* q, const T* v, const T& diam, const double* th,
+                           T out[3]) {
+    T zz = tether_element_height(e, n_el, q[2]);
+    tether_element_drag(e, n_el, q, v, diam, wind_speed(zz, th), isa_density(zz, th), th, out);
 }
 
 // Sub-models that depend on very few node variables (kite-height wind and density on q_z; the

@@ -439,37 +439,54 @@ void ap2_interval_kernel(KArgs a) {
     }
     __syncthreads();
 
-    // ---- phase 0b: sub-models, one (node, tether element, direction) per thread -----------
+    // ---- phase 0b: sub-models -------------------------------------------------------------
+    // stage A, one (node, height) per thread: wind speed and density at the kite and at every
+    // tether element midpoint, as functions of q_z; stage B, one (node, element, direction)
+    // per thread: the element's drag along q0..2, dq0..2, diam_t
 #ifndef AWE_EXP_SKIP_PRE
     {
         const double* s = a.cst + AWE_C_SCALING;
         const int n_el = (int)a.cst[AWE_C_N_ELEMENTS];
-        const int ntask = n_el * kPreDirs + 1;
-        double* scr = tang;   // [NN][n_el][7][6]
+        double* scr = tang;                                   // [NN][n_el][7][6]
+        double* atm = tang + NN * n_el * kPreDirs * 6;        // [NN][n_el][4]
+        for (int t = tid; t < NN * (n_el + 1); t += NT) {
+            const int n = t / (n_el + 1), e = t - n * (n_el + 1) - 1;
+            const awe::Dual qz = awe::Dual(wn[n * 64 + 2], 1.0) * s[2];
+            awe::Dual uw, rho;
+            double* o;
+            if (e < 0) {
+                awe::InlineSubmodels().kite_atmosphere(qz, th, uw, rho);
+                o = pre + n * kPreStride + 24;
+            } else {
+                const awe::Dual zz = awe::tether_element_height(e, n_el, qz);
+                uw = awe::wind_speed(zz, th);
+                rho = awe::isa_density(zz, th);
+                o = atm + (n * n_el + e) * 4;
+            }
+            o[0] = uw.v; o[1] = uw.d; o[2] = rho.v; o[3] = rho.d;
+        }
+        __syncthreads();
+        const int ntask = n_el * kPreDirs;
         for (int t = tid; t < NN * ntask; t += NT) {
             const int n = t / ntask, q = t - n * ntask;
             const double* w = wn + n * 64;
-            if (q < n_el * kPreDirs) {
-                const int e = q / kPreDirs, j = q - e * kPreDirs;
-                const int vj = pre_var(j);
-                awe::Dual qv[3], vv[3];
+            const int e = q / kPreDirs, j = q - e * kPreDirs;
+            const int vj = pre_var(j);
+            awe::Dual qv[3], vv[3];
 #pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    qv[i] = awe::Dual(w[i], vj == i ? 1.0 : 0.0) * s[i];
-                    vv[i] = awe::Dual(w[3 + i], vj == 3 + i ? 1.0 : 0.0) * s[3 + i];
-                }
-                awe::Dual diam = awe::Dual(w[kDirDiam], vj == kDirDiam ? 1.0 : 0.0) * s[kDirDiam];
-                awe::Dual c[3];
-                awe::tether_element(e, n_el, qv, vv, diam, th, c);
-                double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
-#pragma unroll
-                for (int i = 0; i < 3; ++i) { o[i] = c[i].v; o[3 + i] = c[i].d; }
-            } else {
-                awe::Dual uw, rho;
-                awe::InlineSubmodels().kite_atmosphere(awe::Dual(w[2], 1.0) * s[2], th, uw, rho);
-                double* o = pre + n * kPreStride;
-                o[24] = uw.v; o[25] = uw.d; o[26] = rho.v; o[27] = rho.d;
+            for (int i = 0; i < 3; ++i) {
+                qv[i] = awe::Dual(w[i], vj == i ? 1.0 : 0.0) * s[i];
+                vv[i] = awe::Dual(w[3 + i], vj == 3 + i ? 1.0 : 0.0) * s[3 + i];
             }
+            awe::Dual diam = awe::Dual(w[kDirDiam], vj == kDirDiam ? 1.0 : 0.0) * s[kDirDiam];
+            const double* at = atm + (n * n_el + e) * 4;
+            const double dz = vj == 2 ? 1.0 : 0.0;
+            const awe::Dual uw(at[0], dz * at[1]), rho(at[2], dz * at[3]);
+            awe::Dual c[3];
+            awe::tether_element_drag(e, n_el, qv, vv, diam, uw, rho, th, c);
+            double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { o[i] = c[i].v; o[3 + i] = c[i].d; }
         }
         __syncthreads();
         // element sums in element order (the order of the inline model)
@@ -905,10 +922,10 @@ int build_tables(awe_handle_s* h, int n_k, int d, const double* consts, int n_co
             ct.obj_power[dir] = ct.off[1][c] + __builtin_popcountll(cm & ((1ull << kRowPower) - 1ull));
     }
     h->tang_total = ct.tsize[0] + d * ct.tsize[1];
-    {   // the tangent buffer doubles as sub-model scratch [NN][n_el][7][6] in phase 0
+    {   // the tangent buffer doubles as sub-model scratch [NN][n_el][7][6] + [NN][n_el][4]
         const int n_el = (int)h->cst[AWE_C_N_ELEMENTS];
         if (n_el < 1 || n_el > 64) return fail(AWE_ERR_ARG, "tether elements must be in 1..64");
-        h->tang_total = std::max(h->tang_total, NN * n_el * 7 * 6);
+        h->tang_total = std::max(h->tang_total, NN * n_el * (7 * 6 + 4));
     }
 
     // ---- target columns of each (k, node, direction) ------------------------------------
