@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libawegpu.so")
 SOURCES = [os.path.join(CSRC, "awegpu.hip")]
-HEADERS = [os.path.join(CSRC, f) for f in ("ap2_model.hpp", "scalar.hpp")] + [
+HEADERS = [os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
     os.path.join(os.path.dirname(HERE), "include", "awegpu.h")]
 ARCH = os.environ.get("AWE_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wno-unused-value",

@@ -11,9 +11,14 @@ over ranks is reported.  `value` = evaluations/s of the whole job.
 Also reported:
   roofline     -- the dominant kernel (ap2_interval_kernel): algorithmic HBM bytes per launch
                   (SURVEY 8(d) formula with the exact nnz, x B) / its mean duration from HIP events
-                  on the launch stream, against 8 TB/s;
-  cpu_baseline -- the CPU oracle (PyTorch float64 restatement, "port"; the reference CasADi/IPOPT
-                  stack cannot be installed) on a bounded sample, rank 0, N=1 only.
+                  on the launch stream, against 8 TB/s.  `traffic` is the HBM byte rate from the
+                  rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE passes recorded in
+                  profiles/pmc_traffic.json, used only when that record was taken for the same
+                  kernel sources and batch size (else null); the same record carries the FP64
+                  VALU instruction counts behind `fp64`.
+  cpu_baseline -- the CPU port of the evaluator (oracle/cpu, C++ with OpenMP over (instance,
+                  interval), "port"; the reference CasADi/IPOPT stack cannot be installed) on a
+                  bounded sample, rank 0, N=1 only, at all host threads and at one thread.
 """
 from __future__ import annotations
 
@@ -28,6 +33,33 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X spec (MI355X_MICROARCH.md); 6.3 TB/s measured float4 copy
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector spec
+PMC_RECORD = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def kernel_source_hash() -> str:
+    """Hash of the evaluator sources: a PMC record is only valid for the code it was taken on."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "awebox_amd", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".hip", ".hpp")):
+            with open(os.path.join(csrc, name), "rb") as fh:
+                h.update(name.encode() + fh.read())
+    with open(os.path.join(ROOT, "include", "awegpu.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_record(batch: int):
+    """The committed PMC record for these sources and batch size, or None."""
+    try:
+        with open(PMC_RECORD) as fh:
+            rec = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if rec.get("source_hash") != kernel_source_hash() or rec.get("batch") != batch:
+        return None
+    return rec
 
 
 def main():
@@ -36,7 +68,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512, help="NLP instances per step and GPU")
-    ap.add_argument("--cpu-sample", type=int, default=4, help="oracle evaluations in the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per thread setting")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -146,37 +178,54 @@ def main():
                      "finalize_ms": float(np.mean(fms)), "bytes_per_eval": bytes_per_eval},
         "outputs_finite": finite,
     }
+    rec = pmc_record(B)
+    if rec is not None:
+        hbm_bytes = 2.0 * rec["FETCH_SIZE_kB"] * 1024 + rec["WRITE_SIZE_kB"] * 1024
+        line["roofline"]["traffic"] = hbm_bytes / (kernel_ms * 1e-3) / 1e9
+        line["roofline"]["traffic_bytes_per_launch"] = hbm_bytes
+        flops = 64.0 * (rec["SQ_INSTS_VALU_ADD_F64"] + rec["SQ_INSTS_VALU_MUL_F64"] +
+                        2.0 * rec["SQ_INSTS_VALU_FMA_F64"] + rec["SQ_INSTS_VALU_TRANS_F64"])
+        tf = flops / (kernel_ms * 1e-3) / 1e12
+        line["fp64"] = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                        "flops_per_launch": flops, "note": "FP64 VALU instructions x 64 lanes (FMA = 2), "
+                        "from the PMC record; idle lanes of issued instructions count"}
+        line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(consts, lay, v0, args.cpu_sample)
+        line["cpu_baseline"] = cpu_baseline(consts, lay, v0, args.cpu_seconds)
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(consts, lay, v0, n):
-    """Time the CPU oracle (test infrastructure, never the product) on the host cores."""
-    import torch
+def cpu_baseline(consts, lay, v0, seconds):
+    """Time the CPU port of the evaluator (test/baseline infrastructure, never the product) on
+    the host cores: all threads OpenMP grants (OMP_NUM_THREADS), and one thread."""
+    import numpy as np
 
     from awebox_amd import problem as pb
     from awebox_amd.initial_guess import batch_member
-    from oracle.ap2_oracle import from_problem
+    from oracle.cpu_port import CpuPort
 
-    orc = from_problem(consts)
-    P = pb.pack_p(lay, consts, v0)
-    V = batch_member(v0, lay, 0)
-    # warm-up (first-call overheads of torch.func)
-    orc.nlp_g(V, P, lay, pb.THETA0_OFF)
-    t0 = time.perf_counter()
-    for b in range(n):
-        V = batch_member(v0, lay, b)
-        orc.nlp_f(V, P, lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES)
-        orc.nlp_g(V, P, lay, pb.THETA0_OFF)
-        orc.nlp_grad_f(V, P, lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES)
-        orc.nlp_jac_g(V, P, lay, pb.THETA0_OFF)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "evals/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} full evaluations (f, g, grad f, J_g) of the AP2 N=40 d=4 NLP by the PyTorch "
-                      f"float64 oracle, {dt:.1f} s"}
+    port = CpuPort(consts)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+
+    def rate(B, nthreads):
+        V = np.stack([batch_member(v0, lay, b) for b in range(B)])
+        P = np.stack([pb.pack_p(lay, consts, v0)] * B)
+        port.eval_nlp(V, P, threads=nthreads)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            port.eval_nlp(V, P, threads=nthreads)
+            n += B
+        return n / (time.perf_counter() - t0), n
+
+    all_rate, n_all = rate(max(4 * threads, 16), threads)
+    one_rate, n_one = rate(8, 1)
+    return {"value": all_rate, "unit": "evals/s", "cores": threads, "kind": "port",
+            "value_1core": one_rate,
+            "sample": f"C++ CPU port of the evaluator (oracle/cpu, vector-dual forward mode, OpenMP over "
+                      f"(instance, interval)): {n_all} evaluations (f, g, grad f, J_g) of the AP2 N=40 d=4 NLP "
+                      f"on {threads} threads and {n_one} on 1 thread, ~{seconds:.0f} s each"}
 
 
 if __name__ == "__main__":
