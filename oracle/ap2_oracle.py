@@ -566,6 +566,135 @@ class Ap2Oracle:
                    + comp["theta_regularisation"] + beta_cost + time_cost)
         return psi * comp["tracking"] + (1. - psi) * power_cost + general + homotopy
 
+    # ---- per-interval objective and the Hessian of the Lagrangian -----------------------
+    def objective_parts(self, P, layout, theta0_offsets, cost_names):
+        """Effective regularisation weights (objective.py:147-170) and category index sets."""
+        P = torch.as_tensor(P)
+        cost = {n: P[layout.p_cost + i] for i, n in enumerate(cost_names)}
+        weights = P[layout.p_weights:layout.p_weights + NW]
+        c = self.c
+        cats = {"tracking": [], "xdot_regularisation": [], "u_regularisation": [], "fictitious": [],
+                "theta_regularisation": []}
+        for (vt, n), sl in IDX.items():
+            if vt in ("x", "z"):
+                cat = "tracking"
+            elif vt == "xdot":
+                cat = "xdot_regularisation"
+            elif vt == "u":
+                cat = "fictitious" if n in ("f_fict10", "m_fict10") else "u_regularisation"
+            else:
+                cat = None if n == "t_f" else "theta_regularisation"
+            if cat is not None:
+                cats[cat].extend(range(sl.start, sl.stop))
+        norm_of = {"tracking": c["norm_tracking"], "xdot_regularisation": c["norm_xdot_reg"],
+                   "u_regularisation": c["norm_u_reg"], "fictitious": c["norm_fictitious"],
+                   "theta_regularisation": c["norm_theta_reg"]}
+        w_eff = weights.clone()
+        for cat, ids in cats.items():
+            ids_t = torch.as_tensor(ids)
+            w_eff = w_eff.index_put((ids_t,), weights[ids_t] * cost[cat] / norm_of[cat])
+        track = torch.zeros(2, NW, dtype=torch.float64)      # [tracking mask, other-category mask]
+        track[0, torch.as_tensor(cats["tracking"])] = 1.0
+        for cat, ids in cats.items():
+            if cat != "tracking":
+                track[1, torch.as_tensor(ids)] = 1.0
+        return cost, w_eff, track
+
+    def interval_objective(self, wloc, rloc, w_eff, track, cost, th):
+        """The objective terms of one interval's Radau nodes (objective.py:45-544: regularisation,
+        beta cost, power cost through the integral output, collocation.py:272-316) as a function
+        of the interval's local V slice ``wloc`` (layout of ``interval_rows``); ``rloc`` is the
+        same slice of P.p.ref.  Summed over intervals and added to the time and homotopy costs
+        this is ``nlp_f``."""
+        d = self.d
+        nx, nu = 23, 10
+        theta, phi = wloc[0:2], wloc[2:9]
+        psi, gamma = phi[3], phi[0]
+        tf = theta[1]
+        h = 1.0 / self.n_k
+        C = torch.as_tensor(self.C)
+
+        def split(v):
+            o = 9
+            xk = v[o:o + nx]; o += nx
+            uk = v[o:o + nu]; o += nu
+            o += nx + 1
+            cx, cz = [], []
+            for _ in range(d):
+                cx.append(v[o:o + nx]); o += nx
+                cz.append(v[o:o + 1]); o += 1
+            return xk, uk, cx, cz
+
+        xk, uk, cx, cz = split(wloc)
+        _, ru, rcx, rcz = split(rloc)
+        X = [xk] + cx
+        Wn, Rn = [], []
+        for j in range(d):
+            xp = sum(C[r, j + 1] * X[r] for r in range(d + 1))
+            Wn.append(torch.cat([cx[j], xp / h / tf, uk, cz[j], theta]))
+            Rn.append(torch.cat([rcx[j], torch.zeros(nx, dtype=wloc.dtype), ru, rcz[j], rloc[0:2]]))
+        Wn, Rn = torch.stack(Wn), torch.stack(Rn)
+        wj = torch.as_tensor(np.asarray(self.w))
+        reg = wj[:, None] * w_eff[None, :] * (Wn - Rn) ** 2
+        f_track = (reg * track[0][None, :]).sum()
+        f_other = (reg * track[1][None, :]).sum()     # t_f is not regularised
+        eq, ineq, power, beta = vmap(self.node, in_dims=(0, None, None))(Wn, gamma, th)
+        Lam = torch.as_tensor(np.linalg.solve(self.C[1:, 1:], np.eye(d)))
+        Dc = torch.as_tensor(self.D)
+        io = tf / self.n_k * (Lam.T @ power)
+        e_k = sum(Dc[j + 1] * io[j] for j in range(d))
+        power_cost = cost["power"] * (-1.) * e_k / tf
+        beta_cost = cost["beta"] * (wj * beta ** 2).sum() / self.c["norm_beta"]
+        return psi * f_track + (1. - psi) * power_cost + f_other + beta_cost
+
+    def nlp_f_by_interval(self, V, P, layout, theta0_offsets, cost_names, phi_names):
+        """nlp_f assembled from interval_objective (checked against nlp_f in the tests)."""
+        V = torch.as_tensor(V)
+        P = torch.as_tensor(P)
+        th = self.unpack_theta0(P[layout.p_theta0:], theta0_offsets)
+        cost, w_eff, track = self.objective_parts(P, layout, theta0_offsets, cost_names)
+        idx = torch.as_tensor(np.stack([self.local_index(layout, k) for k in range(self.n_k)]))
+        vref = P[layout.p_ref:layout.p_ref + layout.n_v]
+        fk = vmap(self.interval_objective, in_dims=(0, 0, None, None, None, None))(V[idx], vref[idx], w_eff,
+                                                                                 track, cost, th)
+        tf, tf_ref = V[layout.theta()[1]], vref[layout.theta()[1]]
+        phi = V[torch.as_tensor(layout.phi())]
+        homotopy = sum(cost[n] * phi[i] for i, n in enumerate(phi_names))
+        return fk.sum() + cost["t_f"] * (tf - tf_ref) ** 2 + homotopy
+
+    def nlp_hess_l(self, V, P, sigma, lam_g, layout, theta0_offsets, cost_names, phi_names):
+        """Hessian of sigma f + lam_g^T g (nlp_hess_l) as a full symmetric scipy CSC matrix.
+
+        Continuity and periodicity rows are linear; every other row and every objective term
+        lives in one interval, so the Hessian is the sum of per-interval blocks (torch.func
+        hessian of lam_k^T interval_rows + sigma interval_objective) plus the time cost."""
+        import scipy.sparse as sp
+        from torch.func import hessian
+        V = torch.as_tensor(V)
+        P = torch.as_tensor(P)
+        lam_g = torch.as_tensor(lam_g)
+        th = self.unpack_theta0(P[layout.p_theta0:], theta0_offsets)
+        cost, w_eff, track = self.objective_parts(P, layout, theta0_offsets, cost_names)
+        idx = np.stack([self.local_index(layout, k) for k in range(self.n_k)])
+        it = torch.as_tensor(idx)
+        vref = P[layout.p_ref:layout.p_ref + layout.n_v]
+        R = layout.rows_per_interval
+        lam_k = lam_g[:self.n_k * R].reshape(self.n_k, R)
+
+        def lag(wl, rl, lk):
+            return lk @ self.interval_rows(wl, th) + sigma * self.interval_objective(wl, rl, w_eff, track,
+                                                                                     cost, th)
+
+        Hk = vmap(hessian(lag), in_dims=(0, 0, 0))(V[it], vref[it], lam_k).numpy()   # [n_k, 185, 185]
+        n = layout.n_v
+        rows = np.repeat(idx[:, :, None], idx.shape[1], axis=2)
+        cols = np.repeat(idx[:, None, :], idx.shape[1], axis=1)
+        H = sp.csc_matrix((Hk.ravel(), (rows.ravel(), cols.ravel())), shape=(n, n))
+        itf = layout.theta()[1]
+        H = H + sp.csc_matrix(([2.0 * float(sigma) * float(cost["t_f"])], ([itf], [itf])), shape=(n, n))
+        H.eliminate_zeros()
+        return H
+
     def nlp_grad_f(self, V, P, layout, theta0_offsets, cost_names, phi_names):
         V = torch.as_tensor(V)
         return grad(lambda v: self.nlp_f(v, P, layout, theta0_offsets, cost_names, phi_names))(V)
