@@ -496,4 +496,310 @@ inline int build_ap2_tables(int n_k, int d, const double* consts, int n_consts, 
     return AWE_OK;
 }
 
+
+// =========================================================================================
+// Hessian of the Lagrangian (nlp_hess_l)
+// =========================================================================================
+
+// Structural second-order dependency: d = variables the value depends on, h[i] bit j = the value
+// has a (possibly) nonzero second derivative in (i, j).  Propagated through the node model like
+// Dep; what CasADi's symbolic Hessian sparsity provides in the reference.
+struct HDep {
+    unsigned long long d = 0;
+    unsigned long long h[64] = {};
+    HDep() = default;
+    HDep(double) {}
+    static HDep var(int i) { HDep x; x.d = 1ull << i; return x; }
+};
+inline void hdep_cross(HDep& r, unsigned long long a, unsigned long long b) {
+    for (int i = 0; i < 64; ++i) {
+        if ((a >> i) & 1ull) r.h[i] |= b;
+        if ((b >> i) & 1ull) r.h[i] |= a;
+    }
+}
+inline HDep hdep_lin(const HDep& x, const HDep& y) {
+    HDep r; r.d = x.d | y.d;
+    for (int i = 0; i < 64; ++i) r.h[i] = x.h[i] | y.h[i];
+    return r;
+}
+inline HDep hdep_nl(const HDep& x) { HDep r = x; hdep_cross(r, x.d, x.d); return r; }
+inline HDep operator+(const HDep& x, const HDep& y) { return hdep_lin(x, y); }
+inline HDep operator-(const HDep& x, const HDep& y) { return hdep_lin(x, y); }
+inline HDep operator-(const HDep& x) { return x; }
+inline HDep operator*(const HDep& x, const HDep& y) { HDep r = hdep_lin(x, y); hdep_cross(r, x.d, y.d); return r; }
+inline HDep operator/(const HDep& x, const HDep& y) {
+    HDep r = hdep_lin(x, y); hdep_cross(r, x.d, y.d); hdep_cross(r, y.d, y.d); return r;
+}
+inline HDep operator+(const HDep& x, double) { return x; }
+inline HDep operator+(double, const HDep& y) { return y; }
+inline HDep operator-(const HDep& x, double) { return x; }
+inline HDep operator-(double, const HDep& y) { return y; }
+inline HDep operator*(const HDep& x, double) { return x; }
+inline HDep operator*(double, const HDep& y) { return y; }
+inline HDep operator/(const HDep& x, double) { return x; }
+inline HDep operator/(double, const HDep& y) { return hdep_nl(y); }
+inline HDep sqrt(const HDep& x) { return hdep_nl(x); }
+inline HDep exp(const HDep& x) { return hdep_nl(x); }
+inline HDep log(const HDep& x) { return hdep_nl(x); }
+
+constexpr int kHRows = 35;              // node rows incl. power (33) and beta (34)
+constexpr int kHTypeA = 0, kHTypeB = 1, kHTypeC = 2;
+
+// Gather term of one V-space Hessian entry (bits 31..30 type):
+//   A: scale[sa] scale[sb] Hdir_n[pidx]          n 27..29, pidx 14..26, sa 7..13, sb 0..6
+//   B: G[n][i] (-C[r][n] / (h tf^2))              n 27..29, i 22..26, r 19..21
+//   C: sum_i G[n][i] 2 xdot_i / tf^2  (t_f, t_f)  n 27..29
+inline unsigned hterm_a(int n, int pidx, int sa, int sb) {
+    return ((unsigned)kHTypeA << 30) | ((unsigned)n << 27) | ((unsigned)pidx << 14) | ((unsigned)sa << 7) | (unsigned)sb;
+}
+inline unsigned hterm_b(int n, int i, int r) {
+    return ((unsigned)kHTypeB << 30) | ((unsigned)n << 27) | ((unsigned)i << 22) | ((unsigned)r << 19);
+}
+inline unsigned hterm_c(int n) { return ((unsigned)kHTypeC << 30) | ((unsigned)n << 27); }
+
+struct HessTabs {                       // device-visible part
+    int npairs[2];                      // direction pairs per node kind
+    short pidx[2][kDirs][kDirs];        // compact index of the (unordered) direction pair, -1
+    signed char pdir[2][kHalf][kHRows + 1];   // direction of colour c that owns row r, -1
+    int ntask[2];
+    int task_off[2];                    // offsets into the task list (c1 | c2 << 8)
+};
+
+struct Ap2HessTables {
+    HessTabs ht{};
+    std::vector<int> tasks;             // per kind: colour pairs c1 <= c2
+    std::vector<int> colind, row;       // upper-triangular CCS of the V-space Hessian
+    int nnz = 0;
+    std::vector<int> slot0, nslot;      // [n_k] the interval's contiguous CCS range
+    std::vector<int> gslot;             // CCS slots of the global-global entries
+    std::vector<int> ent_off;           // [n_k + 1] entries of each interval (local slots, then globals)
+    std::vector<int> term_off;          // [n_entries + 1] into terms
+    std::vector<unsigned> terms;
+    int max_pairs = 0;
+};
+
+// V columns (with gather-scale index) that direction `dir` of node `node` of interval k feeds
+inline void direction_columns(const Layout& L, int d, int k, int node, int dir,
+                              std::vector<std::pair<int, int>>& cols) {
+    const int NN = d + 1;
+    cols.clear();
+    if (dir == kDirPsi) { cols.emplace_back(L.phi(kPhiPsi), 0); return; }
+    if (dir == kDirGamma) { cols.emplace_back(L.phi(kPhiGamma), 0); return; }
+    if (dir >= 2 * AWE_NX + AWE_NU + AWE_NZ) { cols.emplace_back(L.theta(dir - (2 * AWE_NX + AWE_NU + AWE_NZ)), 0); return; }
+    if (dir >= 2 * AWE_NX && dir < 2 * AWE_NX + AWE_NU) { cols.emplace_back(L.u(k, dir - 2 * AWE_NX), 0); return; }
+    if (node == 0) {
+        if (dir < AWE_NX) cols.emplace_back(L.x(k, dir), 0);
+        else if (dir < 2 * AWE_NX) cols.emplace_back(L.xdot(k, dir - AWE_NX), 0);
+        else cols.emplace_back(L.z(k), 0);
+        return;
+    }
+    if (dir < AWE_NX) { cols.emplace_back(L.coll_x(k, node - 1, dir), 0); return; }
+    if (dir < 2 * AWE_NX) {
+        for (int r = 0; r < NN; ++r)
+            if (r != node) cols.emplace_back(L.X(k, r, dir - AWE_NX), 1 + r * NN + node);
+        return;
+    }
+    cols.emplace_back(L.coll_z(k, node - 1), 0);
+}
+
+inline int build_hess_tables(const Ap2Tables& T, Ap2HessTables& H, std::string& err) {
+    const Layout& L = T.lay;
+    const ColorTabs& ct = T.ct;
+    const int n_k = T.n_k, d = T.d, NN = d + 1;
+    HessTabs& ht = H.ht;
+    std::memset(&ht, 0, sizeof(ht));
+    std::memset(ht.pidx, 0xff, sizeof(ht.pidx));
+    std::memset(ht.pdir, 0xff, sizeof(ht.pdir));
+
+    // ---- second-order structure of every node row, over the node variables + gamma ---------
+    struct HSink {
+        HDep rows[kHRows];
+        void eq_row(int r, const HDep& v) { rows[r] = v; }
+        void ineq_row(int r, const HDep& v) { rows[AWE_N_EQ + r] = v; }
+        void power(const HDep& v) { rows[kRowPower] = v; }
+        void beta(const HDep& v) { rows[kRowBeta] = v; }
+    };
+    struct HIn { HDep operator()(int i) const { return HDep::var(i); } };
+    std::vector<double> th(AWE_NTHETA0, 1.0);
+    HSink hs;
+    awe::ap2_node<HDep>(HIn{}, HDep::var(kDirGamma), th.data(), T.cst.data(), hs, true);
+
+    // node variables each direction seeds
+    auto dvars = [&](int kind, int dir) {
+        unsigned long long m = 0;
+        if (dir > kDirGamma) return m;
+        if (kind == 0) return 1ull << dir;
+        if (dir < AWE_NX) return (1ull << dir) | (1ull << (AWE_NX + dir));
+        if (dir == kDirTf) {
+            for (int i = 0; i < AWE_NX; ++i) m |= 1ull << (AWE_NX + i);
+            return m;
+        }
+        return 1ull << dir;
+    };
+    auto row_used = [&](int kind, int r) {
+        if (kind == 0) return r < kRowPower;
+        return r < AWE_N_EQ || r == kRowPower || r == kRowBeta;
+    };
+    auto interacts = [&](int r, unsigned long long va, unsigned long long vb) {
+        for (int u = 0; u < 64; ++u)
+            if (((va >> u) & 1ull) && (hs.rows[r].h[u] & vb)) return true;
+        return false;
+    };
+    std::vector<std::vector<std::pair<int, int>>> pairs(2);
+    std::vector<std::vector<char>> has(2, std::vector<char>(kDirs * kDirs, 0));
+    auto add_pair = [&](int kind, int p, int q) {
+        if (p > q) std::swap(p, q);
+        if (!has[kind][p * kDirs + q]) { has[kind][p * kDirs + q] = 1; pairs[kind].emplace_back(p, q); }
+    };
+    std::vector<int> task_set[2];
+    for (int kind = 0; kind < 2; ++kind) {
+        std::vector<char> tk(kHalf * kHalf, 0);
+        for (int r = 0; r < kHRows; ++r) {
+            if (!row_used(kind, r)) continue;
+            for (int p = 0; p <= kDirGamma; ++p)
+                for (int q = p; q <= kDirGamma; ++q) {
+                    const unsigned long long vp = dvars(kind, p), vq = dvars(kind, q);
+                    if (!vp || !vq || !interacts(r, vp, vq)) continue;
+                    const int cp = ct.dcolor[kind][p], cq = ct.dcolor[kind][q];
+                    if (cp < 0 || cq < 0 || !((ct.dmask[kind][p] >> r) & 1ull) || !((ct.dmask[kind][q] >> r) & 1ull)) {
+                        err = "internal: Hessian structure outside the first-order pattern";
+                        return AWE_ERR_ARG;
+                    }
+                    add_pair(kind, p, q);
+                    tk[std::min(cp, cq) * kHalf + std::max(cp, cq)] = 1;
+                }
+        }
+        for (int c1 = 0; c1 < kHalf; ++c1)
+            for (int c2 = c1; c2 < kHalf; ++c2)
+                if (tk[c1 * kHalf + c2]) task_set[kind].push_back(c1 | (c2 << 8));
+    }
+    // objective terms at Radau nodes (objective.py; see the kernel's objective Hessian pass)
+    {
+        const int kind = 1;
+        for (int i = 0; i < AWE_NX; ++i) {
+            add_pair(kind, i, i);
+            add_pair(kind, i, AWE_NX + i);
+            add_pair(kind, i, kDirTf);
+            add_pair(kind, AWE_NX + i, AWE_NX + i);
+            add_pair(kind, AWE_NX + i, kDirTf);
+            add_pair(kind, i, kDirPsi);
+        }
+        add_pair(kind, kDirTf, kDirTf);
+        for (int i = 2 * AWE_NX; i <= kDirDiam; ++i) add_pair(kind, i, i);
+        add_pair(kind, kDirZ, kDirPsi);
+        std::vector<int> bdirs, pdirs;
+        for (int p = 0; p <= kDirGamma; ++p) {
+            if ((ct.dmask[1][p] >> kRowBeta) & 1ull) bdirs.push_back(p);
+            if ((ct.dmask[1][p] >> kRowPower) & 1ull) pdirs.push_back(p);
+        }
+        for (size_t a = 0; a < bdirs.size(); ++a)
+            for (size_t b = a; b < bdirs.size(); ++b) add_pair(kind, bdirs[a], bdirs[b]);
+        for (int p : pdirs) add_pair(kind, p, kDirPsi);
+    }
+    for (int kind = 0; kind < 2; ++kind) {
+        std::sort(pairs[kind].begin(), pairs[kind].end());
+        ht.npairs[kind] = (int)pairs[kind].size();
+        if (ht.npairs[kind] >= 8192) { err = "internal: too many Hessian direction pairs"; return AWE_ERR_ARG; }
+        for (int i = 0; i < ht.npairs[kind]; ++i) {
+            const int p = pairs[kind][i].first, q = pairs[kind][i].second;
+            ht.pidx[kind][p][q] = ht.pidx[kind][q][p] = (short)i;
+        }
+        for (int dir = 0; dir < kDirs; ++dir) {
+            const int c = ct.dcolor[kind][dir];
+            if (c < 0) continue;
+            for (int r = 0; r < kHRows; ++r)
+                if ((ct.dmask[kind][dir] >> r) & 1ull) ht.pdir[kind][c][r] = (signed char)dir;
+        }
+        ht.task_off[kind] = (int)H.tasks.size();
+        ht.ntask[kind] = (int)task_set[kind].size();
+        H.tasks.insert(H.tasks.end(), task_set[kind].begin(), task_set[kind].end());
+    }
+    H.max_pairs = std::max(ht.npairs[0], ht.npairs[1]);
+
+    // ---- V-space entries and their gather terms ----------------------------------------------
+    auto is_global = [&](int col) { return col < L.v_int0; };
+    std::vector<std::pair<long long, unsigned>> ent;   // (key = col * n_v + row, term), with the interval
+    std::vector<int> ent_k;
+    std::vector<std::pair<int, int>> ca, cb;
+    const int itf = L.theta(1);
+    for (int k = 0; k < n_k; ++k)
+        for (int node = 0; node < NN; ++node) {
+            const int kind = node > 0;
+            for (const auto& pq : pairs[kind]) {
+                const int p = pq.first, q = pq.second;
+                const int pi = ht.pidx[kind][p][q];
+                direction_columns(L, d, k, node, p, ca);
+                direction_columns(L, d, k, node, q, cb);
+                for (size_t a = 0; a < ca.size(); ++a)
+                    for (size_t b = (p == q ? a : 0); b < cb.size(); ++b) {
+                        int r0 = ca[a].first, c0 = cb[b].first, sa = ca[a].second, sb = cb[b].second;
+                        if (r0 > c0) { std::swap(r0, c0); std::swap(sa, sb); }
+                        ent.emplace_back((long long)c0 * L.n_v + r0, hterm_a(node, pi, sa, sb));
+                        ent_k.push_back(k);
+                    }
+            }
+            if (node == 0) continue;
+            for (int i = 0; i < AWE_NX; ++i)
+                for (int r = 0; r < NN; ++r) {
+                    const int col = L.X(k, r, i);
+                    ent.emplace_back((long long)col * L.n_v + itf, hterm_b(node, i, r));
+                    ent_k.push_back(k);
+                }
+            ent.emplace_back((long long)itf * L.n_v + itf, hterm_c(node));
+            ent_k.push_back(k);
+        }
+    // CCS pattern (upper triangle, column-major) and per-interval slot ranges
+    std::vector<long long> keys;
+    keys.reserve(ent.size());
+    for (auto& e : ent) keys.push_back(e.first);
+    keys.push_back((long long)itf * L.n_v + itf);            // time cost (t_f, t_f)
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    H.nnz = (int)keys.size();
+    H.colind.assign(L.n_v + 1, 0);
+    H.row.resize(H.nnz);
+    for (int i = 0; i < H.nnz; ++i) {
+        H.colind[keys[i] / L.n_v + 1]++;
+        H.row[i] = (int)(keys[i] % L.n_v);
+    }
+    for (int c = 0; c < L.n_v; ++c) H.colind[c + 1] += H.colind[c];
+    auto slot_of = [&](long long key) {
+        return (int)(std::lower_bound(keys.begin(), keys.end(), key) - keys.begin());
+    };
+    for (int c = 0; c < L.v_int0; ++c)
+        for (int s = H.colind[c]; s < H.colind[c + 1]; ++s) H.gslot.push_back(s);
+    const int ng = (int)H.gslot.size();
+    H.slot0.resize(n_k);
+    H.nslot.resize(n_k);
+    for (int k = 0; k < n_k; ++k) {
+        H.slot0[k] = H.colind[L.x(k, 0)];
+        H.nslot[k] = (k == n_k - 1 ? H.nnz : H.colind[L.x(k + 1, 0)]) - H.slot0[k];
+    }
+    // terms per (interval, entry): entries 0..nslot-1 are the local slots, then ng globals
+    std::vector<std::vector<unsigned>> bucket;
+    H.ent_off.assign(n_k + 1, 0);
+    for (int k = 0; k < n_k; ++k) H.ent_off[k + 1] = H.ent_off[k] + H.nslot[k] + ng;
+    bucket.resize(H.ent_off[n_k]);
+    for (size_t e = 0; e < ent.size(); ++e) {
+        const int k = ent_k[e];
+        const int slot = slot_of(ent[e].first);
+        const int col = (int)(ent[e].first / L.n_v);
+        int idx;
+        if (is_global(col)) {
+            idx = (int)(std::find(H.gslot.begin(), H.gslot.end(), slot) - H.gslot.begin());
+            idx += H.nslot[k];
+        } else {
+            idx = slot - H.slot0[k];
+            if (idx < 0 || idx >= H.nslot[k]) { err = "internal: Hessian entry outside its interval"; return AWE_ERR_ARG; }
+        }
+        bucket[H.ent_off[k] + idx].push_back(ent[e].second);
+    }
+    H.term_off.assign(bucket.size() + 1, 0);
+    for (size_t i = 0; i < bucket.size(); ++i) {
+        H.term_off[i + 1] = H.term_off[i] + (int)bucket[i].size();
+        H.terms.insert(H.terms.end(), bucket[i].begin(), bucket[i].end());
+    }
+    return AWE_OK;
+}
+
 }  // namespace awt

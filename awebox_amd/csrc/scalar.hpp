@@ -4,6 +4,7 @@
 //   Dual    -- forward-mode derivative along ONE direction; on the GPU every lane of a
 //              wavefront carries a different direction, so one wavefront produces a full
 //              node Jacobian block
+//   HDual   -- hyper-dual number: mixed second derivative along two directions (Hessian)
 //   Dep     -- structural dependency bitmask over <= 64 node inputs; used once on the host to
 //              derive the fixed CCS sparsity of the constraint Jacobian (what CasADi's
 //              symbolic sparsity propagation provides in the reference, preparation.py:366-400)
@@ -84,6 +85,57 @@ AWE_HD Dual exp(Dual a) {
 AWE_HD Dual log(Dual a) { return Dual(::log(a.v), a.d * rcp(a.v)); }
 AWE_HD double value(Dual a) { return a.v; }
 AWE_HD double tangent(Dual a) { return a.d; }
+
+// ------------------------------------------------------------------------------------------
+// Hyper-dual number v + a e1 + b e2 + ab e1 e2 (e1^2 = e2^2 = 0): forward-over-forward second
+// derivatives.  With e1, e2 seeded along two directions, ab is the mixed second derivative.
+struct HDual {
+    double v, a, b, ab;
+    AWE_HD HDual() : v(0.0), a(0.0), b(0.0), ab(0.0) {}
+    AWE_HD HDual(double x) : v(x), a(0.0), b(0.0), ab(0.0) {}
+    AWE_HD HDual(double x, double xa, double xb, double xab) : v(x), a(xa), b(xb), ab(xab) {}
+};
+AWE_HD HDual operator+(HDual x, HDual y) { return HDual(x.v + y.v, x.a + y.a, x.b + y.b, x.ab + y.ab); }
+AWE_HD HDual operator-(HDual x, HDual y) { return HDual(x.v - y.v, x.a - y.a, x.b - y.b, x.ab - y.ab); }
+AWE_HD HDual operator-(HDual x) { return HDual(-x.v, -x.a, -x.b, -x.ab); }
+AWE_HD HDual operator*(HDual x, HDual y) {
+    return HDual(x.v * y.v, x.a * y.v + x.v * y.a, x.b * y.v + x.v * y.b,
+                 x.ab * y.v + x.a * y.b + x.b * y.a + x.v * y.ab);
+}
+// f(x) for a scalar function with value f0 and derivatives f1, f2 at x.v (chain rule)
+AWE_HD HDual hd_apply(HDual x, double f0, double f1, double f2) {
+    return HDual(f0, f1 * x.a, f1 * x.b, f1 * x.ab + f2 * x.a * x.b);
+}
+AWE_HD HDual operator/(HDual x, HDual y) {
+    const double r = rcp(y.v);
+    return x * hd_apply(y, r, -r * r, 2.0 * r * r * r);
+}
+AWE_HD HDual operator+(HDual x, double y) { return HDual(x.v + y, x.a, x.b, x.ab); }
+AWE_HD HDual operator+(double x, HDual y) { return HDual(x + y.v, y.a, y.b, y.ab); }
+AWE_HD HDual operator-(HDual x, double y) { return HDual(x.v - y, x.a, x.b, x.ab); }
+AWE_HD HDual operator-(double x, HDual y) { return HDual(x - y.v, -y.a, -y.b, -y.ab); }
+AWE_HD HDual operator*(HDual x, double y) { return HDual(x.v * y, x.a * y, x.b * y, x.ab * y); }
+AWE_HD HDual operator*(double x, HDual y) { return HDual(x * y.v, x * y.a, x * y.b, x * y.ab); }
+AWE_HD HDual operator/(HDual x, double y) {
+    const double r = __builtin_constant_p(y) ? 1.0 / y : rcp(y);
+    return x * r;
+}
+AWE_HD HDual operator/(double x, HDual y) {
+    const double r = rcp(y.v);
+    return x * hd_apply(y, r, -r * r, 2.0 * r * r * r);
+}
+AWE_HD HDual sqrt(HDual x) {
+    const double s = ::sqrt(x.v), r = rcp(s);
+    return hd_apply(x, s, 0.5 * r, -0.25 * r * r * r);
+}
+AWE_HD HDual exp(HDual x) {
+    const double e = ::exp(x.v);
+    return hd_apply(x, e, e, e);
+}
+AWE_HD HDual log(HDual x) {
+    const double r = rcp(x.v);
+    return hd_apply(x, ::log(x.v), r, -r * r);
+}
 
 // ------------------------------------------------------------------------------------------
 struct Dep {

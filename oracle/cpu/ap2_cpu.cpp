@@ -70,20 +70,50 @@ struct CpuSink {
 
 struct Handle {
     Ap2Tables t;
+    Ap2HessTables ht;
 };
 
-// one (instance, interval): writes g rows, local grad columns, CCS values, 4 partials
-void eval_interval(const Ap2Tables& T, int k, const double* V, const double* P, double* g, double* grad,
-                   double* jac, double* part, std::vector<double>& tang, std::vector<double>& wn) {
+// hyper-dual inputs: e1 along colour c1, e2 along colour c2 (same seeds as the first-order pass)
+struct CpuHIn {
+    const double* w;
+    const ColorTabs* ct;
+    int kind, c1, c2;
+    double cxx, inv_tf;
+    double seed(int c, int i) const {
+        double t = ((ct->seedA[kind][c] >> i) & 1ull) ? 1.0 : 0.0;
+        if (i >= AWE_NX && i < 2 * AWE_NX) {
+            const int j = i - AWE_NX;
+            if ((ct->seedA[kind][c] >> j) & 1ull) t += cxx;
+            if ((ct->seedXD[kind][c] >> j) & 1u) t += 1.0;
+            if (c == ct->tf_color[kind]) t += -inv_tf * w[i];
+        }
+        return t;
+    }
+    awe::HDual operator()(int i) const { return awe::HDual(w[i], seed(c1, i), seed(c2, i), 0.0); }
+};
+
+struct CpuHSink {
+    double* hd;            // node's direction-pair Hessian
+    const HessTabs* ht;
+    const double* mu;      // row weights
+    int kind, c1, c2;
+    void emit(int r, const awe::HDual& v) {
+        const int p = ht->pdir[kind][c1][r], q = ht->pdir[kind][c2][r];
+        if (p < 0 || q < 0) return;
+        const int idx = ht->pidx[kind][p][q];
+        if (idx >= 0) hd[idx] += mu[r] * v.ab;
+    }
+    void eq_row(int r, const awe::HDual& v) { emit(r, v); }
+    void ineq_row(int r, const awe::HDual& v) { emit(AWE_N_EQ + r, v); }
+    void power(const awe::HDual& v) { emit(kRowPower, v); }
+    void beta(const awe::HDual& v) { emit(kRowBeta, v); }
+};
+
+// scaled node values of the interval's nodes; xdot at Radau nodes from the polynomial
+void node_values(const Ap2Tables& T, int k, const double* V, std::vector<double>& wn) {
     const Layout& L = T.lay;
-    const ColorTabs& ct = T.ct;
     const int d = T.d, NN = d + 1;
     const double* C = T.dcoll.C;
-    const double* cst = T.cst.data();
-    const double* th = P + L.n_v + AWE_NW + AWE_NCOST;
-    const double* cost = P + L.n_v + AWE_NW;
-    const double* wts = P + L.n_v;
-    const double* vref = P;
     const int base = L.v_int0 + k * L.stride;
     const double* vt = V;
     const double* vx = V + base;
@@ -91,14 +121,8 @@ void eval_interval(const Ap2Tables& T, int k, const double* V, const double* P, 
     const double* vxd = vu + AWE_NU;
     const double* vz = vxd + AWE_NX;
     const double* vcoll = vz + AWE_NZ;
-    const double* vx1 = vcoll + d * (AWE_NX + AWE_NZ);
     const double tf = vt[1];
     const double h = 1.0 / T.n_k;
-    const double inv_h_tf = 1.0 / h / tf;
-    const double inv_tf = 1.0 / tf;
-    auto toff = [&](int n) { return n == 0 ? 0 : ct.tsize[0] + (n - 1) * ct.tsize[1]; };
-
-    // node values (scaled)
     wn.assign((size_t)NN * 64, 0.0);
     for (int n = 0; n < NN; ++n)
         for (int i = 0; i < AWE_NW; ++i) {
@@ -126,6 +150,35 @@ void eval_interval(const Ap2Tables& T, int k, const double* V, const double* P, 
             }
             wn[n * 64 + i] = val;
         }
+}
+
+// one (instance, interval): writes g rows, local grad columns, CCS values, 4 partials
+void eval_interval(const Ap2Tables& T, int k, const double* V, const double* P, double* g, double* grad,
+                   double* jac, double* part, std::vector<double>& tang, std::vector<double>& wn) {
+    const Layout& L = T.lay;
+    const ColorTabs& ct = T.ct;
+    const int d = T.d, NN = d + 1;
+    const double* C = T.dcoll.C;
+    const double* cst = T.cst.data();
+    const double* th = P + L.n_v + AWE_NW + AWE_NCOST;
+    const double* cost = P + L.n_v + AWE_NW;
+    const double* wts = P + L.n_v;
+    const double* vref = P;
+    const int base = L.v_int0 + k * L.stride;
+    const double* vt = V;
+    const double* vx = V + base;
+    const double* vu = vx + AWE_NX;
+    const double* vxd = vu + AWE_NU;
+    const double* vz = vxd + AWE_NX;
+    const double* vcoll = vz + AWE_NZ;
+    const double* vx1 = vcoll + d * (AWE_NX + AWE_NZ);
+    const double tf = vt[1];
+    const double h = 1.0 / T.n_k;
+    const double inv_h_tf = 1.0 / h / tf;
+    const double inv_tf = 1.0 / tf;
+    auto toff = [&](int n) { return n == 0 ? 0 : ct.tsize[0] + (n - 1) * ct.tsize[1]; };
+
+    node_values(T, k, V, wn);
 
     // model, all colours of a node at once
     tang.assign((size_t)T.tang_total + 1, 0.0);
@@ -261,6 +314,158 @@ void eval_interval(const Ap2Tables& T, int k, const double* V, const double* P, 
     }
 }
 
+// Hessian of sigma f + lam^T g restricted to one interval: local CCS slots and the interval's
+// share of the global-global entries (mirrors ap2_hess_kernel)
+void hess_interval(const Ap2Tables& T, const Ap2HessTables& HT, int k, const double* V, const double* P,
+                   double sigma, const double* lam, double* H, double* gpart, std::vector<double>& tang,
+                   std::vector<double>& wn, std::vector<double>& hd) {
+    const Layout& L = T.lay;
+    const ColorTabs& ct = T.ct;
+    const HessTabs& ht = HT.ht;
+    const int d = T.d, NN = d + 1;
+    const double* C = T.dcoll.C;
+    const double* cst = T.cst.data();
+    const double* th = P + L.n_v + AWE_NW + AWE_NCOST;
+    const double* cost = P + L.n_v + AWE_NW;
+    const double* wts = P + L.n_v;
+    const double* vref = P;
+    const int base = L.v_int0 + k * L.stride;
+    const double* vt = V;
+    const double tf = vt[1];
+    const double h = 1.0 / T.n_k;
+    const double inv_h_tf = 1.0 / h / tf;
+    const double inv_tf = 1.0 / tf;
+    const double psi = vt[2 + kPhiPsi];
+    auto toff = [&](int n) { return n == 0 ? 0 : ct.tsize[0] + (n - 1) * ct.tsize[1]; };
+    node_values(T, k, V, wn);
+
+    // first-order pass (tangents of the beta / power rows and of the xdot directions)
+    tang.assign((size_t)T.tang_total + 1, 0.0);
+    double gval[8][kGvalStride];
+    for (int n = 0; n < NN; ++n) {
+        const int kind = n > 0;
+        CpuIn in{&wn[n * 64], &ct, kind, n > 0 ? C[n * NN + n] * inv_h_tf : 0.0, inv_tf};
+        CpuSink sink{&tang[toff(n)], gval[n], &ct, kind};
+        DN gamma(vt[2 + kPhiGamma]);
+        for (int c = 0; c < kHalf; ++c) gamma.d[c] = ((ct.seedA[kind][c] >> kDirGamma) & 1ull) ? 1.0 : 0.0;
+        awe::ap2_node<DN>(in, gamma, th, cst, sink, n == 0);
+    }
+    const double w_track = cost[kCostTracking] / cst[AWE_C_NORM_TRACKING];
+    const double w_xdot = cost[kCostXdotRegularisation] / cst[AWE_C_NORM_XDOT_REG];
+    const double w_ureg = cost[kCostURegularisation] / cst[AWE_C_NORM_U_REG];
+    const double w_fict = cost[kCostFictitious] / cst[AWE_C_NORM_FICTITIOUS];
+    const double w_theta = cost[kCostThetaRegularisation] / cst[AWE_C_NORM_THETA_REG];
+
+    // row weights mu per node
+    double mu[8][kHRows + 1];
+    for (int n = 0; n < NN; ++n) {
+        for (int r = 0; r <= kHRows; ++r) mu[n][r] = 0.0;
+        if (n == 0) {
+            for (int r = 0; r < kRowPower; ++r) mu[n][r] = lam[k * L.rows + r];
+        } else {
+            const double wj = T.dcoll.w[n - 1];
+            for (int r = 0; r < AWE_N_EQ; ++r) mu[n][r] = lam[k * L.rows + AWE_N_EQ + AWE_N_INEQ + (n - 1) * AWE_N_EQ + r];
+            const double cb = cost[kCostBeta] * wj / cst[AWE_C_NORM_BETA];
+            const double cp = -cost[kCostPower] * wj / (double)T.n_k;
+            mu[n][kRowPower] = sigma * (1.0 - psi) * cp;
+            mu[n][kRowBeta] = sigma * 2.0 * cb * gval[n][kRowBeta];
+        }
+    }
+    // direction-pair Hessian of every node: colour-pair hyper-dual passes
+    const int hoff1 = ht.npairs[0];
+    hd.assign((size_t)ht.npairs[0] + d * ht.npairs[1], 0.0);
+    auto hoff = [&](int n) { return n == 0 ? 0 : hoff1 + (n - 1) * ht.npairs[1]; };
+    for (int n = 0; n < NN; ++n) {
+        const int kind = n > 0;
+        for (int t = 0; t < ht.ntask[kind]; ++t) {
+            const int task = HT.tasks[ht.task_off[kind] + t];
+            const int c1 = task & 0xff, c2 = task >> 8;
+            CpuHIn in{&wn[n * 64], &ct, kind, c1, c2, n > 0 ? C[n * NN + n] * inv_h_tf : 0.0, inv_tf};
+            CpuHSink sink{&hd[hoff(n)], &ht, mu[n], kind, c1, c2};
+            const double g1 = ((ct.seedA[kind][c1] >> kDirGamma) & 1ull) ? 1.0 : 0.0;
+            const double g2 = ((ct.seedA[kind][c2] >> kDirGamma) & 1ull) ? 1.0 : 0.0;
+            awe::ap2_node<awe::HDual>(in, awe::HDual(vt[2 + kPhiGamma], g1, g2, 0.0), th, cst, sink, n == 0);
+        }
+    }
+    // objective terms at the Radau nodes, in direction space; map terms G
+    double G[8][AWE_NX] = {}, GT[8] = {};
+    for (int n = 1; n < NN; ++n) {
+        const int j = n - 1;
+        const double wj = T.dcoll.w[j];
+        const double* w = &wn[n * 64];
+        const double* rb = vref + base;
+        const double* rcx = rb + 2 * AWE_NX + AWE_NU + AWE_NZ + j * (AWE_NX + AWE_NZ);
+        const double cxx = C[n * NN + n] * inv_h_tf;
+        const double* tp = &tang[toff(n)];
+        double* hn = &hd[hoff(n)];
+        auto addp = [&](int p, int q, double v) { hn[ht.pidx[1][p][q]] += sigma * v; };
+        const double cb = cost[kCostBeta] * wj / cst[AWE_C_NORM_BETA];
+        const double cp = -cost[kCostPower] * wj / (double)T.n_k;
+        double tfsum = 0.0;
+        for (int i = 0; i < AWE_NX; ++i) {
+            const double ai = wts[i] * w_track, bi = wts[AWE_NX + i] * w_xdot, xd = w[AWE_NX + i];
+            addp(i, i, 2.0 * wj * psi * ai + cxx * cxx * 2.0 * wj * bi);
+            addp(i, AWE_NX + i, cxx * 2.0 * wj * bi);
+            addp(i, kDirTf, cxx * (-xd * inv_tf) * 2.0 * wj * bi);
+            addp(AWE_NX + i, AWE_NX + i, 2.0 * wj * bi);
+            addp(AWE_NX + i, kDirTf, (-xd * inv_tf) * 2.0 * wj * bi);
+            addp(i, kDirPsi, 2.0 * wj * ai * (w[i] - rcx[i]));
+            tfsum += (xd * inv_tf) * (xd * inv_tf) * 2.0 * wj * bi;
+        }
+        addp(kDirTf, kDirTf, tfsum);
+        for (int i = 0; i < AWE_NU; ++i)
+            addp(2 * AWE_NX + i, 2 * AWE_NX + i, 2.0 * wj * wts[2 * AWE_NX + i] * (i < 6 ? w_fict : w_ureg));
+        {
+            const double az = wts[kDirZ] * w_track;
+            addp(kDirZ, kDirZ, 2.0 * wj * psi * az);
+            addp(kDirZ, kDirPsi, 2.0 * wj * az * (w[kDirZ] - rcx[AWE_NX]));
+            addp(kDirDiam, kDirDiam, 2.0 * wj * wts[kDirDiam] * w_theta);
+        }
+        for (int p = 0; p <= kDirGamma; ++p) {
+            if (ct.obj_power[p] >= 0) addp(p, kDirPsi, -cp * tp[ct.obj_power[p]]);
+            if (ct.obj_beta[p] < 0) continue;
+            for (int q = p; q <= kDirGamma; ++q)
+                if (ct.obj_beta[q] >= 0) addp(p, q, 2.0 * cb * tp[ct.obj_beta[p]] * tp[ct.obj_beta[q]]);
+        }
+        // gradient of the node Lagrangian w.r.t. xdot_i (rows + objective)
+        for (int i = 0; i < AWE_NX; ++i) {
+            const int dir = AWE_NX + i, c = ct.dcolor[1][dir];
+            double gi = sigma * wj * 2.0 * wts[dir] * w_xdot * w[dir];
+            if (c >= 0) {
+                const unsigned long long m = ct.dmask[1][dir], cm = ct.cmask[1][c];
+                for (int r = 0; r < kHRows; ++r)
+                    if ((m >> r) & 1ull) gi += mu[n][r] * tp[ct.off[1][c] + __builtin_popcountll(cm & ((1ull << r) - 1ull))];
+            }
+            G[n][i] = gi;
+            GT[n] += gi * 2.0 * w[dir] * inv_tf * inv_tf;
+        }
+    }
+    // V-space entries
+    double scl[64];
+    scl[0] = 1.0;
+    for (int i = 1; i <= NN * NN; ++i) scl[i] = C[i - 1] * inv_h_tf;
+    const int ng = (int)HT.gslot.size();
+    const int nloc = HT.nslot[k];
+    for (int e = 0; e < nloc + ng; ++e) {
+        const int ei = HT.ent_off[k] + e;
+        double v = 0.0;
+        for (int t = HT.term_off[ei]; t < HT.term_off[ei + 1]; ++t) {
+            const unsigned term = HT.terms[t];
+            const int type = term >> 30, n = (term >> 27) & 7;
+            if (type == kHTypeA) {
+                v += scl[(term >> 7) & 127] * scl[term & 127] * hd[hoff(n) + ((term >> 14) & 8191)];
+            } else if (type == kHTypeB) {
+                const int i = (term >> 22) & 31, r = (term >> 19) & 7;
+                v += G[n][i] * (-C[r * NN + n] * inv_h_tf * inv_tf);
+            } else {
+                v += GT[n];
+            }
+        }
+        if (e < nloc) H[HT.slot0[k] + e] = v;
+        else gpart[e - nloc] = v;
+    }
+}
+
 void finalize(const Ap2Tables& T, const double* V, const double* P, const double* part, double* f,
               double* g, double* grad) {
     const Layout& L = T.lay;
@@ -342,5 +547,61 @@ int ap2cpu_eval_nlp(void* hv, int batch, const double* V, const double* P, doubl
 }
 
 void ap2cpu_destroy(void* hv) { delete static_cast<Handle*>(hv); }
+
+int ap2cpu_hess_init(void* hv, int* nnz) {
+    Handle* h = static_cast<Handle*>(hv);
+    if (h->ht.nnz == 0) {
+        int rc = build_hess_tables(h->t, h->ht, g_err);
+        if (rc) return rc;
+    }
+    *nnz = h->ht.nnz;
+    return AWE_OK;
+}
+
+int ap2cpu_hess_sparsity(void* hv, int* colind, int* row) {
+    const Ap2HessTables& H = static_cast<Handle*>(hv)->ht;
+    std::memcpy(colind, H.colind.data(), sizeof(int) * H.colind.size());
+    std::memcpy(row, H.row.data(), sizeof(int) * H.row.size());
+    return AWE_OK;
+}
+
+// upper-triangular CCS values of the Hessian of sigma f + lam^T g for each instance
+int ap2cpu_eval_hess(void* hv, int batch, const double* V, const double* P, const double* sigma,
+                     const double* lam, double* H, int nthreads) {
+    Handle* hd = static_cast<Handle*>(hv);
+    const Ap2Tables& T = hd->t;
+    const Ap2HessTables& HT = hd->ht;
+    if (HT.nnz == 0) { g_err = "call ap2cpu_hess_init first"; return AWE_ERR_ARG; }
+    const Layout& L = T.lay;
+    const int ng = (int)HT.gslot.size();
+    std::vector<double> gpart((size_t)batch * T.n_k * ng);
+    const int nt = nthreads > 0 ? nthreads : omp_get_max_threads();
+#pragma omp parallel num_threads(nt)
+    {
+        std::vector<double> tang, wn, hdir;
+#pragma omp for schedule(dynamic)
+        for (long t = 0; t < (long)batch * T.n_k; ++t) {
+            const int b = (int)(t / T.n_k), k = (int)(t % T.n_k);
+            hess_interval(T, HT, k, V + (size_t)b * L.n_v, P + (size_t)b * L.n_p, sigma[b],
+                          lam + (size_t)b * L.n_g, H + (size_t)b * HT.nnz, &gpart[((size_t)b * T.n_k + k) * ng],
+                          tang, wn, hdir);
+        }
+#pragma omp for schedule(static)
+        for (int b = 0; b < batch; ++b) {
+            const double* P_b = P + (size_t)b * L.n_p;
+            const double c_tf = P_b[L.n_v + AWE_NW + kCostTf];
+            const int itf = L.theta(1);
+            for (int g = 0; g < ng; ++g) {
+                double v = 0.0;
+                for (int k = 0; k < T.n_k; ++k) v += gpart[((size_t)b * T.n_k + k) * ng + g];
+                const int slot = HT.gslot[g];
+                if (HT.row[slot] == itf && slot >= HT.colind[itf] && slot < HT.colind[itf + 1])
+                    v += sigma[b] * 2.0 * c_tf;
+                H[(size_t)b * HT.nnz + slot] = v;
+            }
+        }
+    }
+    return AWE_OK;
+}
 
 }  // extern "C"

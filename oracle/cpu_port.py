@@ -31,6 +31,9 @@ def load():
         lib.ap2cpu_sparsity.argtypes = [vp, ip, ip]
         lib.ap2cpu_eval_nlp.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp, dp, ctypes.c_int]
         lib.ap2cpu_destroy.argtypes = [vp]
+        lib.ap2cpu_hess_init.argtypes = [vp, ip]
+        lib.ap2cpu_hess_sparsity.argtypes = [vp, ip, ip]
+        lib.ap2cpu_eval_hess.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp, ctypes.c_int]
         lib.ap2cpu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
@@ -67,6 +70,37 @@ class CpuPort:
         jac = np.zeros((B, self.nnz))
         self.lib.ap2cpu_eval_nlp(self.h, B, _dp(V), _dp(P), _dp(f), _dp(g), _dp(grad), _dp(jac), int(threads))
         return {"f": f, "g": g, "grad_f": grad, "jac": jac}
+
+    def hess_init(self):
+        if getattr(self, "hnnz", None) is None:
+            n = ctypes.c_int()
+            if self.lib.ap2cpu_hess_init(self.h, ctypes.byref(n)) != 0:
+                raise RuntimeError(self.lib.ap2cpu_last_error().decode())
+            self.hnnz = n.value
+            self.hcolind = np.zeros(self.n_v + 1, dtype=np.int32)
+            self.hrow = np.zeros(self.hnnz, dtype=np.int32)
+            ip = ctypes.POINTER(ctypes.c_int)
+            self.lib.ap2cpu_hess_sparsity(self.h, self.hcolind.ctypes.data_as(ip), self.hrow.ctypes.data_as(ip))
+
+    def eval_hess(self, V, P, sigma, lam, threads=0):
+        """Upper-triangular CCS values of the Hessian of sigma f + lam^T g, [B, nnz_h]."""
+        self.hess_init()
+        V = np.ascontiguousarray(np.atleast_2d(V), dtype=np.float64)
+        P = np.ascontiguousarray(np.atleast_2d(P), dtype=np.float64)
+        lam = np.ascontiguousarray(np.atleast_2d(lam), dtype=np.float64)
+        B = V.shape[0]
+        sig = np.ascontiguousarray(np.broadcast_to(np.asarray(sigma, dtype=np.float64), (B,)))
+        H = np.zeros((B, self.hnnz))
+        rc = self.lib.ap2cpu_eval_hess(self.h, B, _dp(V), _dp(P), _dp(sig), _dp(lam), _dp(H), int(threads))
+        if rc != 0:
+            raise RuntimeError(self.lib.ap2cpu_last_error().decode())
+        return H
+
+    def hess_csc(self, values):
+        """Full symmetric scipy matrix from upper-triangular values."""
+        import scipy.sparse as sp
+        U = sp.csc_matrix((np.asarray(values), self.hrow, self.hcolind), shape=(self.n_v, self.n_v))
+        return (U + sp.triu(U, 1).T).tocsc()
 
     def jac_csc(self, values):
         import scipy.sparse as sp

@@ -42,3 +42,34 @@ def test_cpu_port_batch_and_threads_deterministic():
         assert np.array_equal(a[key], b[key])
         assert np.array_equal(a[key][1], one[key][0])
     assert np.isfinite(a["jac"]).all()
+
+
+def _close_hess(Hk, Ho, what="H"):
+    """Full symmetric matrices; entries outside the kernel pattern must be rounding-level zeros
+    (t_f cancels analytically in the power cost; the oracle keeps 1e-16-level residues)."""
+    import scipy.sparse as sp
+    Hk, Ho = sp.csc_matrix(Hk), sp.csc_matrix(Ho)
+    scale = max(abs(Ho).max(), 1e-300)
+    D = abs(Hk - Ho).tocoo()
+    ref = np.asarray(abs(Ho)[D.row, D.col]).ravel()
+    tol = 1e-9 * ref + 1e-11 * scale
+    bad = D.data > tol
+    assert not bad.any(), f"{what}: {bad.sum()} entries off, worst {D.data[bad].max():.3e}"
+
+
+@pytest.mark.parametrize("n_k,d,member", [(3, 2, 1), (5, 3, 2), (2, 5, 0), (3, 1, 3)])
+def test_cpu_port_hessian_matches_oracle(n_k, d, member):
+    from oracle.ap2_oracle import from_problem
+    from oracle.cpu_port import CpuPort
+    consts = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+    lay = pb.NlpLayout(n_k, d)
+    v0 = initial_guess(consts, lay)
+    V = batch_member(v0, lay, member)
+    P = pb.pack_p(lay, consts, v0, u_ref=6.0)
+    lam = np.random.default_rng(7).standard_normal(lay.n_g)
+    sigma = 0.7
+    port = CpuPort(consts)
+    Hk = port.hess_csc(port.eval_hess(V, P, sigma, lam)[0])
+    Ho = from_problem(consts, n_k=n_k, d=d).nlp_hess_l(V, P, sigma, lam, lay, pb.THETA0_OFF, pb.COST_NAMES,
+                                                        pb.PHI_NAMES)
+    _close_hess(Hk, Ho)
