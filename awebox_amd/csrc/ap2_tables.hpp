@@ -575,6 +575,7 @@ struct Ap2HessTables {
     std::vector<int> ent_off;           // [n_k + 1] entries of each interval (local slots, then globals)
     std::vector<int> term_off;          // [n_entries + 1] into terms
     std::vector<unsigned> terms;
+    std::vector<short> task_target;     // [task][kHRows + 1]: pair index a row feeds, -1
     int max_pairs = 0;
 };
 
@@ -715,6 +716,18 @@ inline int build_hess_tables(const Ap2Tables& T, Ap2HessTables& H, std::string& 
         H.tasks.insert(H.tasks.end(), task_set[kind].begin(), task_set[kind].end());
     }
     H.max_pairs = std::max(ht.npairs[0], ht.npairs[1]);
+    // per task and row: the direction pair its mixed second derivative belongs to
+    H.task_target.assign(H.tasks.size() * (kHRows + 1), (short)-1);
+    for (int kind = 0; kind < 2; ++kind)
+        for (int t = 0; t < ht.ntask[kind]; ++t) {
+            const int task = H.tasks[ht.task_off[kind] + t], c1 = task & 0xff, c2 = task >> 8;
+            for (int r = 0; r < kHRows; ++r) {
+                if (!row_used(kind, r)) continue;
+                const int p = ht.pdir[kind][c1][r], q = ht.pdir[kind][c2][r];
+                if (p < 0 || q < 0) continue;
+                H.task_target[(size_t)(ht.task_off[kind] + t) * (kHRows + 1) + r] = ht.pidx[kind][p][q];
+            }
+        }
 
     // ---- V-space entries and their gather terms ----------------------------------------------
     auto is_global = [&](int col) { return col < L.v_int0; };

@@ -187,6 +187,154 @@ constexpr int lds_fixed_doubles() {
     return nloc_pad<D>() + pst_pad<D>() + (D + 1) * (64 + kGvalStride + 64 + kPreStride) + ((D + 2) & ~1) + 64 + 2;
 }
 
+// ---- phases shared by the first- and second-order kernels ---------------------------------
+
+// scaled node values (AWE_NW layout) of the interval's d+1 nodes; xdot at Radau nodes from the
+// collocation polynomial (collocation.py:202-258).  vloc = [theta, phi, x[k], u, xdot, z, coll..]
+template <int D, int NT>
+__device__ __forceinline__ void node_values_pass(const double* vloc, const double* C, int n_k, double* wn,
+                                                 int tid) {
+    constexpr int NN = D + 1;
+    const double* vt = vloc;
+    const double* vx = vloc + 9;
+    const double* vu = vx + AWE_NX;
+    const double* vxd = vu + AWE_NU;
+    const double* vz = vxd + AWE_NX;
+    const double* vcoll = vz + AWE_NZ;
+    const double tf = vt[1];
+    const double h = 1.0 / n_k;
+    for (int t = tid; t < NN * 64; t += NT) {
+        const int n = t >> 6, i = t & 63;
+        double val = 0.0;
+        if (i < AWE_NX) {
+            val = n == 0 ? vx[i] : vcoll[(n - 1) * (AWE_NX + AWE_NZ) + i];
+        } else if (i < 2 * AWE_NX) {
+            const int s = i - AWE_NX;
+            if (n == 0) {
+                val = vxd[s];
+            } else {
+                double xp = 0.0;
+#pragma unroll
+                for (int r = 0; r < NN; ++r) {
+                    const double Xr = (r == 0) ? vx[s] : vcoll[(r - 1) * (AWE_NX + AWE_NZ) + s];
+                    xp += C[r * NN + n] * Xr;
+                }
+                val = xp / h / tf;
+            }
+        } else if (i < 2 * AWE_NX + AWE_NU) {
+            val = vu[i - 2 * AWE_NX];
+        } else if (i < 2 * AWE_NX + AWE_NU + AWE_NZ) {
+            val = n == 0 ? vz[0] : vcoll[(n - 1) * (AWE_NX + AWE_NZ) + AWE_NX];
+        } else if (i < AWE_NW) {
+            val = vt[i - (2 * AWE_NX + AWE_NU + AWE_NZ)];
+        }
+        wn[t] = val;
+    }
+    __syncthreads();
+}
+
+// sub-model preaccumulation: stage A, one (node, height) per thread: wind speed and density at
+// the kite and at every tether element midpoint, as functions of q_z; stage B, one (node,
+// element, direction) per thread: the element's drag along q0..2, dq0..2, diam_t; then the
+// element sums.  tang serves as scratch.
+template <int D, int NT>
+__device__ __forceinline__ void submodel_pass(const double* cst, const double* th, const double* wn, double* pre,
+                                              double* tang, int tid) {
+    constexpr int NN = D + 1;
+    {
+        const double* s = cst + AWE_C_SCALING;
+        const int n_el = (int)cst[AWE_C_N_ELEMENTS];
+        double* scr = tang;                                   // [NN][n_el][7][6]
+        double* atm = tang + NN * n_el * kPreDirs * 6;        // [NN][n_el][4]
+        for (int t = tid; t < NN * (n_el + 1); t += NT) {
+            const int n = t / (n_el + 1), e = t - n * (n_el + 1) - 1;
+            const awe::Dual qz = awe::Dual(wn[n * 64 + 2], 1.0) * s[2];
+            awe::Dual uw, rho;
+            double* o;
+            if (e < 0) {
+                awe::InlineSubmodels().kite_atmosphere(qz, th, uw, rho);
+                o = pre + n * kPreStride + 24;
+            } else {
+                const awe::Dual zz = awe::tether_element_height(e, n_el, qz);
+                uw = awe::wind_speed(zz, th);
+                rho = awe::isa_density(zz, th);
+                o = atm + (n * n_el + e) * 4;
+            }
+            o[0] = uw.v; o[1] = uw.d; o[2] = rho.v; o[3] = rho.d;
+        }
+        __syncthreads();
+        const int ntask = n_el * kPreDirs;
+        for (int t = tid; t < NN * ntask; t += NT) {
+            const int n = t / ntask, q = t - n * ntask;
+            const double* w = wn + n * 64;
+            const int e = q / kPreDirs, j = q - e * kPreDirs;
+            const int vj = pre_var(j);
+            awe::Dual qv[3], vv[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                qv[i] = awe::Dual(w[i], vj == i ? 1.0 : 0.0) * s[i];
+                vv[i] = awe::Dual(w[3 + i], vj == 3 + i ? 1.0 : 0.0) * s[3 + i];
+            }
+            awe::Dual diam = awe::Dual(w[kDirDiam], vj == kDirDiam ? 1.0 : 0.0) * s[kDirDiam];
+            const double* at = atm + (n * n_el + e) * 4;
+            const double dz = vj == 2 ? 1.0 : 0.0;
+            const awe::Dual uw(at[0], dz * at[1]), rho(at[2], dz * at[3]);
+            awe::Dual c[3];
+            awe::tether_element_drag(e, n_el, qv, vv, diam, uw, rho, th, c);
+            double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { o[i] = c[i].v; o[3 + i] = c[i].d; }
+        }
+        __syncthreads();
+        // element sums in element order (the order of the inline model)
+        for (int t = tid; t < NN * kPreDirs * 3; t += NT) {
+            const int n = t / (kPreDirs * 3), j = (t / 3) % kPreDirs, i = t % 3;
+            double val = 0.0, tan = 0.0;
+            for (int e = 0; e < n_el; ++e) {
+                const double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
+                val = val + o[i];
+                tan = tan + o[3 + i];
+            }
+            if (j == 0) pre[n * kPreStride + i] = val;
+            pre[n * kPreStride + 3 + 3 * j + i] = tan;
+        }
+        __syncthreads();
+    }
+}
+
+// first-order model pass: half-wavefront slot = node, lane = colour; rows go to the compressed
+// tangent buffer, values to gval
+template <int D>
+__device__ __forceinline__ void first_order_pass(const ColorTabs* ct, const double* wn, const double* pre,
+                                                 double* tang, double* gval, double* dump, const double* C,
+                                                 const double* vt, const double* th, const double* cst,
+                                                 double inv_h_tf, double inv_tf, int wave, int lane) {
+    constexpr int NN = D + 1;
+    auto toff = [&](int n) { return n == 0 ? 0 : ct->tsize[0] + (n - 1) * ct->tsize[1]; };
+    {
+        const int n = wave * 2 + (lane >> 5);
+        const int c = lane & (kHalf - 1);
+        if (n < NN) {
+            const int kind = n > 0 ? 1 : 0;
+            LaneIn in;
+            in.w = wn + n * 64;
+            in.seedA = ct->seedA[kind][c];
+            in.seedXD = ct->seedXD[kind][c];
+            in.cxx = n > 0 ? C[n * NN + n] * inv_h_tf : 0.0;
+            in.tfs = (c == ct->tf_color[kind]) ? -inv_tf : 0.0;
+            NodeSink sink;
+            sink.tp = tang + toff(n) + ct->off[kind][c];
+            sink.gv = gval + n * kGvalStride;
+            sink.cm = ct->cmask[kind][c];
+            sink.c0 = c == 0;
+            sink.dump = dump;
+            awe::Dual gamma(vt[2 + kPhiGamma], ((in.seedA >> kDirGamma) & 1ull) ? 1.0 : 0.0);
+            LdsSubmodels sub{pre + n * kPreStride, in.seedA};
+            awe::ap2_node<awe::Dual>(in, gamma, th, cst, sink, n == 0, sub);
+        }
+    }
+}
+
 // occupancy target (waves per SIMD) for the register allocator; build-time tunable
 #ifndef AWE_WAVES_PER_EU
 #define AWE_WAVES_PER_EU 3
@@ -261,129 +409,20 @@ void ap2_interval_kernel(KArgs a) {
     }
     if (tid == 0) tang[a.tang_total] = 1.0;
 
-    // node values (scaled, AWE_NW layout); xdot at Radau nodes from the polynomial
-    for (int t = tid; t < NN * 64; t += NT) {
-        const int n = t >> 6, i = t & 63;
-        double val = 0.0;
-        if (i < AWE_NX) {
-            val = n == 0 ? vx[i] : vcoll[(n - 1) * (AWE_NX + AWE_NZ) + i];
-        } else if (i < 2 * AWE_NX) {
-            const int s = i - AWE_NX;
-            if (n == 0) {
-                val = vxd[s];
-            } else {
-                double xp = 0.0;
-#pragma unroll
-                for (int r = 0; r < NN; ++r) {
-                    const double Xr = (r == 0) ? vx[s] : vcoll[(r - 1) * (AWE_NX + AWE_NZ) + s];
-                    xp += C[r * NN + n] * Xr;
-                }
-                val = xp / h / tf;
-            }
-        } else if (i < 2 * AWE_NX + AWE_NU) {
-            val = vu[i - 2 * AWE_NX];
-        } else if (i < 2 * AWE_NX + AWE_NU + AWE_NZ) {
-            val = n == 0 ? vz[0] : vcoll[(n - 1) * (AWE_NX + AWE_NZ) + AWE_NX];
-        } else if (i < AWE_NW) {
-            val = vt[i - (2 * AWE_NX + AWE_NU + AWE_NZ)];
-        }
-        wn[t] = val;
-    }
-    __syncthreads();
+    node_values_pass<D, NT>(vloc, C, a.n_k, wn, tid);
 
     // ---- phase 0b: sub-models -------------------------------------------------------------
     // stage A, one (node, height) per thread: wind speed and density at the kite and at every
     // tether element midpoint, as functions of q_z; stage B, one (node, element, direction)
     // per thread: the element's drag along q0..2, dq0..2, diam_t
 #ifndef AWE_EXP_SKIP_PRE
-    {
-        const double* s = a.cst + AWE_C_SCALING;
-        const int n_el = (int)a.cst[AWE_C_N_ELEMENTS];
-        double* scr = tang;                                   // [NN][n_el][7][6]
-        double* atm = tang + NN * n_el * kPreDirs * 6;        // [NN][n_el][4]
-        for (int t = tid; t < NN * (n_el + 1); t += NT) {
-            const int n = t / (n_el + 1), e = t - n * (n_el + 1) - 1;
-            const awe::Dual qz = awe::Dual(wn[n * 64 + 2], 1.0) * s[2];
-            awe::Dual uw, rho;
-            double* o;
-            if (e < 0) {
-                awe::InlineSubmodels().kite_atmosphere(qz, th, uw, rho);
-                o = pre + n * kPreStride + 24;
-            } else {
-                const awe::Dual zz = awe::tether_element_height(e, n_el, qz);
-                uw = awe::wind_speed(zz, th);
-                rho = awe::isa_density(zz, th);
-                o = atm + (n * n_el + e) * 4;
-            }
-            o[0] = uw.v; o[1] = uw.d; o[2] = rho.v; o[3] = rho.d;
-        }
-        __syncthreads();
-        const int ntask = n_el * kPreDirs;
-        for (int t = tid; t < NN * ntask; t += NT) {
-            const int n = t / ntask, q = t - n * ntask;
-            const double* w = wn + n * 64;
-            const int e = q / kPreDirs, j = q - e * kPreDirs;
-            const int vj = pre_var(j);
-            awe::Dual qv[3], vv[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                qv[i] = awe::Dual(w[i], vj == i ? 1.0 : 0.0) * s[i];
-                vv[i] = awe::Dual(w[3 + i], vj == 3 + i ? 1.0 : 0.0) * s[3 + i];
-            }
-            awe::Dual diam = awe::Dual(w[kDirDiam], vj == kDirDiam ? 1.0 : 0.0) * s[kDirDiam];
-            const double* at = atm + (n * n_el + e) * 4;
-            const double dz = vj == 2 ? 1.0 : 0.0;
-            const awe::Dual uw(at[0], dz * at[1]), rho(at[2], dz * at[3]);
-            awe::Dual c[3];
-            awe::tether_element_drag(e, n_el, qv, vv, diam, uw, rho, th, c);
-            double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) { o[i] = c[i].v; o[3 + i] = c[i].d; }
-        }
-        __syncthreads();
-        // element sums in element order (the order of the inline model)
-        for (int t = tid; t < NN * kPreDirs * 3; t += NT) {
-            const int n = t / (kPreDirs * 3), j = (t / 3) % kPreDirs, i = t % 3;
-            double val = 0.0, tan = 0.0;
-            for (int e = 0; e < n_el; ++e) {
-                const double* o = scr + ((n * n_el + e) * kPreDirs + j) * 6;
-                val = val + o[i];
-                tan = tan + o[3 + i];
-            }
-            if (j == 0) pre[n * kPreStride + i] = val;
-            pre[n * kPreStride + 3 + 3 * j + i] = tan;
-        }
-        __syncthreads();
-    }
+    submodel_pass<D, NT>(a.cst, th, wn, pre, tang, tid);
 #endif
 
     // ---- phase 1: model, one node per half-wavefront, one colour per lane ------------------
-    {
-        const int n = wave * 2 + (lane >> 5);
-        const int c = lane & (kHalf - 1);
 #ifndef AWE_EXP_SKIP_MODEL
-        if (n < NN) {
-#else
-        if (n < 0) {
+    first_order_pass<D>(ct, wn, pre, tang, gval, dfl + tid, C, vt, th, a.cst, inv_h_tf, inv_tf, wave, lane);
 #endif
-            const int kind = n > 0 ? 1 : 0;
-            LaneIn in;
-            in.w = wn + n * 64;
-            in.seedA = ct->seedA[kind][c];
-            in.seedXD = ct->seedXD[kind][c];
-            in.cxx = n > 0 ? C[n * NN + n] * inv_h_tf : 0.0;
-            in.tfs = (c == ct->tf_color[kind]) ? -inv_tf : 0.0;
-            NodeSink sink;
-            sink.tp = tang + toff(n) + ct->off[kind][c];
-            sink.gv = gval + n * kGvalStride;
-            sink.cm = ct->cmask[kind][c];
-            sink.c0 = c == 0;
-            sink.dump = dfl + tid;   // dfl is first written in phase 2
-            awe::Dual gamma(vt[2 + kPhiGamma], ((in.seedA >> kDirGamma) & 1ull) ? 1.0 : 0.0);
-            LdsSubmodels sub{pre + n * kPreStride, in.seedA};
-            awe::ap2_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0, sub);
-        }
-    }
     __syncthreads();
 
     // ---- phase 2: objective directional derivatives (one lane per direction) -------------
@@ -577,6 +616,292 @@ __global__ __launch_bounds__(64) void ap2_finalize_kernel(KArgs a) {
     }
 }
 
+
+// =========================================================================================
+// Hessian of the Lagrangian sigma f + lam^T g (nlp_hess_l)
+// =========================================================================================
+constexpr int kHessWaves = 4;
+constexpr int kHessThreads = 64 * kHessWaves;
+
+struct HKArgs {
+    KArgs a;                       // V, P, tables and sizes of the first-order kernel
+    const HessTabs* ht;
+    const int* tasks;              // colour pairs per node kind
+    const short* task_target;      // [task][36] direction-pair index of each row
+    const int* ent_off;            // [n_k + 1]
+    const int* term_off;
+    const unsigned* terms;
+    const int* slot0;
+    const int* nslot;
+    const int* gslot;
+    const double* sigma;           // [batch]
+    const double* lam;             // [batch][n_g]
+    double* H;                     // [batch][nnz_h] upper-triangular CCS values
+    double* gpart;                 // [batch][n_k][ng]
+    int hnnz, ng, hd_total;
+    int g_tftf;                    // index of the (t_f, t_f) entry among the global entries
+};
+
+// hyper-dual node variable i: e1 along colour c1, e2 along colour c2
+struct LaneHIn {
+    const double* w;
+    unsigned long long sA1, sA2;
+    unsigned int sX1, sX2;
+    double cxx, t1, t2;
+    __device__ __forceinline__ awe::HDual operator()(int i) const {
+        double a = ((sA1 >> i) & 1ull) ? 1.0 : 0.0;
+        double b = ((sA2 >> i) & 1ull) ? 1.0 : 0.0;
+        if (i >= AWE_NX && i < 2 * AWE_NX) {
+            const int j = i - AWE_NX;
+            if ((sA1 >> j) & 1ull) a += cxx;
+            if ((sX1 >> j) & 1u) a += 1.0;
+            a += t1 * w[i];
+            if ((sA2 >> j) & 1ull) b += cxx;
+            if ((sX2 >> j) & 1u) b += 1.0;
+            b += t2 * w[i];
+        }
+        return awe::HDual(w[i], a, b, 0.0);
+    }
+};
+
+// accumulates mu_r * d2F_r/de1de2 into the node's direction-pair Hessian (branch-free)
+struct LaneHSink {
+    double* hd;
+    double* dump;
+    const double* mu;
+    const short* tt;               // this task's row targets
+    __device__ __forceinline__ void emit(int r, const awe::HDual& v) {
+        const int idx = tt[r];
+        double* adr = idx >= 0 ? hd + idx : dump;
+        *adr += mu[r] * v.ab;
+    }
+    __device__ __forceinline__ void eq_row(int r, const awe::HDual& v) { emit(r, v); }
+    __device__ __forceinline__ void ineq_row(int r, const awe::HDual& v) { emit(AWE_N_EQ + r, v); }
+    __device__ __forceinline__ void power(const awe::HDual& v) { emit(kRowPower, v); }
+    __device__ __forceinline__ void beta(const awe::HDual& v) { emit(kRowBeta, v); }
+};
+
+#ifndef AWE_HESS_WAVES_PER_EU
+#define AWE_HESS_WAVES_PER_EU 1
+#endif
+
+template <int D>
+constexpr int hess_lds_fixed_doubles() {
+    return nloc_pad<D>() + pst_pad<D>() + (D + 1) * (64 + kGvalStride + kPreStride + 36 + 24) + 8 + 64 +
+           kHessThreads;
+}
+
+template <int D>
+__global__ __launch_bounds__(kHessThreads)
+__attribute__((amdgpu_waves_per_eu(AWE_HESS_WAVES_PER_EU, AWE_HESS_WAVES_PER_EU)))
+void ap2_hess_kernel(HKArgs ha) {
+    const KArgs& a = ha.a;
+    constexpr int NN = D + 1;
+    constexpr int NT = kHessThreads;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int k = blockIdx.x % a.n_k;
+    const int b = blockIdx.x / a.n_k;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const double* th = P + a.n_v + AWE_NW + AWE_NCOST;
+    const double* cost = P + a.n_v + AWE_NW;
+    const double* wts = P + a.n_v;
+    const double* vref = P;
+    const double* lam = ha.lam + (size_t)b * a.n_g;
+    const double sigma = ha.sigma[b];
+    const ColorTabs* ct = a.ct;
+    const HessTabs* ht = ha.ht;
+    const double* C = a.coll.C;
+
+    extern __shared__ double smem[];
+    double* vloc = smem;
+    double* pst = vloc + nloc_pad<D>();
+    double* wn = pst + pst_pad<D>();
+    double* gval = wn + NN * 64;
+    double* pre = gval + NN * kGvalStride;
+    double* mu = pre + NN * kPreStride;            // [NN][36]
+    double* G = mu + NN * 36;                      // [NN][24]: G[n][23] holds sum_i G 2 xdot / tf^2
+    double* scl = G + NN * 24 + 8;
+    double* dump = scl + 64;                       // one slot per thread
+    double* tang = dump + NT;
+    double* hd = tang + a.tang_total + 1;
+    auto toff = [&](int n) { return n == 0 ? 0 : ct->tsize[0] + (n - 1) * ct->tsize[1]; };
+    auto hoff = [&](int n) { return n == 0 ? 0 : ht->npairs[0] + (n - 1) * ht->npairs[1]; };
+
+    // ---- stage V slice and P (as in the first-order kernel) ----------------------------------
+    const int base = a.v_int0 + k * a.stride;
+    for (int i = tid; i < 9; i += NT) vloc[i] = V[i];
+    for (int i = tid; i < a.stride + AWE_NX; i += NT) vloc[9 + i] = V[base + i];
+    for (int i = tid; i < kPstRef + a.stride; i += NT) {
+        double pv = 0.0;
+        if (i < AWE_NW) pv = wts[i];
+        else if (i >= kPstCost && i < kPstCost + AWE_NCOST) pv = cost[i - kPstCost];
+        else if (i >= kPstThRef && i < kPstRef) pv = vref[i - kPstThRef];
+        else if (i >= kPstRef) pv = vref[base + i - kPstRef];
+        pst[i] = pv;
+    }
+    for (int i = tid; i < ha.hd_total; i += NT) hd[i] = 0.0;
+    __syncthreads();
+    const double* vt = vloc;
+    const double tf = vt[1];
+    const double h = 1.0 / a.n_k;
+    const double inv_h_tf = 1.0 / h / tf;
+    const double inv_tf = 1.0 / tf;
+    const double psi = vt[2 + kPhiPsi];
+    for (int i = tid; i < 1 + NN * NN; i += NT) scl[i] = i == 0 ? 1.0 : C[i - 1] * inv_h_tf;
+    node_values_pass<D, NT>(vloc, C, a.n_k, wn, tid);
+    submodel_pass<D, NT>(a.cst, th, wn, pre, tang, tid);
+    first_order_pass<D>(ct, wn, pre, tang, gval, dump + tid, C, vt, th, a.cst, inv_h_tf, inv_tf, wave, lane);
+    __syncthreads();
+
+    // ---- row weights: lam for constraint rows, sigma-scaled objective weights -----------------
+    const double* pcost = pst + kPstCost;
+    for (int t = tid; t < NN * 36; t += NT) {
+        const int n = t / 36, r = t % 36;
+        double m = 0.0;
+        if (n == 0) {
+            if (r < kRowPower) m = lam[k * a.rows + r];
+        } else {
+            const double wj = a.coll.w[n - 1];
+            if (r < AWE_N_EQ) m = lam[k * a.rows + AWE_N_EQ + AWE_N_INEQ + (n - 1) * AWE_N_EQ + r];
+            else if (r == kRowPower) m = sigma * (1.0 - psi) * (-pcost[kCostPower] * wj / (double)a.n_k);
+            else if (r == kRowBeta)
+                m = sigma * 2.0 * (pcost[kCostBeta] * wj / a.cst[AWE_C_NORM_BETA]) * gval[n * kGvalStride + kRowBeta];
+        }
+        mu[t] = m;
+    }
+    __syncthreads();
+
+    // ---- second-order pass: one (node, colour pair) per thread ---------------------------------
+    const int nt0 = ht->ntask[0], nt1 = ht->ntask[1];
+    for (int t = tid; t < nt0 + D * nt1; t += NT) {
+        const int n = t < nt0 ? 0 : 1 + (t - nt0) / nt1;
+        const int kind = n > 0 ? 1 : 0;
+        const int ti = (kind == 0 ? t : (t - nt0) % nt1) + ht->task_off[kind];
+        const int task = ha.tasks[ti];
+        const int c1 = task & 0xff, c2 = task >> 8;
+        LaneHIn in;
+        in.w = wn + n * 64;
+        in.sA1 = ct->seedA[kind][c1]; in.sA2 = ct->seedA[kind][c2];
+        in.sX1 = ct->seedXD[kind][c1]; in.sX2 = ct->seedXD[kind][c2];
+        in.cxx = n > 0 ? C[n * NN + n] * inv_h_tf : 0.0;
+        in.t1 = (c1 == ct->tf_color[kind]) ? -inv_tf : 0.0;
+        in.t2 = (c2 == ct->tf_color[kind]) ? -inv_tf : 0.0;
+        LaneHSink sink{hd + hoff(n), dump + tid, mu + n * 36, ha.task_target + (size_t)ti * 36};
+        const awe::HDual gamma(vt[2 + kPhiGamma], ((in.sA1 >> kDirGamma) & 1ull) ? 1.0 : 0.0,
+                               ((in.sA2 >> kDirGamma) & 1ull) ? 1.0 : 0.0, 0.0);
+        awe::ap2_node<awe::HDual>(in, gamma, th, a.cst, sink, n == 0);
+    }
+    __syncthreads();
+
+    // ---- objective terms in direction space and the xdot(t_f) map terms (Radau nodes) --------
+    const double w_track = pcost[kCostTracking] / a.cst[AWE_C_NORM_TRACKING];
+    const double w_xdot = pcost[kCostXdotRegularisation] / a.cst[AWE_C_NORM_XDOT_REG];
+    const double w_ureg = pcost[kCostURegularisation] / a.cst[AWE_C_NORM_U_REG];
+    const double w_fict = pcost[kCostFictitious] / a.cst[AWE_C_NORM_FICTITIOUS];
+    const double w_theta = pcost[kCostThetaRegularisation] / a.cst[AWE_C_NORM_THETA_REG];
+    for (int n = 1 + wave; n < NN; n += kHessWaves) {
+        const int p = lane;
+        const int j = n - 1;
+        const double wj = a.coll.w[j];
+        const double* w = wn + n * 64;
+        const double* rcx = pst + kPstRef + 2 * AWE_NX + AWE_NU + AWE_NZ + j * (AWE_NX + AWE_NZ);
+        const double cxx = C[n * NN + n] * inv_h_tf;
+        const double* tp = tang + toff(n);
+        double* hn = hd + hoff(n);
+        auto addp = [&](int q1, int q2, double v) { hn[ht->pidx[1][q1][q2]] += sigma * v; };
+        const double cb = pcost[kCostBeta] * wj / a.cst[AWE_C_NORM_BETA];
+        const double cp = -pcost[kCostPower] * wj / (double)a.n_k;
+        double tfpart = 0.0, gt = 0.0;
+        if (p < AWE_NX) {
+            const double ai = pst[p] * w_track, bi = pst[AWE_NX + p] * w_xdot, xd = w[AWE_NX + p];
+            addp(p, p, 2.0 * wj * psi * ai + cxx * cxx * 2.0 * wj * bi);
+            addp(p, AWE_NX + p, cxx * 2.0 * wj * bi);
+            addp(p, kDirTf, cxx * (-xd * inv_tf) * 2.0 * wj * bi);
+            addp(p, kDirPsi, 2.0 * wj * ai * (w[p] - rcx[p]));
+        } else if (p < 2 * AWE_NX) {
+            const int i = p - AWE_NX;
+            const double bi = pst[p] * w_xdot, xd = w[p];
+            addp(p, p, 2.0 * wj * bi);
+            addp(p, kDirTf, (-xd * inv_tf) * 2.0 * wj * bi);
+            tfpart = (xd * inv_tf) * (xd * inv_tf) * 2.0 * wj * bi;
+            // gradient of the node Lagrangian w.r.t. xdot_i: rows (first-order tangents) + objective
+            double gi = sigma * wj * 2.0 * bi * xd;
+            const int c = ct->dcolor[1][p];
+            if (c >= 0) {
+                const unsigned long long m = ct->dmask[1][p], cm = ct->cmask[1][c];
+                for (unsigned long long mm = m; mm; mm &= mm - 1ull) {
+                    const int r = __builtin_ctzll(mm);
+                    gi += mu[n * 36 + r] * tp[ct->off[1][c] + __popcll(cm & ((1ull << r) - 1ull))];
+                }
+            }
+            G[n * 24 + i] = gi;
+            gt = gi * 2.0 * xd * inv_tf * inv_tf;
+        } else if (p < 2 * AWE_NX + AWE_NU) {
+            const int i = p - 2 * AWE_NX;
+            addp(p, p, 2.0 * wj * pst[p] * (i < 6 ? w_fict : w_ureg));
+        } else if (p == kDirZ) {
+            const double az = pst[kDirZ] * w_track;
+            addp(p, p, 2.0 * wj * psi * az);
+            addp(p, kDirPsi, 2.0 * wj * az * (w[kDirZ] - rcx[AWE_NX]));
+        } else if (p == kDirDiam) {
+            addp(p, p, 2.0 * wj * pst[kDirDiam] * w_theta);
+        }
+        if (p <= kDirGamma) {
+            const int ip = ct->obj_power[p], ib = ct->obj_beta[p];
+            if (ip >= 0) addp(p, kDirPsi, -cp * tp[ip]);
+            if (ib >= 0) {
+                const double bp = 2.0 * cb * tp[ib];
+                for (int q = p; q <= kDirGamma; ++q) {
+                    const int iq = ct->obj_beta[q];
+                    if (iq >= 0) addp(p, q, bp * tp[iq]);
+                }
+            }
+        }
+        tfpart = wave_sum(tfpart);
+        gt = wave_sum(gt);
+        if (p == kDirTf) addp(kDirTf, kDirTf, tfpart);
+        if (p == 0) G[n * 24 + 23] = gt;
+    }
+    __syncthreads();
+
+    // ---- V-space entries: local CCS slots (contiguous) and the global-global partials ---------
+    const int nloc = ha.nslot[k];
+    const int e0 = ha.ent_off[k];
+    const double ctf2 = inv_h_tf * inv_tf;
+    double* Hb = ha.H + (size_t)b * ha.hnnz + ha.slot0[k];
+    double* gp = ha.gpart + ((size_t)b * a.n_k + k) * ha.ng;
+    for (int e = tid; e < nloc + ha.ng; e += NT) {
+        double v = 0.0;
+        for (int t = ha.term_off[e0 + e]; t < ha.term_off[e0 + e + 1]; ++t) {
+            const unsigned term = ha.terms[t];
+            const int type = term >> 30, n = (term >> 27) & 7;
+            if (type == kHTypeA) {
+                v += scl[(term >> 7) & 127] * scl[term & 127] * hd[hoff(n) + ((term >> 14) & 8191)];
+            } else if (type == kHTypeB) {
+                const int i = (term >> 22) & 31, r = (term >> 19) & 7;
+                v += G[n * 24 + i] * (-C[r * NN + n] * ctf2);
+            } else {
+                v += G[n * 24 + 23];
+            }
+        }
+        if (e < nloc) Hb[e] = v;
+        else gp[e - nloc] = v;
+    }
+}
+
+// global-global entries: sum of the interval partials plus the time cost (objective.py)
+__global__ __launch_bounds__(64) void ap2_hess_finalize_kernel(HKArgs ha) {
+    const KArgs& a = ha.a;
+    const int b = blockIdx.x;
+    const int g = threadIdx.x;
+    if (g >= ha.ng) return;
+    double v = 0.0;
+    for (int k = 0; k < a.n_k; ++k) v += ha.gpart[((size_t)b * a.n_k + k) * ha.ng + g];
+    if (g == ha.g_tftf) v += ha.sigma[b] * 2.0 * a.P[(size_t)b * a.n_p + a.n_v + AWE_NW + kCostTf];
+    ha.H[(size_t)b * ha.hnnz + ha.gslot[g]] = v;
+}
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
@@ -584,8 +909,25 @@ __global__ __launch_bounds__(64) void ap2_finalize_kernel(KArgs a) {
 // ---------------------------------------------------------------------------------------
 struct awe_handle_s {
     awt::Ap2Tables t;               // host tables (layout, pattern, colouring, gather list)
+    awt::Ap2HessTables ht;          // Hessian structure, tasks and gather terms
     int batch = 0;
-    size_t lds_bytes = 0;
+    size_t lds_bytes = 0, hess_lds_bytes = 0;
+    int hd_total = 0, g_tftf = -1;
+    awt::HessTabs* d_ht = nullptr;
+    int* d_tasks = nullptr;
+    short* d_task_target = nullptr;
+    int* d_ent_off = nullptr;
+    int* d_term_off = nullptr;
+    unsigned* d_terms = nullptr;
+    int* d_slot0 = nullptr;
+    int* d_nslot = nullptr;
+    int* d_gslot = nullptr;
+    double* d_gpart = nullptr;
+    double* d_scr_sigma = nullptr;
+    double* d_scr_lam = nullptr;
+    double* d_scr_H = nullptr;
+    hipEvent_t hev[2] = {nullptr, nullptr};
+    bool htimed = false;
     // device
     double* d_cst = nullptr;
     awt::ColorTabs* d_ct = nullptr;
@@ -656,6 +998,48 @@ size_t lds_fixed_bytes(int d) {
     }
 }
 
+size_t hess_lds_fixed_bytes(int d) {
+    switch (d) {
+        case 1: return sizeof(double) * hess_lds_fixed_doubles<1>();
+        case 2: return sizeof(double) * hess_lds_fixed_doubles<2>();
+        case 3: return sizeof(double) * hess_lds_fixed_doubles<3>();
+        case 4: return sizeof(double) * hess_lds_fixed_doubles<4>();
+        default: return sizeof(double) * hess_lds_fixed_doubles<5>();
+    }
+}
+
+int launch_hess(awe_handle h, const double* V, const double* P, const double* sigma, const double* lam,
+                double* H, hipStream_t stream) {
+    const awt::Ap2Tables& T = h->t;
+    const awt::Ap2HessTables& HT = h->ht;
+    HKArgs ha{};
+    KArgs& a = ha.a;
+    a.V = V; a.P = P; a.cst = h->d_cst; a.coll = T.dcoll; a.ct = h->d_ct;
+    a.n_k = T.n_k; a.d = T.d; a.n_v = T.lay.n_v; a.n_g = T.lay.n_g; a.n_p = T.lay.n_p;
+    a.nnz = T.nnz; a.batch = h->batch; a.stride = T.lay.stride; a.rows = T.lay.rows;
+    a.v_int0 = T.lay.v_int0; a.tang_total = T.tang_total;
+    ha.ht = h->d_ht; ha.tasks = h->d_tasks; ha.task_target = h->d_task_target; ha.ent_off = h->d_ent_off;
+    ha.term_off = h->d_term_off; ha.terms = h->d_terms; ha.slot0 = h->d_slot0; ha.nslot = h->d_nslot;
+    ha.gslot = h->d_gslot; ha.sigma = sigma; ha.lam = lam; ha.H = H; ha.gpart = h->d_gpart;
+    ha.hnnz = HT.nnz; ha.ng = (int)HT.gslot.size(); ha.hd_total = h->hd_total; ha.g_tftf = h->g_tftf;
+    dim3 grid(h->batch * T.n_k), block(kHessThreads);
+    HIP_TRY(hipEventRecord(h->hev[0], stream));
+    switch (T.d) {
+        case 1: hipLaunchKernelGGL(ap2_hess_kernel<1>, grid, block, h->hess_lds_bytes, stream, ha); break;
+        case 2: hipLaunchKernelGGL(ap2_hess_kernel<2>, grid, block, h->hess_lds_bytes, stream, ha); break;
+        case 3: hipLaunchKernelGGL(ap2_hess_kernel<3>, grid, block, h->hess_lds_bytes, stream, ha); break;
+        case 4: hipLaunchKernelGGL(ap2_hess_kernel<4>, grid, block, h->hess_lds_bytes, stream, ha); break;
+        case 5: hipLaunchKernelGGL(ap2_hess_kernel<5>, grid, block, h->hess_lds_bytes, stream, ha); break;
+        default: return fail(AWE_ERR_ARG, "unsupported collocation degree");
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->hev[1], stream));
+    hipLaunchKernelGGL(ap2_hess_finalize_kernel, dim3(h->batch), dim3(64), 0, stream, ha);
+    HIP_TRY(hipGetLastError());
+    h->htimed = true;
+    return AWE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -685,6 +1069,16 @@ int awe_create(int n_k, int d, const double* consts, int n_consts, int batch, aw
     const awt::Ap2Tables& T = h->t;
     h->lds_bytes = lds_fixed_bytes(d) + sizeof(double) * (size_t)(T.tang_total + 1);
     if (h->lds_bytes > 65536) { delete h; return fail(AWE_ERR_ARG, "internal: LDS image exceeds 64 KiB"); }
+    rc = awt::build_hess_tables(T, h->ht, err);
+    if (rc) { delete h; return fail(rc, err); }
+    const awt::Ap2HessTables& HT = h->ht;
+    h->hd_total = HT.ht.npairs[0] + d * HT.ht.npairs[1];
+    h->hess_lds_bytes = hess_lds_fixed_bytes(d) + sizeof(double) * (size_t)(T.tang_total + 1 + h->hd_total);
+    if (h->hess_lds_bytes > 65536) { delete h; return fail(AWE_ERR_ARG, "internal: Hessian LDS image exceeds 64 KiB"); }
+    for (size_t g = 0; g < HT.gslot.size(); ++g) {
+        const int slot = HT.gslot[g], itf = T.lay.theta(1);
+        if (HT.row[slot] == itf && slot >= HT.colind[itf] && slot < HT.colind[itf + 1]) h->g_tftf = (int)g;
+    }
 
 #define ALLOC_COPY(dst, src, n)                                                     \
     HIP_TRY(hipMalloc((void**)&dst, sizeof(*dst) * (n)));                          \
@@ -694,7 +1088,18 @@ int awe_create(int n_k, int d, const double* consts, int n_consts, int batch, aw
     ALLOC_COPY(h->d_seg, T.seg.data(), T.seg.size());
     ALLOC_COPY(h->d_glist, T.glist.data(), T.glist.size());
     ALLOC_COPY(h->d_glist_off, T.glist_off.data(), T.glist_off.size());
+    ALLOC_COPY(h->d_ht, &HT.ht, 1);
+    ALLOC_COPY(h->d_tasks, HT.tasks.data(), HT.tasks.size());
+    ALLOC_COPY(h->d_task_target, HT.task_target.data(), HT.task_target.size());
+    ALLOC_COPY(h->d_ent_off, HT.ent_off.data(), HT.ent_off.size());
+    ALLOC_COPY(h->d_term_off, HT.term_off.data(), HT.term_off.size());
+    ALLOC_COPY(h->d_terms, HT.terms.data(), HT.terms.size());
+    ALLOC_COPY(h->d_slot0, HT.slot0.data(), HT.slot0.size());
+    ALLOC_COPY(h->d_nslot, HT.nslot.data(), HT.nslot.size());
+    ALLOC_COPY(h->d_gslot, HT.gslot.data(), HT.gslot.size());
 #undef ALLOC_COPY
+    HIP_TRY(hipMalloc((void**)&h->d_gpart, sizeof(double) * (size_t)batch * n_k * std::max<size_t>(1, HT.gslot.size())));
+    for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreate(&h->hev[i]));
     HIP_TRY(hipMalloc((void**)&h->d_partial, sizeof(double) * (size_t)batch * n_k * kNPartial));
     for (int i = 0; i < 3; ++i) HIP_TRY(hipEventCreate(&h->ev[i]));
     *out = h;
@@ -724,7 +1129,12 @@ int awe_destroy(awe_handle h) {
     hipFree(h->d_glist); hipFree(h->d_glist_off); hipFree(h->d_partial);
     hipFree(h->d_scr_jac); hipFree(h->d_scr_grad); hipFree(h->d_scr_g); hipFree(h->d_scr_f);
     hipFree(h->d_in_V); hipFree(h->d_in_P);
+    hipFree(h->d_ht); hipFree(h->d_tasks); hipFree(h->d_task_target); hipFree(h->d_ent_off);
+    hipFree(h->d_term_off); hipFree(h->d_terms); hipFree(h->d_slot0); hipFree(h->d_nslot);
+    hipFree(h->d_gslot); hipFree(h->d_gpart); hipFree(h->d_scr_sigma); hipFree(h->d_scr_lam);
+    hipFree(h->d_scr_H);
     for (int i = 0; i < 3; ++i) if (h->ev[i]) hipEventDestroy(h->ev[i]);
+    for (int i = 0; i < 2; ++i) if (h->hev[i]) hipEventDestroy(h->hev[i]);
     delete h;
     return AWE_OK;
 }
@@ -797,6 +1207,74 @@ int awe_eval_nlp_host(awe_handle h, const double* V, const double* P, double* f,
     if (!finite(f, nb) || !finite(g, nb * h->t.lay.n_g) || !finite(grad_f, nb * h->t.lay.n_v) ||
         !finite(jac, nb * h->t.nnz))
         return fail(AWE_ERR_NONFINITE, "non-finite value in NLP evaluation");
+    return AWE_OK;
+}
+
+int awe_hess_nnz(awe_handle h, int* nnz_h) {
+    if (!h || !nnz_h) return fail(AWE_ERR_ARG, "null argument");
+    *nnz_h = h->ht.nnz;
+    return AWE_OK;
+}
+
+int awe_sparsity_hess(awe_handle h, int* colind, int* row) {
+    if (!h || !colind || !row) return fail(AWE_ERR_ARG, "null argument");
+    std::memcpy(colind, h->ht.colind.data(), sizeof(int) * h->ht.colind.size());
+    std::memcpy(row, h->ht.row.data(), sizeof(int) * h->ht.row.size());
+    return AWE_OK;
+}
+
+int awe_sparsity_hess_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind,
+                             int* row) {
+    if (!consts || !nnz) return fail(AWE_ERR_ARG, "null argument");
+    if (n_consts != AWE_NCONST) return fail(AWE_ERR_ARG, "consts must have AWE_NCONST entries");
+    if (n_k < 1 || d < 1 || d > 5) return fail(AWE_ERR_ARG, "bad n_k/d");
+    if ((int)consts[AWE_C_N_K] != n_k || (int)consts[AWE_C_D] != d)
+        return fail(AWE_ERR_ARG, "consts n_k/d mismatch");
+    awt::Ap2Tables T;
+    awt::Ap2HessTables H;
+    std::string err;
+    int rc = awt::build_ap2_tables(n_k, d, consts, n_consts, T, err);
+    if (!rc) rc = awt::build_hess_tables(T, H, err);
+    if (rc) return fail(rc, err);
+    *nnz = H.nnz;
+    if (colind) std::memcpy(colind, H.colind.data(), sizeof(int) * H.colind.size());
+    if (row) std::memcpy(row, H.row.data(), sizeof(int) * H.row.size());
+    return AWE_OK;
+}
+
+int awe_eval_hess(awe_handle h, const double* V, const double* P, const double* sigma, const double* lam_g,
+                  double* H, void* stream) {
+    if (!h || !V || !P || !sigma || !lam_g || !H) return fail(AWE_ERR_ARG, "null argument");
+    return launch_hess(h, V, P, sigma, lam_g, H, (hipStream_t)stream);
+}
+
+int awe_eval_hess_host(awe_handle h, const double* V, const double* P, const double* sigma,
+                       const double* lam_g, double* H) {
+    if (!h || !V || !P || !sigma || !lam_g || !H) return fail(AWE_ERR_ARG, "null argument");
+    const size_t nb = (size_t)h->batch;
+    const awt::Ap2Tables& T = h->t;
+    if (!h->d_in_V) HIP_TRY(hipMalloc((void**)&h->d_in_V, sizeof(double) * nb * T.lay.n_v));
+    if (!h->d_in_P) HIP_TRY(hipMalloc((void**)&h->d_in_P, sizeof(double) * nb * T.lay.n_p));
+    if (!h->d_scr_sigma) HIP_TRY(hipMalloc((void**)&h->d_scr_sigma, sizeof(double) * nb));
+    if (!h->d_scr_lam) HIP_TRY(hipMalloc((void**)&h->d_scr_lam, sizeof(double) * nb * T.lay.n_g));
+    if (!h->d_scr_H) HIP_TRY(hipMalloc((void**)&h->d_scr_H, sizeof(double) * nb * h->ht.nnz));
+    HIP_TRY(hipMemcpy(h->d_in_V, V, sizeof(double) * nb * T.lay.n_v, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->d_in_P, P, sizeof(double) * nb * T.lay.n_p, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->d_scr_sigma, sigma, sizeof(double) * nb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->d_scr_lam, lam_g, sizeof(double) * nb * T.lay.n_g, hipMemcpyHostToDevice));
+    int rc = launch_hess(h, h->d_in_V, h->d_in_P, h->d_scr_sigma, h->d_scr_lam, h->d_scr_H, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(H, h->d_scr_H, sizeof(double) * nb * h->ht.nnz, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nb * h->ht.nnz; ++i)
+        if (!std::isfinite(H[i])) return fail(AWE_ERR_NONFINITE, "non-finite value in the Hessian");
+    return AWE_OK;
+}
+
+int awe_last_hess_ms(awe_handle h, float* ms) {
+    if (!h || !h->htimed || !ms) return fail(AWE_ERR_ARG, "no timed Hessian launch yet");
+    HIP_TRY(hipEventSynchronize(h->hev[1]));
+    HIP_TRY(hipEventElapsedTime(ms, h->hev[0], h->hev[1]));
     return AWE_OK;
 }
 

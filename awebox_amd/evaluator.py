@@ -26,7 +26,8 @@ AWE_OK, AWE_ERR_ARG, AWE_ERR_HIP, AWE_ERR_NONFINITE, AWE_ERR_NODEVICE = 0, 1, 2,
 EXPORTED_SYMBOLS = ["awe_create", "awe_destroy", "awe_last_error", "awe_sizes", "awe_sparsity_jac",
                     "awe_sparsity_jac_static",
                     "awe_eval_nlp", "awe_eval_g", "awe_eval_f", "awe_eval_nlp_host",
-                    "awe_last_kernel_ms", "awe_device_count"]
+                    "awe_last_kernel_ms", "awe_device_count", "awe_hess_nnz", "awe_sparsity_hess",
+                    "awe_sparsity_hess_static", "awe_eval_hess", "awe_eval_hess_host", "awe_last_hess_ms"]
 
 
 class AwegpuUnavailable(RuntimeError):
@@ -60,6 +61,12 @@ def load_library(path: str = _LIB_PATH):
     lib.awe_last_kernel_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.awe_device_count.restype = ctypes.c_int
     lib.awe_sparsity_jac_static.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip]
+    lib.awe_sparsity_hess_static.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip]
+    lib.awe_hess_nnz.argtypes = [h, ip]
+    lib.awe_sparsity_hess.argtypes = [h, ip, ip]
+    lib.awe_eval_hess.argtypes = [h] + [ctypes.c_void_p] * 6
+    lib.awe_eval_hess_host.argtypes = [h, dp, dp, dp, dp, dp]
+    lib.awe_last_hess_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float)]
     _LIB = lib
     return lib
 
@@ -79,6 +86,26 @@ def sparsity_jac_static(consts: pb.Ap2Constants):
     row = np.zeros(nnz.value, dtype=np.int32)
     rc = lib.awe_sparsity_jac_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
                                      colind.ctypes.data_as(ip), row.ctypes.data_as(ip))
+    if rc != AWE_OK:
+        raise AwegpuError(lib.awe_last_error().decode())
+    return colind, row
+
+
+def sparsity_hess_static(consts: pb.Ap2Constants):
+    """Upper-triangular CCS pattern (colind, row) of nlp_hess_l derived on the CPU."""
+    lib = load_library()
+    cfg = consts.cfg
+    c = np.ascontiguousarray(consts.consts, dtype=np.float64)
+    nnz = ctypes.c_int()
+    ip = ctypes.POINTER(ctypes.c_int)
+    rc = lib.awe_sparsity_hess_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz), None, None)
+    if rc != AWE_OK:
+        raise AwegpuError(lib.awe_last_error().decode())
+    lay = pb.NlpLayout(cfg.n_k, cfg.d)
+    colind = np.zeros(lay.n_v + 1, dtype=np.int32)
+    row = np.zeros(nnz.value, dtype=np.int32)
+    rc = lib.awe_sparsity_hess_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
+                                      colind.ctypes.data_as(ip), row.ctypes.data_as(ip))
     if rc != AWE_OK:
         raise AwegpuError(lib.awe_last_error().decode())
     return colind, row
@@ -113,6 +140,13 @@ class Ap2Evaluator:
         ip = ctypes.POINTER(ctypes.c_int)
         self._check(self._lib.awe_sparsity_jac(self._h, self._colind.ctypes.data_as(ip),
                                                self._row.ctypes.data_as(ip)))
+        hn = ctypes.c_int()
+        self._check(self._lib.awe_hess_nnz(self._h, ctypes.byref(hn)))
+        self.nnz_h = hn.value
+        self._hcolind = np.zeros(self.n_v + 1, dtype=np.int32)
+        self._hrow = np.zeros(self.nnz_h, dtype=np.int32)
+        self._check(self._lib.awe_sparsity_hess(self._h, self._hcolind.ctypes.data_as(ip),
+                                                self._hrow.ctypes.data_as(ip)))
 
     # -------------------------------------------------------------------------------
     def _check(self, rc):
@@ -160,6 +194,49 @@ class Ap2Evaluator:
         import torch
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         self._check(self._lib.awe_eval_f(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), ctypes.c_void_p(s)))
+
+    def eval_hess_device(self, V, P, sigma, lam_g, H, stream=None):
+        """Upper-triangular CCS values of the Hessian of sigma f + lam_g^T g for all batch
+        members: sigma [B], lam_g [B, n_g], H [B, nnz_h] contiguous float64 CUDA tensors."""
+        import torch
+        for t, n in ((V, self.n_v), (P, self.n_p), (sigma, 1), (lam_g, self.n_g), (H, self.nnz_h)):
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
+                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.awe_eval_hess(self._h, V.data_ptr(), P.data_ptr(), sigma.data_ptr(),
+                                            lam_g.data_ptr(), H.data_ptr(), ctypes.c_void_p(s)))
+
+    def eval_hess(self, V, P, sigma, lam_g):
+        """Host arrays in, host array out: H [B, nnz_h] (upper triangle, CCS)."""
+        V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))
+        P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(self.batch, self.n_p))
+        sig = np.ascontiguousarray(np.broadcast_to(np.asarray(sigma, dtype=np.float64), (self.batch,)))
+        lam = np.ascontiguousarray(np.asarray(lam_g, dtype=np.float64).reshape(self.batch, self.n_g))
+        H = np.zeros((self.batch, self.nnz_h))
+        self._check(self._lib.awe_eval_hess_host(self._h, _dptr(V), _dptr(P), _dptr(sig), _dptr(lam), _dptr(H)))
+        return H
+
+    def sparsity_hess(self):
+        """Upper-triangular CCS pattern of nlp_hess_l: (colind[n_v+1], row[nnz_h])."""
+        return self._hcolind.copy(), self._hrow.copy()
+
+    def hess_csc(self, values, full=True):
+        """scipy matrix from upper-triangular values; full=True adds the strict lower triangle."""
+        import scipy.sparse as sp
+        U = sp.csc_matrix((np.asarray(values), self._hrow, self._hcolind), shape=(self.n_v, self.n_v))
+        return (U + sp.triu(U, 1).T).tocsc() if full else U
+
+    def nlp_hess_l(self, x, p, lam_f, lam_g):
+        """CasADi nlp_hess_l: Hessian of lam_f f + lam_g^T g (upper triangle, CCS values)."""
+        if self.batch != 1:
+            raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
+        return self.eval_hess(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1), lam_f,
+                              np.asarray(lam_g).reshape(1, -1))[0]
+
+    def last_hess_ms(self):
+        a = ctypes.c_float()
+        self._check(self._lib.awe_last_hess_ms(self._h, ctypes.byref(a)))
+        return a.value
 
     def last_kernel_ms(self):
         a, b = ctypes.c_float(), ctypes.c_float()

@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--batch", type=int, default=512, help="NLP instances per step and GPU")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per thread setting")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-hessian", action="store_true", help="skip the nlp_hess_l timing block")
     args = ap.parse_args()
 
     import numpy as np
@@ -190,11 +191,35 @@ def main():
                         "flops_per_launch": flops, "note": "FP64 VALU instructions x 64 lanes (FMA = 2), "
                         "from the PMC record; idle lanes of issued instructions count"}
         line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
+    if not args.no_hessian:
+        line["hessian"] = hessian_block(ev, V, P, B, lay, dev)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(consts, lay, v0, args.cpu_seconds)
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def hessian_block(ev, V, P, B, lay, dev, steps=10):
+    """nlp_hess_l throughput (sigma = 1, lam ~ N(0,1) seed 7), reported beside the
+    headline metric; kernel time from the library's HIP events."""
+    import numpy as np
+    import torch
+    sig = torch.ones(B, dtype=torch.float64, device=dev)
+    lam = torch.tensor(np.random.default_rng(7).standard_normal((B, lay.n_g)), device=dev)
+    H = torch.empty(B, ev.nnz_h, dtype=torch.float64, device=dev)
+    ev.eval_hess_device(V, P, sig, lam, H)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(steps):
+        ev.eval_hess_device(V, P, sig, lam, H)
+        kms.append(ev.last_hess_ms())
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"metric": "nlp_hess_l evals/sec", "value": B / dt, "unit": "evals/s", "ms_per_step": dt * 1e3,
+            "kernel_ms": float(np.mean(kms)), "nnz_h": ev.nnz_h, "batch": B,
+            "finite": bool(torch.isfinite(H).all().item())}
 
 
 def cpu_baseline(consts, lay, v0, seconds):

@@ -13,6 +13,8 @@
  *   awe_eval_g        <->  nlp_g       (g)
  *   awe_eval_nlp      <->  nlp_grad_f + nlp_jac_g fused (f, g, grad f, J_g values)
  *   awe_sparsity_jac  <->  Sparsity of nlp_jac_g's output (CCS: colind[n_v+1], row[nnz])
+ *   awe_eval_hess     <->  nlp_hess_l  (Hessian of sigma f + lam_g^T g, upper triangle)
+ *   awe_sparsity_hess <->  Sparsity of nlp_hess_l's output (upper-triangular CCS)
  *
  * Memory: V[b*n_v + i], P[b*n_p + i], g[b*n_g + i], grad_f[b*n_v + i], jac[b*nnz + i] and f[b]
  * are *device* pointers (HBM-resident, caller-owned) for the awe_eval_* functions and *host*
@@ -132,6 +134,20 @@ int awe_eval_f(awe_handle h, const double* V, const double* P, double* f, void* 
 /* Host-pointer wrappers: copy in, evaluate, copy out, synchronise, check finiteness. */
 int awe_eval_nlp_host(awe_handle h, const double* V, const double* P, double* f, double* g,
                       double* grad_f, double* jac);
+
+/* Hessian of the Lagrangian sigma f + lam_g^T g (nlp_hess_l):
+ * values of its upper triangle (row <= col) in the fixed CCS pattern of awe_sparsity_hess.
+ * sigma[b] and lam_g[b*n_g + i] per instance (device pointers for awe_eval_hess). */
+int awe_hess_nnz(awe_handle h, int* nnz_h);
+int awe_sparsity_hess(awe_handle h, int* colind, int* row);
+int awe_sparsity_hess_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind,
+                             int* row);
+int awe_eval_hess(awe_handle h, const double* V, const double* P, const double* sigma, const double* lam_g,
+                  double* H, void* stream);
+int awe_eval_hess_host(awe_handle h, const double* V, const double* P, const double* sigma,
+                       const double* lam_g, double* H);
+/* Kernel time of the last awe_eval_hess call (HIP events), milliseconds. */
+int awe_last_hess_ms(awe_handle h, float* ms);
 
 /* Kernel time of the last awe_eval_* call on its stream, in milliseconds (HIP events). */
 int awe_last_kernel_ms(awe_handle h, float* ms_main, float* ms_finalize);

@@ -138,3 +138,50 @@ def test_nonfinite_is_an_evaluation_error(gpu):
     ev = Ap2Evaluator(consts, batch=1)
     with pytest.raises(AwegpuError, match="non-finite"):
         ev.eval_nlp(V, pb.pack_p(lay, consts, v0))
+
+
+def _close_hess(Hk, Ho, what="H"):
+    """Full symmetric matrices.  Entries outside the kernel pattern must be rounding-level zeros
+    (t_f cancels analytically in the power cost; the oracle keeps 1e-16-level residues)."""
+    Hk, Ho = sp.csc_matrix(Hk), sp.csc_matrix(Ho)
+    scale = max(abs(Ho).max(), 1e-300)
+    D = abs(Hk - Ho).tocoo()
+    ref = np.asarray(abs(Ho)[D.row, D.col]).ravel()
+    tol = RTOL * ref + ATOL_REL * scale
+    bad = D.data > tol
+    assert not bad.any(), f"{what}: {bad.sum()} entries off, worst {D.data[bad].max():.3e}"
+
+
+@pytest.mark.parametrize("n_k,d,member", [(40, 4, 3), (5, 3, 1), (3, 2, 2)])
+def test_hessian_matches_oracle(gpu, n_k, d, member):
+    from awebox_amd.evaluator import Ap2Evaluator
+    consts, lay, v0, orc = _setup(n_k, d)
+    V = batch_member(v0, lay, member)
+    P = pb.pack_p(lay, consts, v0, u_ref=7.0)
+    lam = np.random.default_rng(7).standard_normal(lay.n_g)       # SURVEY 8(d): sigma 1, lam ~ N(0,1)
+    ev = Ap2Evaluator(consts, batch=1)
+    H = ev.hess_csc(ev.eval_hess(V, P, 1.0, lam)[0])
+    Ho = orc.nlp_hess_l(V, P, 1.0, lam, lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES)
+    _close_hess(H, Ho)
+
+
+def test_hessian_batch_sigma_lambda_and_determinism(gpu):
+    torch = gpu
+    from awebox_amd.evaluator import Ap2Evaluator
+    consts, lay, v0, orc = _setup(5, 3)
+    B = 3
+    Vs = np.stack([batch_member(v0, lay, b) for b in range(B)])
+    Ps = np.stack([pb.pack_p(lay, consts, v0, u_ref=u) for u in (5.0, 6.0, 8.0)])
+    sig = np.array([1.0, 0.0, 2.5])
+    lams = np.random.default_rng(11).standard_normal((B, lay.n_g))
+    ev = Ap2Evaluator(consts, batch=B)
+    Hh = ev.eval_hess(Vs, Ps, sig, lams)
+    for b in range(B):
+        Ho = orc.nlp_hess_l(Vs[b], Ps[b], sig[b], lams[b], lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES)
+        _close_hess(ev.hess_csc(Hh[b]), Ho, f"H[{b}]")
+    dev = lambda a: torch.tensor(a, device="cuda")
+    Hd = torch.zeros(B, ev.nnz_h, dtype=torch.float64, device="cuda")
+    ev.eval_hess_device(dev(Vs), dev(Ps), dev(sig), dev(lams), Hd)
+    torch.cuda.synchronize()
+    assert np.array_equal(Hd.cpu().numpy(), Hh)
+    assert ev.last_hess_ms() > 0

@@ -56,3 +56,18 @@ def test_no_device_means_no_fallback(lib):
         pytest.skip("a GPU is visible")
     with pytest.raises(AwegpuUnavailable):
         Ap2Evaluator()
+
+
+def test_static_hessian_sparsity_equals_cpu_port(lib):
+    from awebox_amd.evaluator import sparsity_hess_static
+    from oracle.cpu_port import CpuPort
+    consts = pb.build_constants(pb.Ap2Config(n_k=5, d=3))
+    colind, row = sparsity_hess_static(consts)
+    port = CpuPort(consts)
+    port.hess_init()
+    assert np.array_equal(colind, port.hcolind) and np.array_equal(row, port.hrow)
+    # upper triangle, rows sorted within each column
+    cols = np.repeat(np.arange(len(colind) - 1), np.diff(colind))
+    assert (row <= cols).all()
+    for c in range(len(colind) - 1):
+        assert (np.diff(row[colind[c]:colind[c + 1]]) > 0).all()
