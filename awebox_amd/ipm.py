@@ -1,0 +1,395 @@
+"""Primal-dual interior-point NLP solver on the GPU.
+
+The reference hands the collocation NLP to IPOPT through ``casadi.nlpsol`` (opti/preparation.py:
+366-400) and drives it through the homotopy (opti/optimization.py:273-382).  IPOPT is not
+available here, so this module restates the IPOPT algorithm (Waechter & Biegler, Math. Prog.
+106, 2006) at the level the AP2 problem needs, with every piece of data on the device:
+
+* NLP functions, gradient, Jacobian and the exact Hessian of the Lagrangian come from the HIP
+  evaluator (awebox_amd.evaluator) on device tensors;
+* the primal-dual KKT system [W + Sigma + dw I, A^T; A, -dc I] is assembled densely in HBM and
+  factorised in fp64 by rocSOLVER through torch.linalg (LU); the inertia correction uses the
+  curvature test of Chiang & Zavala (2016) instead of an inertia-revealing factorisation;
+* fixed variables (lbx == ubx) are removed (IPOPT's fixed_variable_treatment=make_parameter);
+  inequality rows get slacks; gradient-based NLP scaling, bound push, monotone Fiacco-McCormick
+  barrier update, fraction-to-the-boundary rule and the filter line search follow IPOPT's
+  defaults (tol 1e-8, mu_init 0.1, kappa_mu 0.2, theta_mu 1.5, tau_min 0.99).
+
+What is left out: second-order corrections, the feasibility restoration phase (a failed line
+search ends the solve with status 'line_search_failure'), and quasi-Newton options.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import problem as pb
+
+
+@dataclass
+class IpmOptions:
+    tol: float = 1e-8
+    acceptable_tol: float = 1e-6
+    max_iter: int = 1000
+    mu_init: float = 0.1
+    kappa_eps: float = 10.0
+    kappa_mu: float = 0.2
+    theta_mu: float = 1.5
+    tau_min: float = 0.99
+    kappa_sigma: float = 1e10
+    bound_push: float = 1e-2
+    bound_frac: float = 1e-2
+    s_max: float = 100.0
+    nlp_scaling_max_gradient: float = 100.0
+    delta_w0: float = 1e-4
+    delta_w_min: float = 1e-20
+    delta_w_max: float = 1e40
+    delta_c: float = 1e-8
+    curvature_kappa: float = 1e-8
+    gamma_theta: float = 1e-5
+    gamma_phi: float = 1e-8
+    delta_switch: float = 1.0
+    s_theta: float = 1.1
+    s_phi: float = 2.3
+    eta_phi: float = 1e-8
+    alpha_min_frac: float = 0.05
+    max_backtracks: int = 40
+    verbose: bool = False
+
+
+@dataclass
+class IpmResult:
+    x: np.ndarray            # full V
+    lam_g: np.ndarray
+    f: float
+    status: str
+    iterations: int
+    kkt_error: float
+    constr_viol: float
+    seconds: float
+    log: list = field(default_factory=list)
+
+
+class DeviceNlp:
+    """Evaluator-backed NLP restricted to the free variables, with slacks for inequality rows."""
+
+    def __init__(self, ev, P, lbx, ubx, lbg, ubg, device):
+        self.ev, self.dev = ev, device
+        n_v, n_g = ev.n_v, ev.n_g
+        self.P = torch.tensor(np.asarray(P, dtype=np.float64).reshape(1, -1), device=device)
+        lbx, ubx = np.asarray(lbx, dtype=np.float64), np.asarray(ubx, dtype=np.float64)
+        self.fixed = lbx >= ubx
+        self.free = np.where(~self.fixed)[0]
+        self.n = len(self.free)
+        self.x_fix = np.where(self.fixed, lbx, 0.0)
+        lbg, ubg = np.asarray(lbg, dtype=np.float64), np.asarray(ubg, dtype=np.float64)
+        self.ineq = np.where(lbg < ubg)[0]
+        self.eq = np.where(lbg >= ubg)[0]
+        self.m, self.mI = n_g, len(self.ineq)
+        self.g_target = torch.tensor(np.where(lbg >= ubg, lbg, 0.0), device=device)
+        # bounds of y = [x_free; s]
+        yl = np.concatenate([lbx[self.free], lbg[self.ineq]])
+        yu = np.concatenate([ubx[self.free], ubg[self.ineq]])
+        self.yl = torch.tensor(yl, device=device)
+        self.yu = torch.tensor(yu, device=device)
+        self.has_l = torch.isfinite(self.yl)
+        self.has_u = torch.isfinite(self.yu)
+        self.ny = self.n + self.mI
+        # reduced patterns
+        col_map = -np.ones(n_v, dtype=np.int64)
+        col_map[self.free] = np.arange(self.n)
+        colind, row = ev.sparsity_jac()
+        jcol = np.repeat(np.arange(n_v), np.diff(colind))
+        keep = col_map[jcol] >= 0
+        self.j_keep = torch.tensor(np.where(keep)[0], device=device)
+        self.j_row = torch.tensor(row[keep].astype(np.int64), device=device)
+        self.j_col = torch.tensor(col_map[jcol[keep]], device=device)
+        hcolind, hrow = ev.sparsity_hess()
+        hcol = np.repeat(np.arange(n_v), np.diff(hcolind))
+        hk = (col_map[hcol] >= 0) & (col_map[hrow] >= 0)
+        self.h_keep = torch.tensor(np.where(hk)[0], device=device)
+        self.h_r = torch.tensor(col_map[hrow[hk]], device=device)
+        self.h_c = torch.tensor(col_map[hcol[hk]], device=device)
+        self.h_offdiag = self.h_r != self.h_c
+        self.s_row = torch.tensor(self.ineq.astype(np.int64), device=device)
+        # device buffers of the evaluator
+        B = 1
+        self.V = torch.tensor(self.x_fix.reshape(1, -1), device=device)
+        self.f = torch.zeros(B, dtype=torch.float64, device=device)
+        self.g = torch.zeros(B, n_g, dtype=torch.float64, device=device)
+        self.grad = torch.zeros(B, n_v, dtype=torch.float64, device=device)
+        self.jac = torch.zeros(B, ev.nnz, dtype=torch.float64, device=device)
+        self.H = torch.zeros(B, ev.nnz_h, dtype=torch.float64, device=device)
+        self.sig = torch.ones(B, dtype=torch.float64, device=device)
+        self.free_t = torch.tensor(self.free, device=device)
+        self.ineq_t = torch.tensor(self.ineq, device=device)
+        self.obj_scale = 1.0
+        self.c_scale = torch.ones(n_g, dtype=torch.float64, device=device)
+
+    def full_x(self, x):
+        self.V[0, self.free_t] = x
+        return self.V
+
+    def eval_all(self, x):
+        """f, grad_f (reduced), c(y) pieces: g(x) and the Jacobian values (reduced, scaled)."""
+        self.ev.eval_nlp_device(self.full_x(x), self.P, self.f, self.g, self.grad, self.jac)
+        f = self.f[0] * self.obj_scale
+        grad = self.grad[0, self.free_t] * self.obj_scale
+        g = self.g[0] * self.c_scale
+        jv = self.jac[0, self.j_keep] * self.c_scale[self.j_row]
+        return f, grad, g, jv
+
+    def eval_fg(self, x):
+        self.ev.eval_nlp_device(self.full_x(x), self.P, self.f, self.g, self.grad, self.jac)
+        return self.f[0] * self.obj_scale, self.g[0] * self.c_scale
+
+    def hess(self, x, lam):
+        """Hessian of obj_scale f + (c_scale lam)^T g, reduced upper values."""
+        lam_unscaled = (lam * self.c_scale).reshape(1, -1).contiguous()
+        self.sig[0] = self.obj_scale
+        self.ev.eval_hess_device(self.full_x(x), self.P, self.sig, lam_unscaled, self.H)
+        return self.H[0, self.h_keep]
+
+    def constraints(self, g, s):
+        """c(y) = [g_E - target; g_I - s] (scaled rows)."""
+        c = g - self.g_target * self.c_scale
+        c = c.clone()
+        c[self.ineq_t] = c[self.ineq_t] - s
+        return c
+
+
+def _dense_A(nlp, jv, N0, K):
+    """Write A = [J | -I_slack] into rows N0.. and its transpose (in place)."""
+    n, mI = nlp.n, nlp.mI
+    rows = N0 + nlp.j_row
+    K[rows, nlp.j_col] = jv
+    K[nlp.j_col, rows] = jv
+    srow = N0 + nlp.s_row
+    scol = n + torch.arange(mI, device=K.device)
+    K[srow, scol] = -1.0
+    K[scol, srow] = -1.0
+
+
+def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, opts: IpmOptions | None = None, device="cuda") -> IpmResult:
+    """Solve min f s.t. lbg <= g <= ubg, lbx <= x <= ubx with the GPU interior-point method."""
+    opts = opts or IpmOptions()
+    t_start = time.perf_counter()
+    dev = torch.device(device)
+    nlp = DeviceNlp(ev, P, lbx, ubx, lbg, ubg, dev)
+    n, mI, m, ny = nlp.n, nlp.mI, nlp.m, nlp.ny
+    N = ny + m
+    f64 = dict(dtype=torch.float64, device=dev)
+    log = []
+
+    # ---- initial point: bound push (IPOPT 3.6) -----------------------------------------------
+    x = torch.tensor(np.asarray(x0, dtype=np.float64)[nlp.free], **f64)
+    yl, yu, hl, hu = nlp.yl, nlp.yu, nlp.has_l, nlp.has_u
+
+    def push(y):
+        lo = torch.where(hl, yl, torch.full_like(yl, -1e300))
+        hi = torch.where(hu, yu, torch.full_like(yu, 1e300))
+        gap = torch.where(hl & hu, hi - lo, torch.full_like(yl, 1e300))
+        pl = torch.minimum(opts.bound_push * torch.clamp(lo.abs(), min=1.0), opts.bound_frac * gap)
+        pu = torch.minimum(opts.bound_push * torch.clamp(hi.abs(), min=1.0), opts.bound_frac * gap)
+        y = torch.where(hl, torch.maximum(y, lo + pl), y)
+        y = torch.where(hu, torch.minimum(y, hi - pu), y)
+        return y
+
+    # gradient-based NLP scaling at the starting point (IPOPT nlp_scaling_method)
+    f0, grad0, g0, jv0 = nlp.eval_all(push(torch.cat([x, torch.zeros(mI, **f64)]))[:n])
+    gmax = float(grad0.abs().max().item()) if n else 0.0
+    nlp.obj_scale = min(1.0, opts.nlp_scaling_max_gradient / gmax) if gmax > 0 else 1.0
+    rowmax = torch.zeros(m, **f64).index_reduce_(0, nlp.j_row, jv0.abs(), "amax", include_self=True)
+    nlp.c_scale = torch.clamp(opts.nlp_scaling_max_gradient / torch.clamp(rowmax, min=1e-300), max=1.0)
+    # slack bounds live in the scaled constraint space
+    cs_I = nlp.c_scale[nlp.ineq_t]
+    nlp.yl[n:] = torch.where(nlp.has_l[n:], nlp.yl[n:] * cs_I, nlp.yl[n:])
+    nlp.yu[n:] = torch.where(nlp.has_u[n:], nlp.yu[n:] * cs_I, nlp.yu[n:])
+
+    y = torch.cat([x, torch.zeros(mI, **f64)])
+    f, grad, g, jv = nlp.eval_all(y[:n])
+    y[n:] = g[nlp.ineq_t]
+    y = push(y)
+    lam = torch.zeros(m, **f64)
+    if lam0 is not None:
+        lam = torch.tensor(np.asarray(lam0, dtype=np.float64), **f64) / nlp.c_scale * nlp.obj_scale
+    zl = torch.where(hl, torch.ones(ny, **f64), torch.zeros(ny, **f64))
+    zu = torch.where(hu, torch.ones(ny, **f64), torch.zeros(ny, **f64))
+    mu = opts.mu_init
+    tau = max(opts.tau_min, 1.0 - mu)
+    filt = []
+    c = nlp.constraints(g, y[n:])
+    theta0 = float(c.abs().sum().item())
+    theta_max = 1e4 * max(1.0, theta0)
+    theta_min = 1e-4 * max(1.0, theta0)
+    delta_w_last = 0.0
+    K = torch.zeros(N, N, **f64)
+    status = "max_iter"
+    it = 0
+    kkt_err = math.inf
+
+    def gaps(yv):
+        dl = torch.where(hl, yv - yl, torch.ones_like(yv))
+        du = torch.where(hu, yu - yv, torch.ones_like(yv))
+        return dl, du
+
+    def barrier_phi(fv, yv):
+        dl, du = gaps(yv)
+        return fv - mu * (torch.log(dl[hl]).sum() + torch.log(du[hu]).sum())
+
+    def grad_y(gradv):
+        return torch.cat([gradv, torch.zeros(mI, **f64)])
+
+    def A_T_lam(jvv, lamv):
+        r = torch.zeros(ny, **f64)
+        r.index_add_(0, nlp.j_col, jvv * lamv[nlp.j_row])
+        r[n:] -= lamv[nlp.ineq_t]
+        return r
+
+    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_):
+        dl, du = gaps(yv)
+        dual = grad_y(gradv) + A_T_lam(jvv, lamv) - zlv + zuv
+        compl_l = torch.where(hl, dl * zlv - mu_, torch.zeros_like(yv))
+        compl_u = torch.where(hu, du * zuv - mu_, torch.zeros_like(yv))
+        nb = int(hl.sum().item() + hu.sum().item())
+        s_d = max(opts.s_max, (lamv.abs().sum() + zlv.abs().sum() + zuv.abs().sum()).item() / max(1, m + nb)) / opts.s_max
+        s_c = max(opts.s_max, (zlv.abs().sum() + zuv.abs().sum()).item() / max(1, nb)) / opts.s_max
+        e_dual = dual.abs().max().item() / s_d
+        e_pr = cv.abs().max().item() if m else 0.0
+        e_c = max(compl_l.abs().max().item(), compl_u.abs().max().item()) / s_c
+        return max(e_dual, e_pr, e_c), e_dual, e_pr, e_c
+
+    while it < opts.max_iter:
+        c = nlp.constraints(g, y[n:])
+        kkt_err, e_d, e_p, e_c = errors(grad, jv, c, y, lam, zl, zu, 0.0)
+        if kkt_err <= opts.tol:
+            status = "solve_succeeded"
+            break
+        # barrier update (monotone)
+        while True:
+            e_mu = errors(grad, jv, c, y, lam, zl, zu, mu)[0]
+            if e_mu > opts.kappa_eps * mu or mu <= opts.tol / 10 * 1.0000001:
+                break
+            mu = max(opts.tol / 10, min(opts.kappa_mu * mu, mu ** opts.theta_mu))
+            tau = max(opts.tau_min, 1.0 - mu)
+            filt = []
+        # ---- Newton system --------------------------------------------------------------------
+        hv = nlp.hess(y[:n], lam)
+        dl, du = gaps(y)
+        sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
+        grad_phi = grad_y(grad) - torch.where(hl, mu / dl, torch.zeros_like(y)) + torch.where(hu, mu / du, torch.zeros_like(y))
+        rhs = -torch.cat([grad_phi + A_T_lam(jv, lam), c])
+        delta_w = 0.0
+        delta_c = 0.0
+        for attempt in range(60):
+            K.zero_()
+            K[nlp.h_r, nlp.h_c] = hv
+            K[nlp.h_c[nlp.h_offdiag], nlp.h_r[nlp.h_offdiag]] = hv[nlp.h_offdiag]
+            idx = torch.arange(ny, device=dev)
+            K[idx, idx] += sigma + delta_w
+            _dense_A(nlp, jv, ny, K)
+            if delta_c > 0:
+                idm = torch.arange(ny, N, device=dev)
+                K[idm, idm] = -delta_c
+            try:
+                sol = torch.linalg.solve(K, rhs)
+                ok = bool(torch.isfinite(sol).all().item())
+            except RuntimeError:
+                ok = False
+            if ok:
+                dy = sol[:ny]
+                # curvature test on the Lagrangian block (inertia-free correction)
+                Wd = torch.zeros(ny, **f64)
+                Wd.index_add_(0, nlp.h_r, hv * dy[nlp.h_c])
+                Wd.index_add_(0, nlp.h_c[nlp.h_offdiag], hv[nlp.h_offdiag] * dy[nlp.h_r[nlp.h_offdiag]])
+                curv = float((dy * (Wd + (sigma + delta_w) * dy)).sum().item())
+                if curv >= opts.curvature_kappa * float((dy * dy).sum().item()):
+                    break
+            else:
+                delta_c = opts.delta_c * mu ** 0.25
+            if delta_w == 0.0:
+                delta_w = opts.delta_w0 if delta_w_last == 0.0 else max(opts.delta_w_min, delta_w_last / 3.0)
+            else:
+                delta_w *= 8.0 if delta_w_last > 0 else 100.0
+            if delta_w > opts.delta_w_max:
+                status = "inertia_correction_failed"
+                break
+        if status == "inertia_correction_failed":
+            break
+        if delta_w > 0:
+            delta_w_last = delta_w
+        dy, dlam = sol[:ny], sol[ny:]
+        dzl = torch.where(hl, mu / dl - zl - zl / dl * dy, torch.zeros_like(y))
+        dzu = torch.where(hu, mu / du - zu + zu / du * dy, torch.zeros_like(y))
+        # fraction to the boundary
+        def max_step(v, dv, mask_pos):
+            ratio = torch.where(mask_pos & (dv < 0), -tau * v / dv, torch.full_like(v, math.inf))
+            return min(1.0, float(ratio.min().item())) if ratio.numel() else 1.0
+        alpha_max = min(max_step(dl, dy, hl), max_step(du, -dy, hu))
+        alpha_z = min(max_step(zl, dzl, hl), max_step(zu, dzu, hu))
+        # ---- filter line search ----------------------------------------------------------------
+        theta = float(c.abs().sum().item())
+        phi = float(barrier_phi(f, y).item())
+        gphi_d = float((grad_phi * dy).sum().item())
+        alpha = alpha_max
+        alpha_min = opts.alpha_min_frac * min(opts.gamma_theta, opts.gamma_phi * theta / max(-gphi_d, 1e-300)
+                                               if gphi_d < 0 else opts.gamma_theta)
+        accepted = False
+        for _ in range(opts.max_backtracks):
+            yt = y + alpha * dy
+            ft, gt = nlp.eval_fg(yt[:n])
+            ct = nlp.constraints(gt, yt[n:])
+            theta_t = float(ct.abs().sum().item())
+            phi_t = float(barrier_phi(ft, yt).item())
+            if not (math.isfinite(theta_t) and math.isfinite(phi_t)):
+                alpha *= 0.5
+                continue
+            switching = gphi_d < 0 and alpha * (-gphi_d) ** opts.s_phi > opts.delta_switch * theta ** opts.s_theta
+            f_type = False
+            if theta <= theta_min and switching:
+                if phi_t <= phi + opts.eta_phi * alpha * gphi_d:
+                    accepted, f_type = True, True
+            else:
+                if theta_t <= theta_max and (theta_t <= (1 - opts.gamma_theta) * theta or
+                                             phi_t <= phi - opts.gamma_phi * theta):
+                    if all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt):
+                        accepted = True
+            if accepted:
+                if not f_type:
+                    filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
+                break
+            alpha *= 0.5
+            if alpha < alpha_min:
+                break
+        if not accepted:
+            status = "line_search_failure"
+            break
+        y = yt
+        lam = lam + alpha * dlam
+        zl = zl + alpha_z * dzl
+        zu = zu + alpha_z * dzu
+        # kappa_sigma safeguard
+        dl, du = gaps(y)
+        zl = torch.where(hl, torch.clamp(zl, min=mu / (opts.kappa_sigma * dl), max=opts.kappa_sigma * mu / dl), zl)
+        zu = torch.where(hu, torch.clamp(zu, min=mu / (opts.kappa_sigma * du), max=opts.kappa_sigma * mu / du), zu)
+        f, grad, g, jv = nlp.eval_all(y[:n])
+        it += 1
+        rec = dict(it=it, f=float(f.item()) / nlp.obj_scale, inf_pr=e_p, inf_du=e_d, mu=mu, alpha=alpha,
+                   alpha_z=alpha_z, delta_w=delta_w)
+        log.append(rec)
+        if opts.verbose:
+            print(f"{it:4d} f={rec['f']: .8e} pr={e_p:.2e} du={e_d:.2e} mu={mu:.1e} a={alpha:.2e} dw={delta_w:.1e}",
+                  flush=True)
+    if status == "max_iter" and kkt_err <= opts.acceptable_tol:
+        status = "solved_to_acceptable_level"
+    xf = nlp.x_fix.copy()
+    xf[nlp.free] = y[:n].cpu().numpy()
+    lam_out = (lam * nlp.c_scale / nlp.obj_scale).cpu().numpy()
+    c = nlp.constraints(g, y[n:])
+    return IpmResult(x=xf, lam_g=lam_out, f=float(f.item()) / nlp.obj_scale, status=status, iterations=it,
+                     kkt_error=kkt_err, constr_viol=float((c / nlp.c_scale).abs().max().item()) if m else 0.0,
+                     seconds=time.perf_counter() - t_start, log=log)

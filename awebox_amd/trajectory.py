@@ -1,0 +1,42 @@
+"""Trajectory optimisation of the AP2 power cycle on the GPU: the homotopy loop of
+awebox/opti/optimization.py:273-382 (solve_homotopy -> solve_specific_homotopy_step ->
+solve_general_homotopy_step) around the GPU interior-point solver (ipm.py) and the HIP
+evaluator.  Each step updates P's cost vector and the variable bounds (homotopy.schedule) and
+warm-starts from the previous solution and multipliers.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from . import homotopy as hm
+from . import problem as pb
+from .initial_guess import initial_guess
+from .ipm import IpmOptions, solve
+
+
+def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device="cuda",
+             v_init: np.ndarray | None = None, final_step: str | None = None, verbose=False):
+    """Run the homotopy; returns (V_opt, list of per-step summaries, outputs)."""
+    lay = pb.NlpLayout(consts.cfg.n_k, consts.cfg.d)
+    v0 = initial_guess(consts, lay) if v_init is None else v_init
+    steps = hm.schedule(consts, lay, v0)
+    lbg, ubg = lay.g_bounds()
+    x, lam = v0.copy(), None
+    summary = []
+    for st in steps:
+        P = pb.pack_p(lay, consts, v0, step=st.cost_step)
+        t0 = time.perf_counter()
+        res = solve(ev, P, x, st.lbx, st.ubx, lbg, ubg, lam0=lam, opts=opts, device=device)
+        out = hm.outputs(consts, lay, res.x)
+        rec = dict(step=st.label, status=res.status, iterations=res.iterations, f=res.f,
+                   kkt_error=res.kkt_error, constr_viol=res.constr_viol, seconds=time.perf_counter() - t0,
+                   **out)
+        summary.append(rec)
+        if verbose:
+            print(rec, flush=True)
+        x, lam = res.x, res.lam_g
+        if final_step is not None and st.label == final_step:
+            break
+    return x, summary, hm.outputs(consts, lay, x)
