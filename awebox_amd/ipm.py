@@ -36,6 +36,9 @@ class IpmOptions:
     acceptable_tol: float = 1e-6
     max_iter: int = 1000
     mu_init: float = 0.1
+    mu_target: float = 0.0           # barrier parameter floor; convergence is measured at it
+    warm_start_bound_push: float = 1e-3
+    warm_start_mult_bound_push: float = 1e-3
     kappa_eps: float = 10.0
     kappa_mu: float = 0.2
     theta_mu: float = 1.5
@@ -71,6 +74,8 @@ class IpmResult:
     kkt_error: float
     constr_viol: float
     seconds: float
+    zl: np.ndarray = None    # bound multipliers on V (lower / upper), for warm starts
+    zu: np.ndarray = None
     log: list = field(default_factory=list)
 
 
@@ -174,8 +179,13 @@ def _dense_A(nlp, jv, N0, K):
     K[scol, srow] = -1.0
 
 
-def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, opts: IpmOptions | None = None, device="cuda") -> IpmResult:
-    """Solve min f s.t. lbg <= g <= ubg, lbx <= x <= ubx with the GPU interior-point method."""
+def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: IpmOptions | None = None,
+          device="cuda") -> IpmResult:
+    """Solve min f s.t. lbg <= g <= ubg, lbx <= x <= ubx with the GPU interior-point method.
+
+    lam0 / zl0 / zu0 (constraint and V-bound multipliers of a previous solve) select IPOPT's
+    warm_start_init_point: the multipliers are kept (pushed away from zero) and the primal point
+    is pushed into the bounds with the smaller warm-start push."""
     opts = opts or IpmOptions()
     t_start = time.perf_counter()
     dev = torch.device(device)
@@ -189,12 +199,16 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, opts: IpmOptions | None = No
     x = torch.tensor(np.asarray(x0, dtype=np.float64)[nlp.free], **f64)
     yl, yu, hl, hu = nlp.yl, nlp.yu, nlp.has_l, nlp.has_u
 
+    warm = lam0 is not None
+    bpush = opts.warm_start_bound_push if warm else opts.bound_push
+    bfrac = opts.warm_start_bound_push if warm else opts.bound_frac
+
     def push(y):
         lo = torch.where(hl, yl, torch.full_like(yl, -1e300))
         hi = torch.where(hu, yu, torch.full_like(yu, 1e300))
         gap = torch.where(hl & hu, hi - lo, torch.full_like(yl, 1e300))
-        pl = torch.minimum(opts.bound_push * torch.clamp(lo.abs(), min=1.0), opts.bound_frac * gap)
-        pu = torch.minimum(opts.bound_push * torch.clamp(hi.abs(), min=1.0), opts.bound_frac * gap)
+        pl = torch.minimum(bpush * torch.clamp(lo.abs(), min=1.0), bfrac * gap)
+        pu = torch.minimum(bpush * torch.clamp(hi.abs(), min=1.0), bfrac * gap)
         y = torch.where(hl, torch.maximum(y, lo + pl), y)
         y = torch.where(hu, torch.minimum(y, hi - pu), y)
         return y
@@ -219,7 +233,20 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, opts: IpmOptions | None = No
         lam = torch.tensor(np.asarray(lam0, dtype=np.float64), **f64) / nlp.c_scale * nlp.obj_scale
     zl = torch.where(hl, torch.ones(ny, **f64), torch.zeros(ny, **f64))
     zu = torch.where(hu, torch.ones(ny, **f64), torch.zeros(ny, **f64))
+    if warm:
+        floor = opts.warm_start_mult_bound_push
+        if zl0 is not None:
+            zx = torch.tensor(np.asarray(zl0, dtype=np.float64)[nlp.free], **f64) * nlp.obj_scale
+            zl[:n] = torch.where(hl[:n], torch.clamp(zx, min=floor), zl[:n])
+        if zu0 is not None:
+            zx = torch.tensor(np.asarray(zu0, dtype=np.float64)[nlp.free], **f64) * nlp.obj_scale
+            zu[:n] = torch.where(hu[:n], torch.clamp(zx, min=floor), zu[:n])
+        # slack bound multipliers from the row multipliers: dL/ds = -lam - z_l + z_u = 0
+        lamI = lam[nlp.ineq_t]
+        zl[n:] = torch.where(hl[n:], torch.clamp(-lamI, min=floor), zl[n:])
+        zu[n:] = torch.where(hu[n:], torch.clamp(lamI, min=floor), zu[n:])
     mu = opts.mu_init
+    mu_floor = max(opts.mu_target, opts.tol / 10)
     tau = max(opts.tau_min, 1.0 - mu)
     filt = []
     c = nlp.constraints(g, y[n:])
@@ -265,16 +292,16 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, opts: IpmOptions | None = No
 
     while it < opts.max_iter:
         c = nlp.constraints(g, y[n:])
-        kkt_err, e_d, e_p, e_c = errors(grad, jv, c, y, lam, zl, zu, 0.0)
+        kkt_err, e_d, e_p, e_c = errors(grad, jv, c, y, lam, zl, zu, opts.mu_target)
         if kkt_err <= opts.tol:
             status = "solve_succeeded"
             break
         # barrier update (monotone)
         while True:
             e_mu = errors(grad, jv, c, y, lam, zl, zu, mu)[0]
-            if e_mu > opts.kappa_eps * mu or mu <= opts.tol / 10 * 1.0000001:
+            if e_mu > opts.kappa_eps * mu or mu <= mu_floor * 1.0000001:
                 break
-            mu = max(opts.tol / 10, min(opts.kappa_mu * mu, mu ** opts.theta_mu))
+            mu = max(mu_floor, min(opts.kappa_mu * mu, mu ** opts.theta_mu))
             tau = max(opts.tau_min, 1.0 - mu)
             filt = []
         # ---- Newton system --------------------------------------------------------------------
@@ -390,6 +417,10 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, opts: IpmOptions | None = No
     xf[nlp.free] = y[:n].cpu().numpy()
     lam_out = (lam * nlp.c_scale / nlp.obj_scale).cpu().numpy()
     c = nlp.constraints(g, y[n:])
+    zl_v = np.zeros(len(xf))
+    zu_v = np.zeros(len(xf))
+    zl_v[nlp.free] = (zl[:n] / nlp.obj_scale).cpu().numpy()
+    zu_v[nlp.free] = (zu[:n] / nlp.obj_scale).cpu().numpy()
     return IpmResult(x=xf, lam_g=lam_out, f=float(f.item()) / nlp.obj_scale, status=status, iterations=it,
                      kkt_error=kkt_err, constr_viol=float((c / nlp.c_scale).abs().max().item()) if m else 0.0,
-                     seconds=time.perf_counter() - t_start, log=log)
+                     seconds=time.perf_counter() - t_start, zl=zl_v, zu=zu_v, log=log)

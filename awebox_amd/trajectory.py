@@ -16,6 +16,20 @@ from .initial_guess import initial_guess
 from .ipm import IpmOptions, solve
 
 
+def hippo_options(label: str, base: IpmOptions | None = None) -> IpmOptions:
+    """awebox's hippo strategy (preparation.py:285-323, default.py:324-351): the initial and
+    intermediate homotopy steps stop at the barrier parameter mu_target = 1e-2 with tol 1e-4
+    (initial: mu_init 1, cold start; middle: mu_init 1e-2, warm start); the final step starts at
+    mu_init 1e-2 and converges to tol 1e-8 (mu_target 0)."""
+    import dataclasses
+    base = base or IpmOptions()
+    if label.startswith("initial"):
+        return dataclasses.replace(base, mu_init=1.0, mu_target=1e-2, tol=1e-4)
+    if label.startswith("final"):
+        return dataclasses.replace(base, mu_init=1e-2, mu_target=0.0, tol=1e-8)
+    return dataclasses.replace(base, mu_init=1e-2, mu_target=1e-2, tol=1e-4)
+
+
 def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device="cuda",
              v_init: np.ndarray | None = None, final_step: str | None = None, verbose=False):
     """Run the homotopy; returns (V_opt, list of per-step summaries, outputs)."""
@@ -23,12 +37,13 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
     v0 = initial_guess(consts, lay) if v_init is None else v_init
     steps = hm.schedule(consts, lay, v0)
     lbg, ubg = lay.g_bounds()
-    x, lam = v0.copy(), None
+    x, lam, zl, zu = v0.copy(), None, None, None
     summary = []
     for st in steps:
         P = pb.pack_p(lay, consts, v0, step=st.cost_step)
         t0 = time.perf_counter()
-        res = solve(ev, P, x, st.lbx, st.ubx, lbg, ubg, lam0=lam, opts=opts, device=device)
+        res = solve(ev, P, x, st.lbx, st.ubx, lbg, ubg, lam0=lam, zl0=zl, zu0=zu,
+                    opts=hippo_options(st.label, opts), device=device)
         out = hm.outputs(consts, lay, res.x)
         rec = dict(step=st.label, status=res.status, iterations=res.iterations, f=res.f,
                    kkt_error=res.kkt_error, constr_viol=res.constr_viol, seconds=time.perf_counter() - t0,
@@ -36,7 +51,7 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
         summary.append(rec)
         if verbose:
             print(rec, flush=True)
-        x, lam = res.x, res.lam_g
+        x, lam, zl, zu = res.x, res.lam_g, res.zl, res.zu
         if final_step is not None and st.label == final_step:
             break
     return x, summary, hm.outputs(consts, lay, x)
