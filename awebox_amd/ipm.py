@@ -217,7 +217,7 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
     f0, grad0, g0, jv0 = nlp.eval_all(push(torch.cat([x, torch.zeros(mI, **f64)]))[:n])
     gmax = float(grad0.abs().max().item()) if n else 0.0
     nlp.obj_scale = min(1.0, opts.nlp_scaling_max_gradient / gmax) if gmax > 0 else 1.0
-    rowmax = torch.zeros(m, **f64).index_reduce_(0, nlp.j_row, jv0.abs(), "amax", include_self=True)
+    rowmax = torch.zeros(m, **f64).scatter_reduce_(0, nlp.j_row, jv0.abs(), "amax", include_self=True)
     nlp.c_scale = torch.clamp(opts.nlp_scaling_max_gradient / torch.clamp(rowmax, min=1e-300), max=1.0)
     # slack bounds live in the scaled constraint space
     cs_I = nlp.c_scale[nlp.ineq_t]
@@ -290,6 +290,64 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
         e_c = max(compl_l.abs().max().item(), compl_u.abs().max().item()) / s_c
         return max(e_dual, e_pr, e_c), e_dual, e_pr, e_c
 
+    def assemble(Kmat, hv, sigma, delta_w, delta_c):
+        Kmat.zero_()
+        if hv is not None:
+            Kmat[nlp.h_r, nlp.h_c] = hv
+            Kmat[nlp.h_c[nlp.h_offdiag], nlp.h_r[nlp.h_offdiag]] = hv[nlp.h_offdiag]
+        idx = torch.arange(ny, device=dev)
+        Kmat[idx, idx] += sigma + delta_w
+        _dense_A(nlp, jv, ny, Kmat)
+        if delta_c > 0:
+            idm = torch.arange(ny, N, device=dev)
+            Kmat[idm, idm] = -delta_c
+
+    def max_step(v, dv, mask_pos):
+        ratio = torch.where(mask_pos & (dv < 0), -tau * v / dv, torch.full_like(v, math.inf))
+        return min(1.0, float(ratio.min().item())) if ratio.numel() else 1.0
+
+    def restoration(y0, c0, theta0_, phi0_, max_steps=50):
+        """Minimum-norm Gauss-Newton corrections toward c(y) = 0, scaled by the barrier Sigma,
+        with backtracking on theta; returns (y, lam) once the point is acceptable to the filter."""
+        yv, cv, th = y0, c0, theta0_
+        lam_r = lam
+        for _ in range(max_steps):
+            _, _, g_c, jv_c = nlp.eval_all(yv[:n])
+            cv = nlp.constraints(g_c, yv[n:])
+            th = float(cv.abs().sum().item())
+            dlv, duv = gaps(yv)
+            sig = torch.where(hl, 1.0 / dlv ** 2, torch.zeros_like(yv)) + torch.where(hu, 1.0 / duv ** 2, torch.zeros_like(yv))
+            assemble_jv(K, jv_c, sig + 1e-8)
+            rhs = -torch.cat([torch.zeros(ny, **f64), cv])
+            try:
+                sol = torch.linalg.solve(K, rhs)
+            except RuntimeError:
+                return None
+            dyv = sol[:ny]
+            a = min(max_step(dlv, dyv, hl), max_step(duv, -dyv, hu))
+            for _ in range(30):
+                yt = yv + a * dyv
+                ft, gt = nlp.eval_fg(yt[:n])
+                ct = nlp.constraints(gt, yt[n:])
+                tht = float(ct.abs().sum().item())
+                if math.isfinite(tht) and tht < (1 - 1e-4 * a) * th:
+                    break
+                a *= 0.5
+            else:
+                return None
+            yv = yt
+            lam_r = lam_r + a * sol[ny:]
+            pht = float(barrier_phi(ft, yt).item())
+            if tht <= 0.9 * theta0_ and all(not (tht >= th_f and pht >= ph_f) for th_f, ph_f in filt):
+                return yv, lam_r
+        return None
+
+    def assemble_jv(Kmat, jv_c, diag):
+        Kmat.zero_()
+        idx = torch.arange(ny, device=dev)
+        Kmat[idx, idx] = diag
+        _dense_A(nlp, jv_c, ny, Kmat)
+
     while it < opts.max_iter:
         c = nlp.constraints(g, y[n:])
         kkt_err, e_d, e_p, e_c = errors(grad, jv, c, y, lam, zl, zu, opts.mu_target)
@@ -309,92 +367,104 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
         dl, du = gaps(y)
         sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
         grad_phi = grad_y(grad) - torch.where(hl, mu / dl, torch.zeros_like(y)) + torch.where(hu, mu / du, torch.zeros_like(y))
-        rhs = -torch.cat([grad_phi + A_T_lam(jv, lam), c])
-        delta_w = 0.0
-        delta_c = 0.0
-        for attempt in range(60):
-            K.zero_()
-            K[nlp.h_r, nlp.h_c] = hv
-            K[nlp.h_c[nlp.h_offdiag], nlp.h_r[nlp.h_offdiag]] = hv[nlp.h_offdiag]
-            idx = torch.arange(ny, device=dev)
-            K[idx, idx] += sigma + delta_w
-            _dense_A(nlp, jv, ny, K)
-            if delta_c > 0:
-                idm = torch.arange(ny, N, device=dev)
-                K[idm, idm] = -delta_c
-            try:
-                sol = torch.linalg.solve(K, rhs)
-                ok = bool(torch.isfinite(sol).all().item())
-            except RuntimeError:
-                ok = False
-            if ok:
-                dy = sol[:ny]
-                # curvature test on the Lagrangian block (inertia-free correction)
-                Wd = torch.zeros(ny, **f64)
-                Wd.index_add_(0, nlp.h_r, hv * dy[nlp.h_c])
-                Wd.index_add_(0, nlp.h_c[nlp.h_offdiag], hv[nlp.h_offdiag] * dy[nlp.h_r[nlp.h_offdiag]])
-                curv = float((dy * (Wd + (sigma + delta_w) * dy)).sum().item())
-                if curv >= opts.curvature_kappa * float((dy * dy).sum().item()):
-                    break
-            else:
-                delta_c = opts.delta_c * mu ** 0.25
-            if delta_w == 0.0:
-                delta_w = opts.delta_w0 if delta_w_last == 0.0 else max(opts.delta_w_min, delta_w_last / 3.0)
-            else:
-                delta_w *= 8.0 if delta_w_last > 0 else 100.0
-            if delta_w > opts.delta_w_max:
-                status = "inertia_correction_failed"
-                break
-        if status == "inertia_correction_failed":
-            break
-        if delta_w > 0:
-            delta_w_last = delta_w
-        dy, dlam = sol[:ny], sol[ny:]
-        dzl = torch.where(hl, mu / dl - zl - zl / dl * dy, torch.zeros_like(y))
-        dzu = torch.where(hu, mu / du - zu + zu / du * dy, torch.zeros_like(y))
-        # fraction to the boundary
-        def max_step(v, dv, mask_pos):
-            ratio = torch.where(mask_pos & (dv < 0), -tau * v / dv, torch.full_like(v, math.inf))
-            return min(1.0, float(ratio.min().item())) if ratio.numel() else 1.0
-        alpha_max = min(max_step(dl, dy, hl), max_step(du, -dy, hu))
-        alpha_z = min(max_step(zl, dzl, hl), max_step(zu, dzu, hu))
-        # ---- filter line search ----------------------------------------------------------------
         theta = float(c.abs().sum().item())
         phi = float(barrier_phi(f, y).item())
-        gphi_d = float((grad_phi * dy).sum().item())
-        alpha = alpha_max
-        alpha_min = opts.alpha_min_frac * min(opts.gamma_theta, opts.gamma_phi * theta / max(-gphi_d, 1e-300)
-                                               if gphi_d < 0 else opts.gamma_theta)
-        accepted = False
-        for _ in range(opts.max_backtracks):
-            yt = y + alpha * dy
-            ft, gt = nlp.eval_fg(yt[:n])
-            ct = nlp.constraints(gt, yt[n:])
-            theta_t = float(ct.abs().sum().item())
-            phi_t = float(barrier_phi(ft, yt).item())
-            if not (math.isfinite(theta_t) and math.isfinite(phi_t)):
+
+        def newton_direction(dw_floor):
+            """(dy, dlam, delta_w) with the curvature-tested inertia correction."""
+            nonlocal delta_w_last
+            rhs = -torch.cat([grad_phi + A_T_lam(jv, lam), c])
+            delta_w = dw_floor
+            delta_c = 0.0
+            for attempt in range(60):
+                assemble(K, hv, sigma, delta_w, delta_c)
+                try:
+                    sol = torch.linalg.solve(K, rhs)
+                    ok = bool(torch.isfinite(sol).all().item())
+                except RuntimeError:
+                    ok = False
+                if ok:
+                    dy = sol[:ny]
+                    Wd = torch.zeros(ny, **f64)
+                    Wd.index_add_(0, nlp.h_r, hv * dy[nlp.h_c])
+                    Wd.index_add_(0, nlp.h_c[nlp.h_offdiag], hv[nlp.h_offdiag] * dy[nlp.h_r[nlp.h_offdiag]])
+                    curv = float((dy * (Wd + (sigma + delta_w) * dy)).sum().item())
+                    if curv >= opts.curvature_kappa * float((dy * dy).sum().item()):
+                        if delta_w > 0:
+                            delta_w_last = delta_w
+                        return sol[:ny], sol[ny:], delta_w
+                else:
+                    delta_c = opts.delta_c * mu ** 0.25
+                if delta_w == 0.0:
+                    delta_w = opts.delta_w0 if delta_w_last == 0.0 else max(opts.delta_w_min, delta_w_last / 3.0)
+                else:
+                    delta_w *= 8.0 if delta_w_last > 0 else 100.0
+                if delta_w > opts.delta_w_max:
+                    return None
+            return None
+
+        def line_search(dy):
+            """Filter line search from the fraction-to-the-boundary step; (alpha, y_trial) or None."""
+            nonlocal filt
+            alpha = min(max_step(dl, dy, hl), max_step(du, -dy, hu))
+            gphi_d = float((grad_phi * dy).sum().item())
+            alpha_min = opts.alpha_min_frac * min(opts.gamma_theta, opts.gamma_phi * theta / max(-gphi_d, 1e-300)
+                                                   if gphi_d < 0 else opts.gamma_theta)
+            for _ in range(opts.max_backtracks):
+                yt = y + alpha * dy
+                ft, gt = nlp.eval_fg(yt[:n])
+                ct = nlp.constraints(gt, yt[n:])
+                theta_t = float(ct.abs().sum().item())
+                phi_t = float(barrier_phi(ft, yt).item())
+                if math.isfinite(theta_t) and math.isfinite(phi_t):
+                    switching = gphi_d < 0 and alpha * (-gphi_d) ** opts.s_phi > opts.delta_switch * theta ** opts.s_theta
+                    if theta <= theta_min and switching:
+                        if phi_t <= phi + opts.eta_phi * alpha * gphi_d:
+                            return alpha, yt
+                    elif theta_t <= theta_max and (theta_t <= (1 - opts.gamma_theta) * theta or
+                                                   phi_t <= phi - opts.gamma_phi * theta):
+                        if all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt):
+                            filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
+                            return alpha, yt
                 alpha *= 0.5
+                if alpha < alpha_min:
+                    break
+            return None
+
+        accepted = None
+        delta_w = 0.0
+        for dw_floor in (0.0, 1e-2, 1.0, 1e2):
+            nd = newton_direction(dw_floor)
+            if nd is None:
                 continue
-            switching = gphi_d < 0 and alpha * (-gphi_d) ** opts.s_phi > opts.delta_switch * theta ** opts.s_theta
-            f_type = False
-            if theta <= theta_min and switching:
-                if phi_t <= phi + opts.eta_phi * alpha * gphi_d:
-                    accepted, f_type = True, True
-            else:
-                if theta_t <= theta_max and (theta_t <= (1 - opts.gamma_theta) * theta or
-                                             phi_t <= phi - opts.gamma_phi * theta):
-                    if all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt):
-                        accepted = True
-            if accepted:
-                if not f_type:
-                    filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
+            dy, dlam, delta_w = nd
+            accepted = line_search(dy)
+            if accepted is not None:
                 break
-            alpha *= 0.5
-            if alpha < alpha_min:
+        if accepted is None:
+            # feasibility restoration: Gauss-Newton steps on ||c|| inside the bounds until the
+            # filter accepts the point (IPOPT's restoration phase, reduced to its core)
+            rest = restoration(y, c, theta, phi)
+            if rest is None:
+                status = "restoration_failed"
                 break
-        if not accepted:
-            status = "line_search_failure"
-            break
+            y, lam = rest
+            filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
+            dl, du = gaps(y)
+            zl = torch.where(hl, torch.clamp(mu / dl, max=1e3), zl)
+            zu = torch.where(hu, torch.clamp(mu / du, max=1e3), zu)
+            f, grad, g, jv = nlp.eval_all(y[:n])
+            it += 1
+            log.append(dict(it=it, f=float(f.item()) / nlp.obj_scale, inf_pr=e_p, inf_du=e_d, mu=mu,
+                            alpha=0.0, alpha_z=0.0, delta_w=-1.0))
+            if opts.verbose:
+                print(f"{it:4d} restoration theta {theta:.3e} -> {float(nlp.constraints(g, y[n:]).abs().sum().item()):.3e}",
+                      flush=True)
+            continue
+        alpha, yt = accepted
+        dzl = torch.where(hl, mu / dl - zl - zl / dl * dy, torch.zeros_like(y))
+        dzu = torch.where(hu, mu / du - zu + zu / du * dy, torch.zeros_like(y))
+        alpha_z = min(max_step(zl, dzl, hl), max_step(zu, dzu, hu))
         y = yt
         lam = lam + alpha * dlam
         zl = zl + alpha_z * dzl
