@@ -1,0 +1,172 @@
+"""Wind-speed sweep of the AP2 power cycle, sharded across GPUs.
+
+The reference sweeps the trial over ``user_options.wind.u_ref`` sequentially, warm-starting each
+point from the previous one (awebox/sweep.py:120-163, examples/dual_kites_power_curve.py:48-52).
+Only ``P.theta0.wind.u_ref`` changes between points; the NLP (layout, scaling, bounds) is built
+once.  Here the points are independent work items, one process per GPU:
+
+* rank 0 builds the problem template (model constants + initial guess) and broadcasts it
+  (RCCL over xGMI when the backend is nccl, ~0.2 MB);
+* the u_ref seeds are scattered: rank r gets the contiguous block [r*P/N, (r+1)*P/N);
+* each rank runs the full homotopy for its first point and warm-starts every further point of
+  its block from the previous solution (the reference's sweeping warm start), with the final
+  homotopy step's costs and bounds;
+* the optimal V and the per-point outputs are gathered to rank 0.
+
+There is no data-path collective: evaluation and solves never leave the rank's GPU.
+
+Launch: ``python -m torch.distributed.run --nproc-per-node N -m awebox_amd.sweep --points 64``
+(or plain ``python -m awebox_amd.sweep`` for one GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import homotopy as hm
+from . import problem as pb
+from .initial_guess import initial_guess
+from .ipm import IpmOptions, solve
+from .trajectory import hippo_options, optimize
+
+N_OUT = 6   # u_ref, avg power, period, iterations, status ok, seconds
+
+
+def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda", opts: IpmOptions | None = None,
+              verbose=False, point_solver=None):
+    """Returns (on rank 0) dict with per-point outputs, V_opt [P, n_v] and timing; None elsewhere.
+
+    ``point_solver(u, prev) -> (V, outputs, iterations, ok, prev)`` replaces the per-point solve
+    (the default is the homotopy for a shard's first point and the warm-started final step after)."""
+    rank = dist.get_rank() if dist is not None else 0
+    world = dist.get_world_size() if dist is not None else 1
+    coll_dev = torch.device(device)
+    cfg = pb.Ap2Config(n_k=n_k, d=d)
+    consts = pb.build_constants(cfg)
+    lay = pb.NlpLayout(n_k, d)
+    n_pts = len(u_refs)
+    per = -(-n_pts // world)
+
+    # ---- template broadcast: model constants + initial guess (rank 0 -> all) ----------------
+    tmpl = torch.zeros(pb.NCONST + lay.n_v, dtype=torch.float64, device=coll_dev)
+    if rank == 0:
+        tmpl[:pb.NCONST] = torch.tensor(consts.consts)
+        tmpl[pb.NCONST:] = torch.tensor(initial_guess(consts, lay))
+    if dist is not None:
+        dist.broadcast(tmpl, src=0)
+    consts.consts = tmpl[:pb.NCONST].cpu().numpy().copy()
+    v0 = tmpl[pb.NCONST:].cpu().numpy().copy()
+
+    # ---- seed scatter ---------------------------------------------------------------------------
+    seeds = torch.full((per,), float("nan"), dtype=torch.float64, device=coll_dev)
+    if dist is not None:
+        chunks = None
+        if rank == 0:
+            padded = np.full(per * world, np.nan)
+            padded[:n_pts] = u_refs
+            chunks = [torch.tensor(padded[r * per:(r + 1) * per], device=coll_dev) for r in range(world)]
+        dist.scatter(seeds, chunks, src=0)
+    else:
+        seeds[:n_pts] = torch.tensor(np.asarray(u_refs, dtype=np.float64))
+    my_u = [u for u in seeds.cpu().numpy() if np.isfinite(u)]
+
+    # ---- local solves ---------------------------------------------------------------------------
+    if point_solver is None:
+        ev = make_evaluator(consts)
+        final = hm.schedule(consts, lay, v0)[-1]
+        lbg, ubg = lay.g_bounds()
+        done = ("solve_succeeded", "solved_to_acceptable_level")
+
+        def point_solver(u, prev):
+            if prev is None:
+                V, summary, out, res = optimize(consts, ev, opts, device=device, v_init=v0, u_ref=u)
+                return V, out, sum(r["iterations"] for r in summary), all(r["status"] in done for r in summary), res
+            P = pb.pack_p(lay, consts, v0, step=final.cost_step, u_ref=u)
+            res = solve(ev, P, prev.x, final.lbx, final.ubx, lbg, ubg, lam0=prev.lam_g, zl0=prev.zl, zu0=prev.zu,
+                        opts=hippo_options("final", opts), device=device)
+            return res.x, hm.outputs(consts, lay, res.x), res.iterations, res.status in done, res
+
+    res_v = torch.zeros(per, lay.n_v, dtype=torch.float64, device=coll_dev)
+    res_o = torch.full((per, N_OUT), float("nan"), dtype=torch.float64, device=coll_dev)
+    prev = None
+    t_rank = time.perf_counter()
+    for i, u in enumerate(my_u):
+        t0 = time.perf_counter()
+        V, out, iters, ok, prev = point_solver(u, prev)
+        res_v[i] = torch.tensor(V, device=coll_dev)
+        res_o[i] = torch.tensor([u, out["avg_power_W"], out["period_s"], iters, float(ok),
+                                 time.perf_counter() - t0], device=coll_dev)
+        if verbose:
+            print(f"[rank {rank}] u_ref={u:.3f} P={out['avg_power_W']:.1f} W T={out['period_s']:.2f} s "
+                  f"iters={iters} ok={ok} {time.perf_counter() - t0:.1f} s", flush=True)
+    t_rank = time.perf_counter() - t_rank
+
+    # ---- gather to rank 0 -----------------------------------------------------------------------
+    if dist is not None:
+        gv = [torch.zeros_like(res_v) for _ in range(world)] if rank == 0 else None
+        go = [torch.zeros_like(res_o) for _ in range(world)] if rank == 0 else None
+        dist.gather(res_v, gv, dst=0)
+        dist.gather(res_o, go, dst=0)
+        t = torch.tensor([t_rank], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_rank = float(t.item())
+        if rank != 0:
+            return None
+        V_all = torch.cat(gv).cpu().numpy()
+        O_all = torch.cat(go).cpu().numpy()
+    else:
+        V_all, O_all = res_v.cpu().numpy(), res_o.cpu().numpy()
+    keep = np.isfinite(O_all[:, 0])
+    O_all, V_all = O_all[keep], V_all[keep]
+    return {"u_ref": O_all[:, 0].tolist(), "avg_power_W": O_all[:, 1].tolist(), "period_s": O_all[:, 2].tolist(),
+            "iterations": O_all[:, 3].astype(int).tolist(), "ok": O_all[:, 4].astype(bool).tolist(),
+            "seconds": O_all[:, 5].tolist(), "V_opt": V_all, "wall_s": t_rank, "world": world,
+            "trials_per_s": len(O_all) / t_rank}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=64)
+    ap.add_argument("--u-min", type=float, default=5.0)
+    ap.add_argument("--u-max", type=float, default=8.0)
+    ap.add_argument("--n-k", type=int, default=40)
+    ap.add_argument("--d", type=int, default=4)
+    ap.add_argument("--max-iter", type=int, default=600)
+    ap.add_argument("--out", default="gpurun_out/sweep.json")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    from .build import build
+    from .evaluator import Ap2Evaluator
+    if local_rank == 0:
+        build()
+    if dist is not None:
+        dist.barrier()
+    u = np.linspace(args.u_min, args.u_max, args.points)
+    res = run_sweep(u, n_k=args.n_k, d=args.d, make_evaluator=lambda c: Ap2Evaluator(c, batch=1), dist=dist,
+                    device=f"cuda:{local_rank}", opts=IpmOptions(max_iter=args.max_iter), verbose=args.verbose)
+    if res is not None:
+        res = dict(res)
+        res.pop("V_opt")
+        res.update(n_k=args.n_k, d=args.d, metric="sweep trials/sec, AP2 power curve", gpus=world)
+        os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+        with open(args.out, "w") as fh:
+            json.dump(res, fh, indent=1)
+        print(json.dumps({k: res[k] for k in ("gpus", "trials_per_s", "wall_s")}))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -31,8 +31,10 @@ def hippo_options(label: str, base: IpmOptions | None = None) -> IpmOptions:
 
 
 def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device="cuda",
-             v_init: np.ndarray | None = None, final_step: str | None = None, verbose=False):
-    """Run the homotopy; returns (V_opt, list of per-step summaries, outputs)."""
+             v_init: np.ndarray | None = None, final_step: str | None = None, verbose=False,
+             u_ref: float | None = None):
+    """Run the homotopy; returns (V_opt, per-step summaries, outputs, last IpmResult).
+    ``u_ref`` overrides the wind reference speed in P (the sweep parameter)."""
     lay = pb.NlpLayout(consts.cfg.n_k, consts.cfg.d)
     v0 = initial_guess(consts, lay) if v_init is None else v_init
     steps = hm.schedule(consts, lay, v0)
@@ -40,7 +42,7 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
     x, lam, zl, zu = v0.copy(), None, None, None
     summary = []
     for st in steps:
-        P = pb.pack_p(lay, consts, v0, step=st.cost_step)
+        P = pb.pack_p(lay, consts, v0, step=st.cost_step, u_ref=u_ref)
         t0 = time.perf_counter()
         res = solve(ev, P, x, st.lbx, st.ubx, lbg, ubg, lam0=lam, zl0=zl, zu0=zu,
                     opts=hippo_options(st.label, opts), device=device)
@@ -54,4 +56,4 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
         x, lam, zl, zu = res.x, res.lam_g, res.zl, res.zu
         if final_step is not None and st.label == final_step:
             break
-    return x, summary, hm.outputs(consts, lay, x)
+    return x, summary, hm.outputs(consts, lay, x), res

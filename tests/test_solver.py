@@ -32,7 +32,7 @@ def test_homotopy_on_cpu_port():
     consts = pb.build_constants(pb.Ap2Config(n_k=5, d=3))
     lay = pb.NlpLayout(5, 3)
     ev = CpuDeviceEvaluator(consts)
-    V, summary, out = optimize(consts, ev, IpmOptions(max_iter=400), device="cpu")
+    V, summary, out, _ = optimize(consts, ev, IpmOptions(max_iter=400), device="cpu")
     _check_solution(consts, lay, V, summary)
 
 
@@ -63,5 +63,64 @@ def test_homotopy_on_gpu_n10():
     build()
     consts = pb.build_constants(pb.Ap2Config(n_k=10, d=4))
     lay = pb.NlpLayout(10, 4)
-    V, summary, out = optimize(consts, Ap2Evaluator(consts, batch=1), IpmOptions(max_iter=600))
+    V, summary, out, _ = optimize(consts, Ap2Evaluator(consts, batch=1), IpmOptions(max_iter=600))
     _check_solution(consts, lay, V, summary)
+
+
+def _fake_point_solver(n_v):
+    """Deterministic stand-in for a solve: V encodes u_ref and the number of warm starts."""
+    def solve_point(u, prev):
+        chain = 0 if prev is None else prev + 1
+        V = np.full(n_v, u) + chain
+        return V, {"avg_power_W": 1000.0 * u, "period_s": 30.0 + u}, 10 + chain, True, chain
+    return solve_point
+
+
+def _sweep_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from awebox_amd.sweep import run_sweep
+    n_v = pb.NlpLayout(4, 2).n_v
+    res = run_sweep([5.0, 5.5, 6.0, 6.5, 7.0], n_k=4, d=2, dist=dist, device="cpu",
+                    point_solver=_fake_point_solver(n_v))
+    if rank == 0:
+        q.put({k: (v.tolist() if hasattr(v, "tolist") else v) for k, v in res.items()})
+    dist.destroy_process_group()
+
+
+def test_sweep_collectives_over_two_ranks():
+    """world_size 2 over gloo: template broadcast, seeds scattered in contiguous blocks (3 + 2
+    points, padded), solutions gathered to rank 0 in point order, warm-start chains per shard."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sweep_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+    assert res["world"] == 2
+    assert res["u_ref"] == [5.0, 5.5, 6.0, 6.5, 7.0]
+    assert res["iterations"] == [10, 11, 12, 10, 11]          # rank 0: 3 chained points, rank 1: 2
+    V = np.asarray(res["V_opt"])
+    assert np.array_equal(V[:, 0], np.array([5.0, 6.5, 8.0, 6.5, 8.0]))
+    assert res["avg_power_W"] == [1000.0 * u for u in res["u_ref"]]
+
+
+def test_sweep_single_process_warm_start_chain():
+    from awebox_amd.sweep import run_sweep
+    from oracle.cpu_device import CpuDeviceEvaluator
+    res = run_sweep([7.0, 7.5], n_k=5, d=3, make_evaluator=CpuDeviceEvaluator, device="cpu",
+                    opts=IpmOptions(max_iter=500))
+    assert all(res["ok"]), res
+    assert res["iterations"][1] < res["iterations"][0]        # the warm start is cheaper than the homotopy
+    assert res["avg_power_W"][1] > 0

@@ -29,7 +29,7 @@ def main():
     consts = pb.build_constants(pb.Ap2Config(n_k=args.n_k, d=args.d, u_ref=args.u_ref))
     ev = Ap2Evaluator(consts, batch=1)
     t0 = time.perf_counter()
-    V, summary, out = optimize(consts, ev, IpmOptions(max_iter=args.max_iter, verbose=args.verbose),
+    V, summary, out, _ = optimize(consts, ev, IpmOptions(max_iter=args.max_iter, verbose=args.verbose),
                                verbose=True)
     rec = {"n_k": args.n_k, "d": args.d, "u_ref": args.u_ref, "seconds": time.perf_counter() - t0,
            "steps": summary, "outputs": out, "device": torch.cuda.get_device_name(0)}
