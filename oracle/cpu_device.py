@@ -14,6 +14,8 @@ class CpuDeviceEvaluator:
         self.port.hess_init()
         self.n_v, self.n_g, self.n_p, self.nnz = self.port.n_v, self.port.n_g, self.port.n_p, self.port.nnz
         self.nnz_h = self.port.hnnz
+        from awebox_amd import problem as pb
+        self.layout = pb.NlpLayout(consts.cfg.n_k, consts.cfg.d)
 
     def sparsity_jac(self):
         return self.port.colind.copy(), self.port.row.copy()

@@ -29,11 +29,50 @@ def _check_solution(consts, lay, V, summary):
 
 def test_homotopy_on_cpu_port():
     from oracle.cpu_device import CpuDeviceEvaluator
-    consts = pb.build_constants(pb.Ap2Config(n_k=5, d=3))
-    lay = pb.NlpLayout(5, 3)
+    consts = pb.build_constants(pb.Ap2Config(n_k=6, d=3))
+    lay = pb.NlpLayout(6, 3)
     ev = CpuDeviceEvaluator(consts)
     V, summary, out, _ = optimize(consts, ev, IpmOptions(max_iter=400), device="cpu")
     _check_solution(consts, lay, V, summary)
+
+
+@pytest.mark.parametrize("delta_c", [0.0, 1e-6])
+def test_structured_kkt_matches_dense(delta_c):
+    """Interval elimination + Schur complement solves the same KKT system as a dense LU."""
+    import torch
+    from oracle.cpu_device import CpuDeviceEvaluator
+    from awebox_amd.ipm import DeviceNlp, StructuredKKT, _dense_A
+    n_k, d = 5, 3
+    consts = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+    lay = pb.NlpLayout(n_k, d)
+    v0 = initial_guess(consts, lay)
+    st = hm.schedule(consts, lay, v0)[0]
+    lbg, ubg = lay.g_bounds()
+    nlp = DeviceNlp(CpuDeviceEvaluator(consts), pb.pack_p(lay, consts, v0, step=st.cost_step), st.lbx, st.ubx,
+                    lbg, ubg, "cpu")
+    sk = StructuredKKT(nlp, lay, "cpu")
+    assert sk.nS < sk.N // 4
+    gen = torch.Generator().manual_seed(1)
+    f64 = dict(dtype=torch.float64)
+    hv = torch.randn(len(nlp.h_keep), generator=gen, **f64)
+    jv = torch.randn(len(nlp.j_row), generator=gen, **f64)
+    diag = torch.rand(nlp.ny, generator=gen, **f64) + 1.0
+    N, ny = sk.N, nlp.ny
+    K = torch.zeros(N, N, **f64)
+    K[nlp.h_r, nlp.h_c] = hv
+    K[nlp.h_c[nlp.h_offdiag], nlp.h_r[nlp.h_offdiag]] = hv[nlp.h_offdiag]
+    i = torch.arange(ny)
+    K[i, i] += diag
+    _dense_A(nlp, jv, ny, K)
+    if delta_c:
+        K[torch.arange(ny, N), torch.arange(ny, N)] = -delta_c
+    rhs = torch.randn(N, generator=gen, **f64)
+    sk.factor(hv, diag, jv, delta_c, nlp.mI)
+    x = sk.solve(rhs)
+    assert sk.n_dense == 0
+    assert (K @ x - rhs).abs().max().item() <= 1e-9 * rhs.abs().max().item()
+    x_ref = torch.linalg.solve(K, rhs)
+    assert (x - x_ref).abs().max().item() <= 1e-7 * x_ref.abs().max().item()
 
 
 def test_ipm_handles_fixed_variables_and_inequalities():
@@ -119,7 +158,7 @@ def test_sweep_collectives_over_two_ranks():
 def test_sweep_single_process_warm_start_chain():
     from awebox_amd.sweep import run_sweep
     from oracle.cpu_device import CpuDeviceEvaluator
-    res = run_sweep([7.0, 7.5], n_k=5, d=3, make_evaluator=CpuDeviceEvaluator, device="cpu",
+    res = run_sweep([10.0, 10.5], n_k=6, d=3, make_evaluator=CpuDeviceEvaluator, device="cpu",
                     opts=IpmOptions(max_iter=500))
     assert all(res["ok"]), res
     assert res["iterations"][1] < res["iterations"][0]        # the warm start is cheaper than the homotopy
