@@ -492,11 +492,52 @@ void finalize(const Ap2Tables& T, const double* V, const double* P, const double
     for (int i = 0; i < AWE_NX; ++i) grad[L.v_int0 + T.n_k * L.stride + i] = 0.0;
 }
 
+// one node of the shared model with a dense Jacobian: direction c of the pass seeds input base + c
+struct NodeIn {
+    const double* w;
+    int base;
+    DN operator()(int i) const {
+        DN r(w[i]);
+        if (i >= base && i < base + kHalf) r.d[i - base] = 1.0;
+        return r;
+    }
+};
+
+struct NodeSinkDense {
+    double* rows;   // [kGvalStride]
+    double* jac;    // [kGvalStride][AWE_NW], row-major
+    int base;
+    void emit(int r, const DN& v) {
+        rows[r] = v.v;
+        for (int c = 0; c < kHalf && base + c < AWE_NW; ++c) jac[r * AWE_NW + base + c] = v.d[c];
+    }
+    void eq_row(int r, const DN& v) { emit(r, v); }
+    void ineq_row(int r, const DN& v) { emit(AWE_N_EQ + r, v); }
+    void power(const DN& v) { emit(kRowPower, v); }
+    void beta(const DN& v) { emit(kRowBeta, v); }
+};
+
 }  // namespace
 
 extern "C" {
 
 const char* ap2cpu_last_error(void) { return g_err.c_str(); }
+
+// Model rows of one node (24 eq, 9 ineq, power, beta; kGvalStride doubles) and their Jacobian
+// w.r.t. the 59 scaled node variables, for model-level known-answer tests (integration of the
+// DAE).  theta0 in the flat AWE_TH_* layout; the phi-gamma embedding factor is `gamma`.
+int ap2cpu_node(void* hv, const double* w_sc, const double* theta0, double gamma, double* rows,
+                double* jac) {
+    const Ap2Tables& T = static_cast<Handle*>(hv)->t;
+    const double* cst = T.cst.data();
+    std::memset(jac, 0, sizeof(double) * kGvalStride * AWE_NW);
+    for (int base = 0; base < AWE_NW; base += kHalf) {
+        NodeIn in{w_sc, base};
+        NodeSinkDense sink{rows, jac, base};
+        awe::ap2_node<DN>(in, DN(gamma), theta0, cst, sink, true);
+    }
+    return AWE_OK;
+}
 
 int ap2cpu_create(int n_k, int d, const double* consts, int n_consts, void** out) {
     if (!out || !consts) { g_err = "null argument"; return AWE_ERR_ARG; }

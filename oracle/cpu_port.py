@@ -34,6 +34,7 @@ def load():
         lib.ap2cpu_hess_init.argtypes = [vp, ip]
         lib.ap2cpu_hess_sparsity.argtypes = [vp, ip, ip]
         lib.ap2cpu_eval_hess.argtypes = [vp, ctypes.c_int, dp, dp, dp, dp, dp, ctypes.c_int]
+        lib.ap2cpu_node.argtypes = [vp, dp, dp, ctypes.c_double, dp, dp]
         lib.ap2cpu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
@@ -70,6 +71,16 @@ class CpuPort:
         jac = np.zeros((B, self.nnz))
         self.lib.ap2cpu_eval_nlp(self.h, B, _dp(V), _dp(P), _dp(f), _dp(g), _dp(grad), _dp(jac), int(threads))
         return {"f": f, "g": g, "grad_f": grad, "jac": jac}
+
+    def node(self, w_sc, theta0, gamma=1.0):
+        """Rows [36] (24 eq, 9 ineq, power, beta, pad) of the shared node model at the scaled node
+        vector w_sc [59] and their Jacobian [36, 59]."""
+        w = np.ascontiguousarray(w_sc, dtype=np.float64)
+        th = np.ascontiguousarray(theta0, dtype=np.float64)
+        rows = np.zeros(36)
+        jac = np.zeros((36, w.size))
+        self.lib.ap2cpu_node(self.h, _dp(w), _dp(th), float(gamma), _dp(rows), _dp(jac))
+        return rows, jac
 
     def hess_init(self):
         if getattr(self, "hnnz", None) is None:
