@@ -62,6 +62,7 @@ class IpmOptions:
     alpha_min_frac: float = 0.05
     max_backtracks: int = 40
     kkt: str = "structured"          # "structured" (interval elimination + Schur) or "dense"
+    profile: bool = False            # synchronise and time the solver's phases (IpmResult.timing)
     verbose: bool = False
 
 
@@ -80,6 +81,7 @@ class IpmResult:
     log: list = field(default_factory=list)
     kkt_solves: int = 0      # linear solves, and how many fell back to a dense LU (structured KKT)
     kkt_dense: int = 0
+    timing: dict = field(default_factory=dict)   # seconds per phase when IpmOptions.profile
 
 
 class DeviceNlp:
@@ -170,6 +172,25 @@ class DeviceNlp:
         return c
 
 
+class _Csr:
+    """Fixed COO pattern as a CSR operator: y = A(vals) x through a sparse matrix-vector product
+    (no atomics; fp64 scatter-adds with many duplicates are slow on the GPU)."""
+
+    def __init__(self, rows, cols, shape, dev):
+        rows = np.asarray(rows, dtype=np.int64)
+        cols = np.asarray(cols, dtype=np.int64)
+        order = np.lexsort((cols, rows))
+        self.perm = torch.tensor(order, device=dev)
+        self.col = torch.tensor(cols[order], device=dev)
+        self.crow = torch.tensor(np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=shape[0]))]),
+                                 dtype=torch.int64, device=dev)
+        self.shape = shape
+
+    def mv(self, vals, x):
+        A = torch.sparse_csr_tensor(self.crow, self.col, vals[self.perm], size=self.shape)
+        return (A @ x.unsqueeze(1)).squeeze(1)
+
+
 def _dense_A(nlp, jv, N0, K):
     """Write A = [J | -I_slack] into rows N0.. and its transpose (in place)."""
     n, mI = nlp.n, nlp.mI
@@ -234,6 +255,7 @@ class StructuredKKT:
         Q_ = np.concatenate([hc, hr[off], np.arange(ny), jc, ny + jr, sc, ny + sr, ny + np.arange(m)])
         self.off_mask = torch.tensor(off, device=dev)
         self.P_, self.Q_ = torch.tensor(P_, device=dev), torch.tensor(Q_, device=dev)
+        self.csr = _Csr(P_, Q_, (N, N), dev)
         self.n_solve = self.n_dense = 0
         oP, oQ = owner[P_], owner[Q_]
         ii = (oP >= 0) & (oP == oQ)
@@ -273,6 +295,7 @@ class StructuredKKT:
         vals = torch.cat([hv, hv[self.off_mask], diag, jv, jv, -torch.ones(2 * mI, **f64),
                           torch.full((m,), -float(delta_c), **f64)])
         self.vals = vals
+        self.k_norm = float(self.csr.mv(vals.abs(), torch.ones(self.N, **f64)).max().item())
         nI, L, nS, n_k = self.nI, self.L, self.nS, self.n_k
         KII = torch.zeros(n_k * nI * nI, **f64)
         KII.index_put_((self.dst_ii,), vals[self.sel_ii], accumulate=True)
@@ -295,23 +318,24 @@ class StructuredKKT:
         self.LU_S, self.piv_S = torch.linalg.lu_factor(S)
 
     def matvec(self, x):
-        return torch.zeros_like(x).index_add_(0, self.P_, self.vals * x[self.Q_])
+        return self.csr.mv(self.vals, x)
 
-    def solve(self, rhs, refine=3, rtol=1e-10):
-        """Elimination solve with iterative refinement on the sparse residual: the interior
+    def solve(self, rhs, refine=3, rtol=1e-12):
+        """Elimination solve with iterative refinement on the sparse residual.  The interior
         pivots come from blocks that may be ill-conditioned even when K is not (an indefinite
-        interior Hessian), so the result is only accepted once ||K x - rhs|| is at round-off
-        level; otherwise the system is solved once by a dense LU of the assembled K."""
+        interior Hessian), so the result is accepted once its backward error is small,
+        ||K x - rhs|| <= rtol (||K|| ||x|| + ||rhs||) in the max norm; otherwise the system is
+        solved once by a dense LU of the assembled K."""
         self.n_solve += 1
         x = self._solve(rhs)
-        scale = rtol * max(1.0, float(rhs.abs().max().item()))
+        b_norm = float(rhs.abs().max().item())
         for _ in range(refine + 1):
             r = rhs - self.matvec(x)
             err = float(r.abs().max().item())
-            if err <= scale:
-                return x
             if not math.isfinite(err):
                 break
+            if err <= rtol * (self.k_norm * float(x.abs().max().item()) + b_norm):
+                return x
             x = x + self._solve(r)
         # ill-conditioned interior pivots: one dense LU of the assembled K for this system
         self.n_dense += 1
@@ -421,6 +445,24 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
         except ValueError:
             skkt = None
     K = torch.zeros(N, N, **f64) if skkt is None else None
+    timing = {}
+
+    class _Phase:
+        def __init__(self, key):
+            self.key = key
+
+        def __enter__(self):
+            if opts.profile:
+                if torch.cuda.is_available() and str(dev).startswith("cuda"):
+                    torch.cuda.synchronize()
+                self.t = time.perf_counter()
+
+        def __exit__(self, *exc):
+            if opts.profile:
+                if torch.cuda.is_available() and str(dev).startswith("cuda"):
+                    torch.cuda.synchronize()
+                timing[self.key] = timing.get(self.key, 0.0) + time.perf_counter() - self.t
+            return False
     status = "max_iter"
     it = 0
     kkt_err = math.inf
@@ -437,9 +479,13 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
     def grad_y(gradv):
         return torch.cat([gradv, torch.zeros(mI, **f64)])
 
+    jt_op = _Csr(nlp.j_col.cpu().numpy(), nlp.j_row.cpu().numpy(), (ny, m), dev)
+    hr_np, hc_np = nlp.h_r.cpu().numpy(), nlp.h_c.cpu().numpy()
+    off_np = hr_np != hc_np
+    h_op = _Csr(np.concatenate([hr_np, hc_np[off_np]]), np.concatenate([hc_np, hr_np[off_np]]), (ny, ny), dev)
+
     def A_T_lam(jvv, lamv):
-        r = torch.zeros(ny, **f64)
-        r.index_add_(0, nlp.j_col, jvv * lamv[nlp.j_row])
+        r = jt_op.mv(jvv, lamv)
         r[n:] -= lamv[nlp.ineq_t]
         return r
 
@@ -535,7 +581,8 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
             tau = max(opts.tau_min, 1.0 - mu)
             filt = []
         # ---- Newton system --------------------------------------------------------------------
-        hv = nlp.hess(y[:n], lam)
+        with _Phase("hessian"):
+            hv = nlp.hess(y[:n], lam)
         dl, du = gaps(y)
         sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
         grad_phi = grad_y(grad) - torch.where(hl, mu / dl, torch.zeros_like(y)) + torch.where(hu, mu / du, torch.zeros_like(y))
@@ -550,20 +597,19 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
             delta_c = 0.0
             for attempt in range(60):
                 try:
-                    if skkt is not None:
-                        skkt.factor(hv, sigma + delta_w, jv, delta_c, mI)
-                        sol = skkt.solve(rhs)
-                    else:
-                        assemble(K, hv, sigma, delta_w, delta_c)
-                        sol = torch.linalg.solve(K, rhs)
+                    with _Phase("kkt_factor"):
+                        if skkt is not None:
+                            skkt.factor(hv, sigma + delta_w, jv, delta_c, mI)
+                        else:
+                            assemble(K, hv, sigma, delta_w, delta_c)
+                    with _Phase("kkt_solve"):
+                        sol = skkt.solve(rhs) if skkt is not None else torch.linalg.solve(K, rhs)
                     ok = bool(torch.isfinite(sol).all().item())
                 except RuntimeError:
                     ok = False
                 if ok:
                     dy = sol[:ny]
-                    Wd = torch.zeros(ny, **f64)
-                    Wd.index_add_(0, nlp.h_r, hv * dy[nlp.h_c])
-                    Wd.index_add_(0, nlp.h_c[nlp.h_offdiag], hv[nlp.h_offdiag] * dy[nlp.h_r[nlp.h_offdiag]])
+                    Wd = h_op.mv(torch.cat([hv, hv[nlp.h_offdiag]]), dy)
                     curv = float((dy * (Wd + (sigma + delta_w) * dy)).sum().item())
                     if curv >= opts.curvature_kappa * float((dy * dy).sum().item()):
                         if delta_w > 0:
@@ -588,7 +634,8 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
                                                    if gphi_d < 0 else opts.gamma_theta)
             for _ in range(opts.max_backtracks):
                 yt = y + alpha * dy
-                ft, gt = nlp.eval_fg(yt[:n])
+                with _Phase("eval_fg"):
+                    ft, gt = nlp.eval_fg(yt[:n])
                 ct = nlp.constraints(gt, yt[n:])
                 theta_t = float(ct.abs().sum().item())
                 phi_t = float(barrier_phi(ft, yt).item())
@@ -649,7 +696,8 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
         dl, du = gaps(y)
         zl = torch.where(hl, torch.clamp(zl, min=mu / (opts.kappa_sigma * dl), max=opts.kappa_sigma * mu / dl), zl)
         zu = torch.where(hu, torch.clamp(zu, min=mu / (opts.kappa_sigma * du), max=opts.kappa_sigma * mu / du), zu)
-        f, grad, g, jv = nlp.eval_all(y[:n])
+        with _Phase("eval_all"):
+            f, grad, g, jv = nlp.eval_all(y[:n])
         it += 1
         rec = dict(it=it, f=float(f.item()) / nlp.obj_scale, inf_pr=e_p, inf_du=e_d, mu=mu, alpha=alpha,
                    alpha_z=alpha_z, delta_w=delta_w)
@@ -671,4 +719,4 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
                      kkt_error=kkt_err, constr_viol=float((c / nlp.c_scale).abs().max().item()) if m else 0.0,
                      seconds=time.perf_counter() - t_start, zl=zl_v, zu=zu_v, log=log,
                      kkt_solves=skkt.n_solve if skkt is not None else 0,
-                     kkt_dense=skkt.n_dense if skkt is not None else 0)
+                     kkt_dense=skkt.n_dense if skkt is not None else 0, timing=timing)
