@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import math
 import time
+import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -187,7 +188,9 @@ class _Csr:
         self.shape = shape
 
     def mv(self, vals, x):
-        A = torch.sparse_csr_tensor(self.crow, self.col, vals[self.perm], size=self.shape)
+        with warnings.catch_warnings():
+            warnings.filterwarnings("ignore", message="Sparse CSR tensor support is in beta state")
+            A = torch.sparse_csr_tensor(self.crow, self.col, vals[self.perm], size=self.shape)
         return (A @ x.unsqueeze(1)).squeeze(1)
 
 

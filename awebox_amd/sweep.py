@@ -97,7 +97,12 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     t_rank = time.perf_counter()
     for i, u in enumerate(my_u):
         t0 = time.perf_counter()
-        V, out, iters, ok, prev = point_solver(u, prev)
+        try:
+            V, out, iters, ok, prev = point_solver(u, prev)
+        except (RuntimeError, ValueError, FloatingPointError) as exc:
+            # a failed point must not leave the other ranks waiting in the gather below
+            print(f"[rank {rank}] u_ref={u:.3f} failed: {exc}", flush=True)
+            V, out, iters, ok, prev = v0, {"avg_power_W": float("nan"), "period_s": float("nan")}, 0, False, None
         res_v[i] = torch.tensor(V, device=coll_dev)
         res_o[i] = torch.tensor([u, out["avg_power_W"], out["period_s"], iters, float(ok),
                                  time.perf_counter() - t0], device=coll_dev)

@@ -16,6 +16,8 @@ Also reported:
                   profiles/pmc_traffic.json, used only when that record was taken for the same
                   kernel sources and batch size (else null); the same record carries the FP64
                   VALU instruction counts behind `fp64`.
+  sweep        -- the metric's second half: wind-speed sweep trials/s, --sweep-points per GPU
+                  (first point: full homotopy; then warm starts), collectives over RCCL.
   cpu_baseline -- the CPU port of the evaluator (oracle/cpu, C++ with OpenMP over (instance,
                   interval), "port"; the reference CasADi/IPOPT stack cannot be installed) on a
                   bounded sample, rank 0, N=1 only, at all host threads and at one thread.
@@ -71,6 +73,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per thread setting")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hessian", action="store_true", help="skip the nlp_hess_l timing block")
+    ap.add_argument("--sweep-points", type=int, default=2,
+                    help="u_ref sweep points solved per GPU for the sweep block (0: skip)")
     args = ap.parse_args()
 
     import numpy as np
@@ -146,6 +150,9 @@ def main():
     torch.cuda.synchronize()
     finite = bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item())
 
+    sweep = None
+    if args.sweep_points > 0:
+        sweep = sweep_block(args.sweep_points, world, dist, dev, consts)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -191,6 +198,8 @@ def main():
                         "flops_per_launch": flops, "note": "FP64 VALU instructions x 64 lanes (FMA = 2), "
                         "from the PMC record; idle lanes of issued instructions count"}
         line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
+    if sweep is not None:
+        line["sweep"] = sweep
     if not args.no_hessian:
         line["hessian"] = hessian_block(ev, V, P, B, lay, dev)
     if world == 1 and not args.no_cpu_baseline:
@@ -198,6 +207,36 @@ def main():
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def sweep_block(per_gpu, world, dist, dev, consts):
+    """Second half of the headline metric: wind-speed sweep trials/s (config 4's recipe,
+    u_ref = linspace(5, 8), contiguous blocks per GPU, template broadcast / seed scatter / solution
+    gather over RCCL).  Weak scaling: `per_gpu` points per rank; each rank solves its first point
+    with the full homotopy and warm-starts the rest.  The whole sweep is timed between barriers,
+    max over ranks (run_sweep's own clock, all-reduced)."""
+    import numpy as np
+    import torch
+
+    from awebox_amd.evaluator import Ap2Evaluator
+    from awebox_amd.ipm import IpmOptions
+    from awebox_amd.sweep import run_sweep
+
+    n_pts = per_gpu * world
+    u = np.linspace(5.0, 8.0, n_pts)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    res = run_sweep(u, n_k=consts.cfg.n_k, d=consts.cfg.d, make_evaluator=lambda c: Ap2Evaluator(c, batch=1),
+                    dist=dist, device=str(dev), opts=IpmOptions(max_iter=600))
+    if res is None:
+        return None
+    return {"metric": "sweep trials/sec, AP2 N=40 d=4 power curve", "value": res["trials_per_s"],
+            "unit": "trials/s", "points": n_pts, "points_per_gpu": per_gpu, "wall_s": res["wall_s"],
+            "all_converged": bool(all(res["ok"])), "iterations": res["iterations"],
+            "avg_power_W": [round(p, 1) for p in res["avg_power_W"]],
+            "period_s": [round(t, 2) for t in res["period_s"]], "scaling": "weak",
+            "solver": "GPU interior point (awebox_amd/ipm.py), structured KKT, exact Hessian"}
 
 
 def hessian_block(ev, V, P, B, lay, dev, steps=10):
