@@ -21,7 +21,8 @@ for s in $STAGES; do
     test)  run 900 pytest_gpu.log python -m pytest tests -m gpu -x -q ;;
     smoke) run 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run 600 bench.log python bench.py --steps ${BENCH_STEPS:-30} --warmup 5 ${BENCH_ARGS} ;;
-    prof)  run 600 rocprof.log rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS} ;;
+    prof)  run 600 rocprof.log rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS} && \
+           find $OUT/prof -name '*_trace.csv' -size +4M -delete ;;
     pmc)   run 600 rocprof_pmc.log rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} && \
            run 600 rocprof_pmc2.log rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} ;;
     sq)    i=0; IFS=';' read -ra GROUPS_ARR <<< "${PMC_GROUPS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY}"
