@@ -1,0 +1,422 @@
+// awempc -- MI355X (gfx950) evaluator for the awebox tracking-MPC NLP of a 3-DOF kite
+// (pmpc.py:193-217; SURVEY.md section 8 row a37, config 5: B MPC instances per launch).
+//
+// Execution model (same shape as the AP2 evaluator, awegpu.hip, specialised for the small node):
+//   * one workgroup per (MPC instance, horizon interval), W = ceil((d+1)/2) wavefronts; the
+//     interval's slice of V and the parameters it reads are staged in LDS with coalesced loads;
+//   * model pass: every half-wavefront evaluates ONE node of kite3_node in forward-mode dual
+//     arithmetic with one seed direction per lane -- 31 node variables + phi.gamma = 32 lanes, so
+//     a wavefront produces two complete node Jacobian blocks and no colouring is needed.  The
+//     collocation chain rule xdot = C X / (h tf) is folded into the seeds (kite3_tables.hpp);
+//   * tracking objective (pmpc.py:304-358) and its gradient are closed-form per V column;
+//   * J_g values come from a host-built gather list (one entry per CCS slot: tangent index and
+//     polynomial scale, or a constant for the initial-condition and continuity rows), so the J
+//     stores of one interval are contiguous; a one-wave finalize kernel per instance reduces the
+//     interval objective partials in a fixed order and adds the terminal cost (no float atomics).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/awegpu.h"
+#include "../../include/awempc.h"
+#include "kite3_model.hpp"
+#include "kite3_tables.hpp"
+
+namespace {
+
+using namespace k3t;
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define MPC_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess)                                                          \
+            return fail(AWE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct MArgs {
+    int n_k, d, n_v, n_g, n_p, nnz, stride;
+    const double* V;
+    const double* P;
+    double* f;
+    double* g;
+    double* grad;
+    double* jac;
+    const double* cst;
+    const awt::DevColl* coll;
+    const int* goff;
+    const int* gslot;
+    const uint32_t* gcode;
+    double* fpart;       // [B][n_k]
+};
+
+struct LaneIn {
+    const double* w;     // node values (scaled), [32]
+    int lane;
+    bool radau;
+    double cnn_ihtf;     // C[n][n] / (h tf)
+    double inv_tf;
+    __device__ __forceinline__ awe::Dual operator()(int i) const {
+        double t = (i == lane) ? 1.0 : 0.0;
+        if (radau && i >= K3_NX && i < 2 * K3_NX) {
+            if (lane == i - K3_NX) t = cnn_ihtf;
+            if (lane == kDirTf) t = -w[i] * inv_tf;
+        }
+        return awe::Dual(w[i], t);
+    }
+};
+
+struct LaneSink {
+    double* tang;        // node base: [row][32]
+    double* gval;        // node base: [16]
+    int lane;
+    __device__ __forceinline__ void eq_row(int r, const awe::Dual& v) {
+        tang[r * kLanes + lane] = v.d;
+        if (lane == 0) gval[r] = v.v;
+    }
+    __device__ __forceinline__ void ineq_row(int r, const awe::Dual& v) { eq_row(K3_N_EQ + r, v); }
+};
+
+template <int D>
+constexpr int waves_for() { return (D + 2) / 2; }
+
+template <int D>
+__global__ __launch_bounds__(64 * waves_for<D>()) void mpc_interval_kernel(MArgs a) {
+    constexpr int NN = D + 1;
+    constexpr int NT = 64 * waves_for<D>();
+    constexpr int STRIDE = K3_NX + K3_NU + K3_NX + K3_NZ + D * (K3_NX + K3_NZ);
+    constexpr int NLOC = 9 + STRIDE + K3_NX;
+    __shared__ double vloc[NLOC];                  // theta, phi, x[k], u, xdot, z, coll.., x[k+1]
+    __shared__ double rloc[STRIDE + K3_NX];        // p.ref slice of the same block
+    __shared__ double wts[K3_NX + K3_NZ + K3_NU];  // Q, Z(=1), R
+    __shared__ double wn[NN][kLanes];
+    __shared__ double tang[NN * kRowsPerNode * kLanes];
+    __shared__ double gval[NN][16];
+    __shared__ double fterm[STRIDE];
+
+    const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
+    const int tid = threadIdx.x;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const int base = 9 + 2 + k * STRIDE;            // v_int0 = 11
+    // ---- stage ---------------------------------------------------------------------------
+    for (int i = tid; i < NLOC; i += NT) vloc[i] = i < 9 ? V[i] : V[base + (i - 9)];
+    const double* pref = P + K3_NX;                 // p.ref (V-shaped)
+    for (int i = tid; i < STRIDE + K3_NX; i += NT) rloc[i] = pref[base + i];
+    const double u_ref = P[K3_NX + a.n_v];
+    const double* pQ = P + K3_NX + a.n_v + 1;
+    for (int i = tid; i < K3_NX + K3_NZ + K3_NU; i += NT)
+        wts[i] = i < K3_NX ? pQ[i] : (i == K3_NX ? 1.0 : pQ[K3_NX + (i - K3_NX - 1)]);
+    __syncthreads();
+
+    const double tf = vloc[1];
+    const double inv_h_tf = (double)a.n_k / tf;
+    const double* C = a.coll->C;                    // C[j*(d+1)+r] = l_j'(tau_r)
+    const double* xk = vloc + 9;
+    const double* uk = xk + K3_NX;
+    const double* xdk = uk + K3_NU;
+    const double* zk = xdk + K3_NX;
+    const double* coll = zk + K3_NZ;
+    const double* xk1 = coll + D * (K3_NX + K3_NZ);
+    auto Xv = [&](int r, int i) -> double { return r == 0 ? xk[i] : coll[(r - 1) * (K3_NX + K3_NZ) + i]; };
+
+    // ---- node values -----------------------------------------------------------------------
+    for (int t = tid; t < NN * kLanes; t += NT) {
+        const int n = t / kLanes, i = t % kLanes;
+        double val;
+        if (i < K3_NX) val = Xv(n, i);
+        else if (i < 2 * K3_NX) {
+            if (n == 0) val = xdk[i - K3_NX];
+            else {
+                double s = 0.0;
+                for (int r = 0; r < NN; ++r) s += C[r * NN + n] * Xv(r, i - K3_NX);
+                val = s * inv_h_tf;
+            }
+        } else if (i < 2 * K3_NX + K3_NU) val = uk[i - 2 * K3_NX];
+        else if (i == 2 * K3_NX + K3_NU) val = n == 0 ? zk[0] : coll[(n - 1) * (K3_NX + K3_NZ) + K3_NX];
+        else if (i < K3_NW) val = vloc[i - (2 * K3_NX + K3_NU + K3_NZ)];
+        else val = vloc[2];                         // phi.gamma
+        wn[n][i] = val;
+    }
+    __syncthreads();
+
+    // ---- model pass: half-wave = node, lane = direction --------------------------------------
+    {
+        const int n = tid / kLanes, lane = tid % kLanes;
+        if (n < NN) {
+            LaneIn in{wn[n], lane, n > 0, n > 0 ? C[n * NN + n] * inv_h_tf : 0.0, 1.0 / tf};
+            LaneSink sink{tang + n * kRowsPerNode * kLanes, gval[n], lane};
+            awe::Dual gamma(wn[n][kDirGamma], lane == kDirGamma ? 1.0 : 0.0);
+            awe::kite3_node<awe::Dual>(in, gamma, u_ref, a.cst, sink, n == 0);
+        }
+    }
+    // ---- tracking objective: per local column (pmpc.py:304-358) -----------------------------
+    double* grad = a.grad + (size_t)b * a.n_v + base;
+    const double* w = a.coll->w;
+    const double invN = 1.0 / a.n_k;
+    for (int c = tid; c < STRIDE; c += NT) {
+        double gr = 0.0, ft = 0.0;
+        if (c >= K3_NX && c < K3_NX + K3_NU) {                       // u[k], zero-order hold
+            const int i = c - K3_NX;
+            const double e = vloc[9 + c] - rloc[c], W = wts[K3_NX + K3_NZ + i];
+            double sw = 0.0;
+            for (int j = 0; j < D; ++j) sw += w[j];
+            gr = 2.0 * sw * W * e * invN;
+            ft = sw * W * e * e;
+        } else if (c >= 2 * K3_NX + K3_NU + K3_NZ) {                 // coll_var[k][j] = {x, z}
+            const int q = c - (2 * K3_NX + K3_NU + K3_NZ);
+            const int j = q / (K3_NX + K3_NZ), e_ = q % (K3_NX + K3_NZ);
+            const double e = vloc[9 + c] - rloc[c], W = wts[e_];
+            gr = 2.0 * w[j] * W * e * invN;
+            ft = w[j] * W * e * e;
+        }
+        grad[c] = gr;
+        fterm[c] = ft;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double s = 0.0;
+        for (int c = 0; c < STRIDE; ++c) s += fterm[c];
+        a.fpart[(size_t)b * a.n_k + k] = s * invN;
+    }
+
+    // ---- g ---------------------------------------------------------------------------------------
+    double* g = a.g + (size_t)b * a.n_g;
+    const int row0 = K3_NX + k * (K3_N_EQ + K3_N_INEQ + D * K3_N_EQ + K3_NX);
+    constexpr int ROWS = K3_N_EQ + K3_N_INEQ + D * K3_N_EQ + K3_NX;
+    const double* Dc = a.coll->D;
+    for (int r = tid; r < ROWS; r += NT) {
+        double val;
+        if (r < K3_N_EQ + K3_N_INEQ) val = gval[0][r];
+        else if (r < K3_N_EQ + K3_N_INEQ + D * K3_N_EQ) {
+            const int q = r - (K3_N_EQ + K3_N_INEQ);
+            val = gval[1 + q / K3_N_EQ][q % K3_N_EQ];
+        } else {
+            const int i = r - (K3_N_EQ + K3_N_INEQ + D * K3_N_EQ);
+            double s = 0.0;
+            for (int rr = 0; rr < NN; ++rr) s += Dc[rr] * Xv(rr, i);
+            val = xk1[i] - s;
+        }
+        g[row0 + r] = val;
+    }
+    if (k == 0)
+        for (int i = tid; i < K3_NX; i += NT) g[i] = xk[i] - P[i];     // initial conditions
+
+    // ---- J_g values through the gather list ------------------------------------------------------
+    double* jac = a.jac + (size_t)b * a.nnz;
+    const int e0 = a.goff[k], e1 = a.goff[k + 1];
+    for (int e = e0 + tid; e < e1; e += NT) {
+        const uint32_t cd = a.gcode[e];
+        const uint32_t kind = cd >> 29;
+        const int rr = (cd >> 25) & 15, n = (cd >> 21) & 15, idx = cd & ((1u << 21) - 1u);
+        double val;
+        if (kind == kKindTang) val = tang[idx];
+        else if (kind == kKindTangPoly) val = tang[idx] * (C[rr * NN + n] * inv_h_tf);
+        else if (kind == kKindOne) val = 1.0;
+        else val = -Dc[rr];
+        jac[a.gslot[e]] = val;
+    }
+}
+
+// one wave per instance: objective partials in a fixed order, terminal cost, global gradient
+__global__ __launch_bounds__(64) void mpc_finalize_kernel(MArgs a) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const double* ref = P + K3_NX;
+    const double* pP = P + K3_NX + a.n_v + 1 + K3_NX + K3_NU;
+    double* grad = a.grad + (size_t)b * a.n_v;
+    const int xN = 11 + a.n_k * a.stride;
+    double term = 0.0;
+    if (lane < K3_NX) {
+        const double e = V[xN + lane] - ref[xN + lane];
+        grad[xN + lane] = 2.0 * pP[lane] * e;
+        term = pP[lane] * e * e;
+    }
+    if (lane < 11) grad[lane] = 0.0;                     // theta, phi, xi
+    __shared__ double tt[64];
+    tt[lane] = term;
+    __syncthreads();
+    if (lane == 0) {
+        double s = 0.0;
+        for (int k = 0; k < a.n_k; ++k) s += a.fpart[(size_t)b * a.n_k + k];
+        for (int i = 0; i < K3_NX; ++i) s += tt[i];
+        a.f[b] = s;
+    }
+}
+
+}  // namespace
+
+struct awempc_handle_s {
+    Tables t;
+    int batch = 0;
+    std::vector<double> consts;
+    double* d_cst = nullptr;
+    awt::DevColl* d_coll = nullptr;
+    int* d_goff = nullptr;
+    int* d_gslot = nullptr;
+    uint32_t* d_gcode = nullptr;
+    double* d_fpart = nullptr;
+    double *d_V = nullptr, *d_P = nullptr, *d_f = nullptr, *d_g = nullptr, *d_grad = nullptr, *d_jac = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool timed = false;
+};
+
+extern "C" {
+
+const char* awempc_last_error(void) { return g_err.c_str(); }
+
+int awempc_sparsity_jac_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind, int* row) {
+    if (!consts || !nnz) return fail(AWE_ERR_ARG, "null argument");
+    Tables T;
+    std::string err;
+    if (build_tables(n_k, d, consts, n_consts, T, err)) return fail(AWE_ERR_ARG, err);
+    *nnz = (int)T.row.size();
+    if (colind) std::memcpy(colind, T.colind.data(), sizeof(int) * T.colind.size());
+    if (row) std::memcpy(row, T.row.data(), sizeof(int) * T.row.size());
+    return AWE_OK;
+}
+
+int awempc_create(int n_k, int d, const double* consts, int n_consts, int batch, awempc_handle* out) {
+    if (!consts || !out || batch < 1) return fail(AWE_ERR_ARG, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(AWE_ERR_NODEVICE, "no HIP device");
+    if (d < 2 || d > 5) return fail(AWE_ERR_ARG, "the MPC kernel is instantiated for 2 <= d <= 5");
+    auto* h = new awempc_handle_s();
+    std::string err;
+    if (build_tables(n_k, d, consts, n_consts, h->t, err)) {
+        delete h;
+        return fail(AWE_ERR_ARG, err);
+    }
+    if (consts[K3_C_N_K] != (double)n_k || consts[K3_C_D] != (double)d) {
+        delete h;
+        return fail(AWE_ERR_ARG, "consts[K3_C_N_K], consts[K3_C_D] disagree with n_k, d");
+    }
+    h->batch = batch;
+    h->consts.assign(consts, consts + n_consts);
+    awt::DevColl dc{};
+    const int NN = d + 1;
+    for (int j = 0; j < NN; ++j) {
+        for (int r = 0; r < NN; ++r) dc.C[j * NN + r] = h->t.coll.C[j][r];
+        dc.D[j] = h->t.coll.D[j];
+    }
+    for (int j = 0; j < d; ++j) dc.w[j] = h->t.coll.w[j];
+    const Tables& T = h->t;
+#define MPC_UPLOAD(dst, src, n)                                                         \
+    MPC_TRY(hipMalloc((void**)&dst, sizeof(*dst) * (n)));                              \
+    MPC_TRY(hipMemcpy(dst, src, sizeof(*dst) * (n), hipMemcpyHostToDevice));
+    MPC_UPLOAD(h->d_cst, consts, n_consts);
+    MPC_UPLOAD(h->d_coll, &dc, 1);
+    MPC_UPLOAD(h->d_goff, T.goff.data(), T.goff.size());
+    MPC_UPLOAD(h->d_gslot, T.gslot.data(), T.gslot.size());
+    MPC_UPLOAD(h->d_gcode, T.gcode.data(), T.gcode.size());
+#undef MPC_UPLOAD
+    MPC_TRY(hipMalloc((void**)&h->d_fpart, sizeof(double) * (size_t)batch * n_k));
+    for (auto& e : h->ev) MPC_TRY(hipEventCreate(&e));
+    *out = h;
+    return AWE_OK;
+}
+
+int awempc_destroy(awempc_handle h) {
+    if (!h) return AWE_OK;
+    void* bufs[] = {h->d_cst, h->d_coll, h->d_goff, h->d_gslot, h->d_gcode, h->d_fpart,
+                    h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete h;
+    return AWE_OK;
+}
+
+int awempc_sizes(awempc_handle h, int* n_v, int* n_g, int* n_p, int* nnz) {
+    if (!h) return fail(AWE_ERR_ARG, "null handle");
+    if (n_v) *n_v = h->t.lay.n_v;
+    if (n_g) *n_g = h->t.lay.n_g;
+    if (n_p) *n_p = h->t.lay.n_p;
+    if (nnz) *nnz = (int)h->t.row.size();
+    return AWE_OK;
+}
+
+int awempc_sparsity_jac(awempc_handle h, int* colind, int* row) {
+    if (!h || !colind || !row) return fail(AWE_ERR_ARG, "null argument");
+    std::memcpy(colind, h->t.colind.data(), sizeof(int) * h->t.colind.size());
+    std::memcpy(row, h->t.row.data(), sizeof(int) * h->t.row.size());
+    return AWE_OK;
+}
+
+int awempc_eval_nlp(awempc_handle h, const double* V, const double* p, double* f, double* g, double* grad_f,
+                    double* jac, void* stream) {
+    if (!h || !V || !p || !f || !g || !grad_f || !jac) return fail(AWE_ERR_ARG, "null argument");
+    const Tables& T = h->t;
+    hipStream_t s = (hipStream_t)stream;
+    MArgs a{T.lay.n_k, T.lay.d, T.lay.n_v, T.lay.n_g, T.lay.n_p, (int)T.row.size(), T.lay.stride,
+            V, p, f, g, grad_f, jac, h->d_cst, h->d_coll, h->d_goff, h->d_gslot, h->d_gcode, h->d_fpart};
+    const dim3 grid((unsigned)(h->batch * T.lay.n_k));
+    MPC_TRY(hipEventRecord(h->ev[0], s));
+    switch (T.lay.d) {
+        case 2: mpc_interval_kernel<2><<<grid, 64 * waves_for<2>(), 0, s>>>(a); break;
+        case 3: mpc_interval_kernel<3><<<grid, 64 * waves_for<3>(), 0, s>>>(a); break;
+        case 4: mpc_interval_kernel<4><<<grid, 64 * waves_for<4>(), 0, s>>>(a); break;
+        case 5: mpc_interval_kernel<5><<<grid, 64 * waves_for<5>(), 0, s>>>(a); break;
+        default: return fail(AWE_ERR_ARG, "unsupported d");
+    }
+    MPC_TRY(hipGetLastError());
+    MPC_TRY(hipEventRecord(h->ev[1], s));
+    mpc_finalize_kernel<<<dim3((unsigned)h->batch), 64, 0, s>>>(a);
+    MPC_TRY(hipGetLastError());
+    MPC_TRY(hipEventRecord(h->ev[2], s));
+    h->timed = true;
+    return AWE_OK;
+}
+
+int awempc_last_kernel_ms(awempc_handle h, float* ms_main, float* ms_fin) {
+    if (!h || !h->timed) return fail(AWE_ERR_ARG, "no timed evaluation yet");
+    MPC_TRY(hipEventSynchronize(h->ev[2]));
+    if (ms_main) MPC_TRY(hipEventElapsedTime(ms_main, h->ev[0], h->ev[1]));
+    if (ms_fin) MPC_TRY(hipEventElapsedTime(ms_fin, h->ev[1], h->ev[2]));
+    return AWE_OK;
+}
+
+int awempc_eval_nlp_host(awempc_handle h, const double* V, const double* p, double* f, double* g, double* grad_f,
+                         double* jac) {
+    if (!h || !V || !p || !f || !g || !grad_f || !jac) return fail(AWE_ERR_ARG, "null argument");
+    const Tables& T = h->t;
+    const size_t nb = (size_t)h->batch, nnz = T.row.size();
+    if (!h->d_V) {
+        MPC_TRY(hipMalloc((void**)&h->d_V, sizeof(double) * nb * T.lay.n_v));
+        MPC_TRY(hipMalloc((void**)&h->d_P, sizeof(double) * nb * T.lay.n_p));
+        MPC_TRY(hipMalloc((void**)&h->d_f, sizeof(double) * nb));
+        MPC_TRY(hipMalloc((void**)&h->d_g, sizeof(double) * nb * T.lay.n_g));
+        MPC_TRY(hipMalloc((void**)&h->d_grad, sizeof(double) * nb * T.lay.n_v));
+        MPC_TRY(hipMalloc((void**)&h->d_jac, sizeof(double) * nb * nnz));
+    }
+    MPC_TRY(hipMemcpy(h->d_V, V, sizeof(double) * nb * T.lay.n_v, hipMemcpyHostToDevice));
+    MPC_TRY(hipMemcpy(h->d_P, p, sizeof(double) * nb * T.lay.n_p, hipMemcpyHostToDevice));
+    int rc = awempc_eval_nlp(h, h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac, nullptr);
+    if (rc) return rc;
+    MPC_TRY(hipDeviceSynchronize());
+    MPC_TRY(hipMemcpy(f, h->d_f, sizeof(double) * nb, hipMemcpyDeviceToHost));
+    MPC_TRY(hipMemcpy(g, h->d_g, sizeof(double) * nb * T.lay.n_g, hipMemcpyDeviceToHost));
+    MPC_TRY(hipMemcpy(grad_f, h->d_grad, sizeof(double) * nb * T.lay.n_v, hipMemcpyDeviceToHost));
+    MPC_TRY(hipMemcpy(jac, h->d_jac, sizeof(double) * nb * nnz, hipMemcpyDeviceToHost));
+    auto finite = [](const double* x, size_t n) {
+        for (size_t i = 0; i < n; ++i)
+            if (!std::isfinite(x[i])) return false;
+        return true;
+    };
+    if (!finite(f, nb) || !finite(g, nb * T.lay.n_g) || !finite(grad_f, nb * T.lay.n_v) || !finite(jac, nb * nnz))
+        return fail(AWE_ERR_NONFINITE, "non-finite output");
+    return AWE_OK;
+}
+
+}  // extern "C"

@@ -83,6 +83,8 @@ AWE_HD Dual exp(Dual a) {
     return Dual(e, e * a.d);
 }
 AWE_HD Dual log(Dual a) { return Dual(::log(a.v), a.d * rcp(a.v)); }
+AWE_HD Dual sin(Dual a) { return Dual(::sin(a.v), ::cos(a.v) * a.d); }
+AWE_HD Dual cos(Dual a) { return Dual(::cos(a.v), -::sin(a.v) * a.d); }
 AWE_HD double value(Dual a) { return a.v; }
 AWE_HD double tangent(Dual a) { return a.d; }
 
@@ -164,10 +166,14 @@ AWE_HD Dep& operator*=(Dep& a, Dep b) { a.m |= b.m; return a; }
 AWE_HD Dep sqrt(Dep a) { return a; }
 AWE_HD Dep exp(Dep a) { return a; }
 AWE_HD Dep log(Dep a) { return a; }
+AWE_HD Dep sin(Dep a) { return a; }
+AWE_HD Dep cos(Dep a) { return a; }
 
 AWE_HD double value(double a) { return a; }
 AWE_HD double sqrt(double a) { return ::sqrt(a); }
 AWE_HD double exp(double a) { return ::exp(a); }
 AWE_HD double log(double a) { return ::log(a); }
+AWE_HD double sin(double a) { return ::sin(a); }
+AWE_HD double cos(double a) { return ::cos(a); }
 
 }  // namespace awe

@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per thread setting")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hessian", action="store_true", help="skip the nlp_hess_l timing block")
+    ap.add_argument("--mpc-batch", type=int, default=256,
+                    help="MPC instances for the config-5 block (3-DOF tracking MPC, N=20 d=4; 0: skip)")
     ap.add_argument("--sweep-points", type=int, default=2,
                     help="u_ref sweep points solved per GPU for the sweep block (0: skip)")
     args = ap.parse_args()
@@ -150,6 +152,9 @@ def main():
     torch.cuda.synchronize()
     finite = bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item())
 
+    mpc = None
+    if args.mpc_batch > 0:
+        mpc = mpc_block(args.mpc_batch, rank, dev, dist, world)
     sweep = None
     if args.sweep_points > 0:
         sweep = sweep_block(args.sweep_points, world, dist, dev, consts)
@@ -198,6 +203,8 @@ def main():
                         "flops_per_launch": flops, "note": "FP64 VALU instructions x 64 lanes (FMA = 2), "
                         "from the PMC record; idle lanes of issued instructions count"}
         line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
+    if mpc is not None:
+        line["mpc"] = mpc
     if sweep is not None:
         line["sweep"] = sweep
     if not args.no_hessian:
@@ -207,6 +214,61 @@ def main():
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def mpc_block(B, rank, dev, dist, world, steps=50, warmup=5):
+    """Config 5: B tracking-MPC NLP instances of the 3-DOF AP2 kite (N=20, d=4) per
+    GPU, instance i starting at phase i T / B of the reference orbit with 0.01 N(0,1) noise (seed
+    99 + i); one step = one batched {f, g, grad f, J_g} evaluation (the linearisation of one
+    real-time iteration of every instance).  Weak scaling, max over ranks."""
+    import numpy as np
+    import torch
+
+    from awebox_amd import kite3 as k3
+    from awebox_amd.mpc import MpcEvaluator
+
+    c = k3.build_constants()
+    lay = k3.MpcLayout(c.cfg.n_k, c.cfg.d)
+    orbit = k3.CircularOrbit(c.cfg)
+    inst = [k3.batch_instance(c, lay, rank * B + i, B * world, orbit=orbit) for i in range(B)]
+    V = torch.tensor(np.stack([v for v, _ in inst]), device=dev)
+    P = torch.tensor(np.stack([p for _, p in inst]), device=dev)
+    ev = MpcEvaluator(c, batch=B)
+    f = torch.empty(B, dtype=torch.float64, device=dev)
+    g = torch.empty(B, ev.n_g, dtype=torch.float64, device=dev)
+    gr = torch.empty(B, ev.n_v, dtype=torch.float64, device=dev)
+    jac = torch.empty(B, ev.nnz, dtype=torch.float64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(warmup):
+        ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kms = []
+    for _ in range(10):
+        ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
+        kms.append(ev.last_kernel_ms()[0])
+    bytes_per_eval = 8 * (lay.n_v + lay.n_p + lay.n_g + lay.n_v + ev.nnz + 1)
+    kernel_ms = float(np.mean(kms))
+    achieved = bytes_per_eval * B / (kernel_ms * 1e-3) / 1e9
+    return {"metric": "MPC NLP f/g/Jacobian evals/sec, 3-DOF AP2 tracking MPC N=20 d=4 (config 5)",
+            "value": B * steps * world / el, "unit": "evals/s", "instances_per_gpu": B,
+            "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": ev.nnz,
+            "finite": bool(torch.isfinite(jac).all().item()),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "kernel": "mpc_interval_kernel<4>",
+                         "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval}}
 
 
 def sweep_block(per_gpu, world, dist, dev, consts):
