@@ -196,12 +196,13 @@ def main():
         hbm_bytes = 2.0 * rec["FETCH_SIZE_kB"] * 1024 + rec["WRITE_SIZE_kB"] * 1024
         line["roofline"]["traffic"] = hbm_bytes / (kernel_ms * 1e-3) / 1e9
         line["roofline"]["traffic_bytes_per_launch"] = hbm_bytes
-        flops = 64.0 * (rec["SQ_INSTS_VALU_ADD_F64"] + rec["SQ_INSTS_VALU_MUL_F64"] +
-                        2.0 * rec["SQ_INSTS_VALU_FMA_F64"] + rec["SQ_INSTS_VALU_TRANS_F64"])
-        tf = flops / (kernel_ms * 1e-3) / 1e12
-        line["fp64"] = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                        "flops_per_launch": flops, "note": "FP64 VALU instructions x 64 lanes (FMA = 2), "
-                        "from the PMC record; idle lanes of issued instructions count"}
+        f64 = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"]
+        if all(k in rec for k in f64):
+            flops = 64.0 * (rec[f64[0]] + rec[f64[1]] + 2.0 * rec[f64[2]] + rec[f64[3]])
+            tf = flops / (kernel_ms * 1e-3) / 1e12
+            line["fp64"] = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                            "flops_per_launch": flops, "note": "FP64 VALU instructions x 64 lanes (FMA = 2), "
+                            "from the PMC record; idle lanes of issued instructions count"}
         line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
     if mpc is not None:
         line["mpc"] = mpc
