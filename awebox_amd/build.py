@@ -1,7 +1,8 @@
 """Build the in-tree HIP shared libraries for gfx950.
 
 * ``awebox_amd/libawegpu.so`` -- the AP2 collocation evaluator (include/awegpu.h);
-* ``awebox_amd/libawempc.so`` -- the 3-DOF tracking-MPC evaluator (include/awempc.h).
+* ``awebox_amd/libawempc.so`` -- the 3-DOF tracking-MPC evaluator (include/awempc.h);
+* ``awebox_amd/libawedual.so`` -- the dual-kite (multi-kite) evaluator (include/awedual.h).
 
 Plain ``hipcc -shared -fPIC`` (no JIT cache): the .so files live next to this file so that they
 travel with the repository snapshot to the GPU box.
@@ -17,6 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libawegpu.so")
 LIB_MPC = os.path.join(HERE, "libawempc.so")
+LIB_DUAL = os.path.join(HERE, "libawedual.so")
 _COMMON = [os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
     os.path.join(INCLUDE, "awegpu.h")]
 TARGETS = {
@@ -24,6 +26,9 @@ TARGETS = {
     LIB_MPC: ([os.path.join(CSRC, "awempc.hip")],
               _COMMON + [os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp")]
               + [os.path.join(INCLUDE, "awempc.h")]),
+    LIB_DUAL: ([os.path.join(CSRC, "awedual.hip")],
+               _COMMON + [os.path.join(CSRC, f) for f in ("dual_model.hpp", "dual_tables.hpp")]
+               + [os.path.join(INCLUDE, "awedual.h")]),
 }
 ARCH = os.environ.get("AWE_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wno-unused-value",

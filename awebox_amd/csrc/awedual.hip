@@ -1,0 +1,651 @@
+// awedual -- MI355X (gfx950) evaluator for the awebox multi-kite power-cycle NLP (config 3: two
+// 6-DOF AP2 kites on secondary tethers, architecture {1: 0, 2: 1, 3: 1}, direct collocation
+// radau, zoh, phase_fix 'single_reelout'; examples/dual_kites_power_curve.py).
+//
+// Replaces the CasADi-expanded SX evaluation of f, g, grad f and J_g that IPOPT reaches through
+// nlpsol (awebox/opti/preparation.py:366-400).
+//
+// Execution model (the AP2 evaluator's design, awegpu.hip, scaled to the 126-variable node):
+//   * one workgroup per (NLP instance, shooting interval), ONE wavefront per node (d + 1 waves);
+//   * the interval's slice of V and of P.p.ref plus the effective objective weights are staged
+//     in LDS with coalesced loads;
+//   * model pass, compressed forward mode: the 127 seed directions of a node are coloured on the
+//     host into <= 64 groups with disjoint row sets (37 at the shooting node, 39 at a Radau node),
+//     so lane c of the node's wavefront evaluates dual_node in dual arithmetic along colour c and
+//     the wavefront recovers the whole node Jacobian block.  The collocation chain rule
+//     xdot = C X / (h t_f(k)) is folded into the seeds (dual_tables.hpp);
+//   * rows stream from the lanes into a compressed LDS tangent buffer (branch-free sink);
+//   * objective pass: one thread per (Radau node, direction) forms the directional derivative
+//     of the regularisation, beta and power terms; per V column they are summed in a fixed order;
+//   * write-out: g rows and grad f columns of the interval are contiguous stores; J_g values come
+//     from a host-built gather list (one entry per CCS slot: tangent index, polynomial scale or
+//     constant); a one-workgroup-per-instance finalize kernel reduces the interval partials in a
+//     fixed order (power cost over the phase-fixed period, time cost, homotopy) and writes the
+//     global gradient entries, the periodicity and t_f-bound rows.  No float atomics.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/awedual.h"
+#include "../../include/awegpu.h"
+#include "dual_model.hpp"
+#include "dual_tables.hpp"
+
+namespace {
+
+using namespace dlt;
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define ADL_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess)                                                          \
+            return fail(AWE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+constexpr int kNPart = 8;   // per interval: tracking, other, power integral A_k, d/d diam_t, t_f, l_s, diam_s
+constexpr int kCostTracking = 0, kCostURegularisation = 1, kCostXdotRegularisation = 2, kCostFictitious = 10,
+              kCostPower = 11, kCostTf = 13, kCostThetaRegularisation = 14, kCostBeta = 18;
+constexpr int kPhiCost[7] = {3, 6, 4, 5, 7, 8, 9};   // cost index of phi = [gamma tau iota psi eta nu upsilon]
+constexpr int kPhiPsi = 3;
+
+struct DArgs {
+    const double* V;
+    const double* P;
+    const double* cst;
+    awt::DevColl coll;
+    const ColorTabs* ct;
+    const int* goff;
+    const int* gslot;
+    const uint32_t* gcode;
+    double kconst[kMaxConst];
+    double* f;
+    double* g;
+    double* grad;
+    double* jac;
+    double* part;         // [B][n_k][kNPart]
+    int n_k, d, n_v, n_g, n_p, nnz, stride, v_int0, nkr, single, n_thv, tang_total;
+};
+
+__device__ __forceinline__ double time_period(const double* V, const DArgs& a) {
+    if (!a.single) return V[1];
+    return V[1] * a.nkr / a.n_k + V[2] * (a.n_k - a.nkr) / a.n_k;   // ocp_outputs.py:118-140
+}
+
+// node variable i along lane's colour
+struct DLaneIn {
+    const double* w;
+    const int8_t* col;
+    int lane;
+    double cxx;          // C[n][n] / (h tf) at a Radau node, 0 at the shooting node
+    double tfl;          // -1/tf if this lane carries the t_f colour of a Radau node, else 0
+    __device__ __forceinline__ awe::Dual operator()(int i) const {
+        double t = (col[i] == lane) ? 1.0 : 0.0;
+        if (i >= ADL_NX && i < 2 * ADL_NX) {
+            if (col[i - ADL_NX] == lane) t += cxx;
+            t += tfl * w[i];
+        }
+        return awe::Dual(w[i], t);
+    }
+};
+
+struct DSink {
+    double* tp;          // node tangent base + colour offset
+    double* gv;          // node values [kGvalStride]
+    double* dump;        // this lane's private dump slot
+    uint64_t lo, hi;
+    bool c0;
+    __device__ __forceinline__ void emit(int r, const awe::Dual& v) {
+        *(c0 ? gv + r : dump) = v.v;
+        bool on;
+        int idx;
+        if (r < 64) {
+            on = (lo >> r) & 1u;
+            idx = __popcll(lo & ((1ull << r) - 1ull));
+        } else {
+            on = (hi >> (r - 64)) & 1u;
+            idx = __popcll(lo) + __popcll(hi & ((1ull << (r - 64)) - 1ull));
+        }
+        *(on ? tp + idx : dump) = v.d;
+    }
+    __device__ __forceinline__ void eq_row(int r, const awe::Dual& v) { emit(r, v); }
+    __device__ __forceinline__ void ineq_row(int r, const awe::Dual& v) { emit(ADL_N_EQ + r, v); }
+    __device__ __forceinline__ void power(const awe::Dual& v) { emit(kRowPower, v); }
+    __device__ __forceinline__ void beta(int k, const awe::Dual& v) { emit(kRowBeta0 + k, v); }
+};
+
+template <int D>
+__global__ __launch_bounds__(64 * (D + 1)) void dual_interval_kernel(DArgs a) {
+    constexpr int NN = D + 1;
+    constexpr int NT = 64 * NN;
+    constexpr int STRIDE = 2 * ADL_NX + ADL_NU + ADL_NZ + D * (ADL_NX + ADL_NZ);
+    constexpr int NLOC = ADL_NTHV + 7 + STRIDE + ADL_NX;
+    __shared__ double vloc[NLOC];               // theta_v, phi, x[k], u, xdot, z, coll.., x[k+1]
+    __shared__ double rloc[ADL_NTHV + STRIDE];  // p.ref: theta_v, interval slice
+    __shared__ double wtr[ADL_NW];              // effective weights (x psi for tracking)
+    __shared__ double wef[ADL_NW];              // effective weights
+    __shared__ double wn[NN][128];              // node values (scaled), [126] = phi.gamma
+    __shared__ double rn[D][ADL_NW];            // reference values at the Radau nodes
+    __shared__ double gval[NN][kGvalStride];
+    __shared__ double obj[D][128];
+    __shared__ double fterm[D][128];
+    __shared__ double dumpbuf[NT];
+    __shared__ int8_t colb[2][128];
+    extern __shared__ double tang[];            // [tang_total]
+
+    const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
+    const int tid = threadIdx.x;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const int nthv = a.n_thv;
+    const int base = a.v_int0 + k * STRIDE;
+    // ---- stage -------------------------------------------------------------------------
+    for (int i = tid; i < NLOC; i += NT) {
+        double v = 0.0;
+        if (i < ADL_NTHV) v = i < nthv ? V[i] : 0.0;
+        else if (i < ADL_NTHV + 7) v = V[nthv + (i - ADL_NTHV)];
+        else v = V[base + (i - ADL_NTHV - 7)];
+        vloc[i] = v;
+    }
+    for (int i = tid; i < ADL_NTHV + STRIDE; i += NT)
+        rloc[i] = i < ADL_NTHV ? (i < nthv ? P[i] : 0.0) : P[base + (i - ADL_NTHV)];
+    for (int i = tid; i < 256; i += NT) colb[i >> 7][i & 127] = a.ct->col[i >> 7][i & 127];
+    const double* wts = P + a.n_v;
+    const double* cost = P + a.n_v + ADL_NW;
+    const double* th = P + a.n_v + ADL_NW + 20;
+    const double psi = vloc[ADL_NTHV + kPhiPsi];
+    for (int i = tid; i < ADL_NW; i += NT) {
+        int ci;
+        double nrm;
+        bool track = false;
+        if (i < ADL_NX || (i >= 119 && i < 122)) { ci = kCostTracking; nrm = a.cst[ADL_C_NORM_TRACKING]; track = true; }
+        else if (i < 2 * ADL_NX) { ci = kCostXdotRegularisation; nrm = a.cst[ADL_C_NORM_XDOT_REG]; }
+        else if (i < 119) {
+            const int u = i - 100;
+            const bool fict = (u % 9) < 6 && u < 18;
+            ci = fict ? kCostFictitious : kCostURegularisation;
+            nrm = a.cst[fict ? ADL_C_NORM_FICTITIOUS : ADL_C_NORM_U_REG];
+        } else { ci = kCostThetaRegularisation; nrm = a.cst[ADL_C_NORM_THETA_REG]; }
+        double we = wts[i] * cost[ci] / nrm;
+        if (i == awe::dl::kTf) we = 0.0;                      // objective.py:132 (t_f exception)
+        wef[i] = we;
+        wtr[i] = track ? psi * we : we;
+    }
+    __syncthreads();
+
+    const int tfi = a.single ? (k < a.nkr ? 1 : 2) : 1;
+    const double tf = vloc[tfi];
+    const double ihtf = (double)a.n_k / tf;
+    const double* C = a.coll.C;
+    const double* xk = vloc + ADL_NTHV + 7;
+    const double* uk = xk + ADL_NX;
+    const double* xdk = uk + ADL_NU;
+    const double* zk = xdk + ADL_NX;
+    const double* coll = zk + ADL_NZ;
+    const double* xk1 = coll + D * (ADL_NX + ADL_NZ);
+    auto Xv = [&](int r, int i) -> double { return r == 0 ? xk[i] : coll[(r - 1) * (ADL_NX + ADL_NZ) + i]; };
+    auto node_theta = [&](const double* tv, int t) -> double {   // [diam_t, t_f(k), l_s, diam_s]
+        if (t == 1) return tv[tfi];
+        return a.single ? tv[t == 0 ? 0 : t + 1] : tv[t];
+    };
+
+    // ---- node values --------------------------------------------------------------------
+    for (int t = tid; t < NN * 128; t += NT) {
+        const int n = t >> 7, i = t & 127;
+        double val = 0.0;
+        if (i < ADL_NX) val = Xv(n, i);
+        else if (i < 2 * ADL_NX) {
+            if (n == 0) val = xdk[i - ADL_NX];
+            else {
+                double s = 0.0;
+                for (int r = 0; r < NN; ++r) s += C[r * NN + n] * Xv(r, i - ADL_NX);
+                val = s * ihtf;
+            }
+        } else if (i < 2 * ADL_NX + ADL_NU) val = uk[i - 2 * ADL_NX];
+        else if (i < 2 * ADL_NX + ADL_NU + ADL_NZ) {
+            const int z = i - (2 * ADL_NX + ADL_NU);
+            val = n == 0 ? zk[z] : coll[(n - 1) * (ADL_NX + ADL_NZ) + ADL_NX + z];
+        } else if (i < ADL_NW) val = node_theta(vloc, i - (2 * ADL_NX + ADL_NU + ADL_NZ));
+        else if (i == 126) val = vloc[ADL_NTHV];                 // phi.gamma
+        wn[n][i] = val;
+    }
+    for (int t = tid; t < D * ADL_NW; t += NT) {
+        const int j = t / ADL_NW, i = t % ADL_NW;
+        const double* rl = rloc + ADL_NTHV;
+        double val;
+        if (i < ADL_NX) val = rl[2 * ADL_NX + ADL_NU + ADL_NZ + j * (ADL_NX + ADL_NZ) + i];
+        else if (i < 2 * ADL_NX) val = 0.0;                       // objective.py:186
+        else if (i < 2 * ADL_NX + ADL_NU) val = rl[ADL_NX + (i - 2 * ADL_NX)];
+        else if (i < 2 * ADL_NX + ADL_NU + ADL_NZ)
+            val = rl[2 * ADL_NX + ADL_NU + ADL_NZ + j * (ADL_NX + ADL_NZ) + ADL_NX + (i - (2 * ADL_NX + ADL_NU))];
+        else val = node_theta(rloc, i - (2 * ADL_NX + ADL_NU + ADL_NZ));
+        rn[j][i] = val;
+    }
+    __syncthreads();
+
+    // ---- model pass: wave = node, lane = colour ------------------------------------------
+    {
+        const int n = tid >> 6, lane = tid & 63;
+        const int kind = n > 0;
+        if (lane < a.ct->ncol[kind]) {
+            const int toff = n == 0 ? 0 : a.ct->tsize[0] + (n - 1) * a.ct->tsize[1];
+            DLaneIn in{wn[n], colb[kind], lane, n > 0 ? C[n * NN + n] * ihtf : 0.0,
+                       (n > 0 && colb[1][awe::dl::kTf] == lane) ? -1.0 / tf : 0.0};
+            DSink sink{tang + toff + a.ct->off[kind][lane], gval[n], &dumpbuf[tid], a.ct->cm_lo[kind][lane],
+                       a.ct->cm_hi[kind][lane], lane == 0};
+            awe::Dual gamma(wn[n][126], colb[kind][126] == lane ? 1.0 : 0.0);
+            awe::dual_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0);
+        }
+    }
+    __syncthreads();
+
+    // ---- objective: directional derivatives at the Radau nodes (objective.py:45-544) ------
+    const double T = time_period(V, a);
+    const double cb = cost[kCostBeta] / a.cst[ADL_C_NORM_BETA];
+    const double* wq_all = a.coll.w;
+    for (int t = tid; t < D * 128; t += NT) {
+        const int j = t >> 7, dir = t & 127, n = j + 1;
+        const double wq = wq_all[j];
+        const double* wv = wn[n];
+        const double* rv = rn[j];
+        const double cxx = C[n * NN + n] * ihtf;
+        double acc = 0.0, fterm_v = 0.0;
+        if (dir < ADL_NX) {
+            acc = 2.0 * wq * (wtr[dir] * (wv[dir] - rv[dir]) + wtr[ADL_NX + dir] * wv[ADL_NX + dir] * cxx);
+        } else if (dir < 2 * ADL_NX) {
+            acc = 2.0 * wq * wtr[dir] * wv[dir];
+        } else if (dir == awe::dl::kTf) {
+            for (int i = 0; i < ADL_NX; ++i) acc -= 2.0 * wq * wtr[ADL_NX + i] * wv[ADL_NX + i] * wv[ADL_NX + i] / tf;
+        } else if (dir < ADL_NW) {
+            acc = 2.0 * wq * wtr[dir] * (wv[dir] - rv[dir]);
+        }
+        if (dir < ADL_NW) {
+            const double e = wv[dir] - rv[dir];
+            fterm_v = wq * wef[dir] * e * e;
+        }
+        if (dir < 127) {
+            const int toff = a.ct->tsize[0] + (n - 1) * a.ct->tsize[1];
+            const int tp = a.ct->obj_tang[dir][0];
+            if (tp >= 0)
+                acc += (1.0 - psi) * (-cost[kCostPower]) * (tf / a.n_k) * wq / T * tang[toff + tp];
+            for (int kk = 0; kk < 2; ++kk) {
+                const int tb = a.ct->obj_tang[dir][1 + kk];
+                if (tb >= 0) acc += 2.0 * wq * cb * gval[n][kRowBeta0 + kk] * tang[toff + tb];
+            }
+        }
+        obj[j][dir] = acc;
+        fterm[j][dir] = fterm_v;
+    }
+    __syncthreads();
+
+    // ---- interval partials (fixed order) ---------------------------------------------------
+    if (tid == 0) {
+        double tr = 0.0, ot = 0.0, A = 0.0, pd[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < D; ++j) {
+            const int n = j + 1;
+            const double wq = wq_all[j];
+            for (int i = 0; i < ADL_NW; ++i) {
+                const bool track = i < ADL_NX || (i >= 119 && i < 122);
+                if (track) tr += fterm[j][i]; else ot += fterm[j][i];
+            }
+            ot += wq * cb * (gval[n][kRowBeta0] * gval[n][kRowBeta0] + gval[n][kRowBeta0 + 1] * gval[n][kRowBeta0 + 1]);
+            A += wq * gval[n][kRowPower] / a.n_k;
+            for (int q = 0; q < 4; ++q) pd[q] += obj[j][122 + q];
+        }
+        double* pp = a.part + ((size_t)b * a.n_k + k) * kNPart;
+        pp[0] = tr; pp[1] = ot; pp[2] = A;
+        for (int q = 0; q < 4; ++q) pp[3 + q] = pd[q];
+        pp[7] = 0.0;
+    }
+
+    // ---- gradient of the interval's own columns ------------------------------------------------
+    double* grad = a.grad + (size_t)b * a.n_v + base;
+    for (int c = tid; c < STRIDE; c += NT) {
+        double gr = 0.0;
+        if (c < ADL_NX) {
+            for (int m = 1; m < NN; ++m) gr += obj[m - 1][ADL_NX + c] * C[0 * NN + m] * ihtf;
+        } else if (c < ADL_NX + ADL_NU) {
+            for (int m = 1; m < NN; ++m) gr += obj[m - 1][2 * ADL_NX + (c - ADL_NX)];
+        } else if (c >= 2 * ADL_NX + ADL_NU + ADL_NZ) {
+            const int q = c - (2 * ADL_NX + ADL_NU + ADL_NZ);
+            const int j = q / (ADL_NX + ADL_NZ), e = q % (ADL_NX + ADL_NZ), n = j + 1;
+            if (e < ADL_NX) {
+                gr = obj[j][e];
+                for (int m = 1; m < NN; ++m)
+                    if (m != n) gr += obj[m - 1][ADL_NX + e] * C[n * NN + m] * ihtf;
+            } else {
+                gr = obj[j][2 * ADL_NX + ADL_NU + (e - ADL_NX)];
+            }
+        }
+        grad[c] = gr;
+    }
+    if (k == a.n_k - 1)
+        for (int c = tid; c < ADL_NX; c += NT) grad[STRIDE + c] = 0.0;    // x[n_k]
+
+    // ---- g rows of the interval --------------------------------------------------------------
+    double* g = a.g + (size_t)b * a.n_g;
+    constexpr int ROWS = ADL_N_EQ + ADL_N_INEQ + D * ADL_N_EQ + ADL_NX;
+    const int row0 = k * ROWS;
+    const double* Dc = a.coll.D;
+    for (int r = tid; r < ROWS; r += NT) {
+        double val;
+        if (r < ADL_N_EQ + ADL_N_INEQ) val = gval[0][r];
+        else if (r < ADL_N_EQ + ADL_N_INEQ + D * ADL_N_EQ) {
+            const int q = r - (ADL_N_EQ + ADL_N_INEQ);
+            val = gval[1 + q / ADL_N_EQ][q % ADL_N_EQ];
+        } else {
+            const int i = r - (ADL_N_EQ + ADL_N_INEQ + D * ADL_N_EQ);
+            double s = 0.0;
+            for (int rr = 0; rr < NN; ++rr) s += Dc[rr] * Xv(rr, i);
+            val = xk1[i] - s;
+        }
+        g[row0 + r] = val;
+    }
+
+    // ---- J_g values through the gather list -------------------------------------------------
+    double* jac = a.jac + (size_t)b * a.nnz;
+    const int e0 = a.goff[k], e1 = a.goff[k + 1];
+    for (int e = e0 + tid; e < e1; e += NT) {
+        const uint32_t cd = a.gcode[e];
+        const uint32_t kind = cd >> 29;
+        const int rr = (cd >> 25) & 15, n = (cd >> 21) & 15, idx = cd & ((1u << 21) - 1u);
+        double val;
+        if (kind == kKindTang) val = tang[idx];
+        else if (kind == kKindTangPoly) val = tang[idx] * (C[rr * NN + n] * ihtf);
+        else val = a.kconst[idx];
+        jac[a.gslot[e]] = val;
+    }
+}
+
+// one workgroup per instance: objective partials in a fixed order, power cost over the
+// phase-fixed period, time and homotopy costs, global gradient entries, periodicity and t_f rows
+__global__ __launch_bounds__(64) void dual_finalize_kernel(DArgs a) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const double* cost = P + a.n_v + ADL_NW;
+    double* grad = a.grad + (size_t)b * a.n_v;
+    double* g = a.g + (size_t)b * a.n_g;
+    const int nthv = a.n_thv;
+    if (lane == 0) {
+        const double* pp = a.part + (size_t)b * a.n_k * kNPart;
+        double tr = 0.0, ot = 0.0, e_end = 0.0, A0 = 0.0, A1 = 0.0, pdt = 0.0, pls = 0.0, pds = 0.0;
+        double ptf0 = 0.0, ptf1 = 0.0;
+        for (int k = 0; k < a.n_k; ++k) {
+            const double* q = pp + (size_t)k * kNPart;
+            const bool ph1 = a.single && k >= a.nkr;
+            const double tfk = V[ph1 ? 2 : 1];
+            tr += q[0];
+            ot += q[1];
+            e_end += tfk * q[2];
+            if (ph1) { A1 += q[2]; ptf1 += q[4]; } else { A0 += q[2]; ptf0 += q[4]; }
+            pdt += q[3]; pls += q[5]; pds += q[6];
+        }
+        const double T = time_period(V, a);
+        const double Tref = time_period(P, a);
+        const double psi = V[nthv + kPhiPsi];
+        const double cp = cost[kCostPower], ct = cost[kCostTf];
+        const double f_power = -cp * e_end / T;
+        double f = psi * tr + (1.0 - psi) * f_power + ot + ct * (T - Tref) * (T - Tref);
+        for (int i = 0; i < 7; ++i) f += cost[kPhiCost[i]] * V[nthv + i];
+        a.f[b] = f;
+        const double n0 = a.single ? (double)a.nkr / a.n_k : 1.0, n1 = a.single ? (double)(a.n_k - a.nkr) / a.n_k : 0.0;
+        grad[0] = pdt;
+        grad[1] = ptf0 + (1.0 - psi) * (-cp) * (A0 * T - e_end * n0) / (T * T) + 2.0 * ct * (T - Tref) * n0;
+        if (a.single) {
+            grad[2] = ptf1 + (1.0 - psi) * (-cp) * (A1 * T - e_end * n1) / (T * T) + 2.0 * ct * (T - Tref) * n1;
+            grad[3] = pls;
+            grad[4] = pds;
+        } else {
+            grad[2] = pls;
+            grad[3] = pds;
+        }
+        for (int i = 0; i < 7; ++i) grad[nthv + i] = cost[kPhiCost[i]] + (i == kPhiPsi ? tr - f_power : 0.0);
+        grad[nthv + 7] = 0.0;
+        grad[nthv + 8] = 0.0;
+        if (a.single) {
+            const double frac = a.cst[ADL_C_PHASE_FIX_REELOUT];
+            const int gt = a.n_k * (ADL_N_EQ + ADL_N_INEQ + a.d * ADL_N_EQ + ADL_NX) + ADL_NX;
+            g[gt] = (T - a.cst[ADL_C_TF_UB]) / frac;
+            g[gt + 1] = (a.cst[ADL_C_TF_LB] - T) / frac;
+        }
+    }
+    // periodicity rows, sorted x names (operation.py:245-266)
+    constexpr int kOrder[ADL_NX] = {24, 25, 26, 45, 46, 47, 49, 3, 4, 5, 9, 10, 11, 30, 31, 32, 48,
+                                    12, 13, 14, 33, 34, 35, 0, 1, 2, 6, 7, 8, 27, 28, 29,
+                                    15, 16, 17, 18, 19, 20, 21, 22, 23, 36, 37, 38, 39, 40, 41, 42, 43, 44};
+    const int gp = a.n_k * (ADL_N_EQ + ADL_N_INEQ + a.d * ADL_N_EQ + ADL_NX);
+    const int x0 = a.v_int0;
+    const int xT = a.v_int0 + (a.n_k - 1) * a.stride + 2 * ADL_NX + ADL_NU + ADL_NZ + (a.d - 1) * (ADL_NX + ADL_NZ);
+    for (int i = lane; i < ADL_NX; i += 64) g[gp + i] = V[x0 + kOrder[i]] - V[xT + kOrder[i]];
+}
+
+template <int D>
+int launch(const DArgs& a, int batch, size_t dyn, hipStream_t s) {
+    dual_interval_kernel<D><<<dim3((unsigned)(batch * a.n_k)), 64 * (D + 1), dyn, s>>>(a);
+    return 0;
+}
+
+}  // namespace
+
+struct adl_handle_s {
+    Tables t;
+    int batch = 0;
+    std::vector<double> consts;
+    double* d_cst = nullptr;
+    ColorTabs* d_ct = nullptr;
+    int* d_goff = nullptr;
+    int* d_gslot = nullptr;
+    uint32_t* d_gcode = nullptr;
+    double* d_part = nullptr;
+    double *d_V = nullptr, *d_P = nullptr, *d_f = nullptr, *d_g = nullptr, *d_grad = nullptr, *d_jac = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool timed = false;
+};
+
+extern "C" {
+
+const char* adl_last_error(void) { return g_err.c_str(); }
+
+int adl_sparsity_jac_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind, int* row) {
+    if (!consts || !nnz) return fail(AWE_ERR_ARG, "null argument");
+    Tables T;
+    std::string err;
+    if (build_tables(n_k, d, consts, n_consts, T, err)) return fail(AWE_ERR_ARG, err);
+    *nnz = (int)T.row.size();
+    if (colind) std::memcpy(colind, T.colind.data(), sizeof(int) * T.colind.size());
+    if (row) std::memcpy(row, T.row.data(), sizeof(int) * T.row.size());
+    return AWE_OK;
+}
+
+int adl_colour_counts(int n_k, int d, const double* consts, int n_consts, int* n_col_shoot, int* n_col_radau,
+                      int* tang_shoot, int* tang_radau) {
+    if (!consts) return fail(AWE_ERR_ARG, "null argument");
+    Tables T;
+    std::string err;
+    if (build_tables(n_k, d, consts, n_consts, T, err)) return fail(AWE_ERR_ARG, err);
+    if (n_col_shoot) *n_col_shoot = T.ct.ncol[0];
+    if (n_col_radau) *n_col_radau = T.ct.ncol[1];
+    if (tang_shoot) *tang_shoot = T.ct.tsize[0];
+    if (tang_radau) *tang_radau = T.ct.tsize[1];
+    return AWE_OK;
+}
+
+// Diagnostics (CPU, no device): value and full Jacobian of one node of the model, one direction
+// at a time in dual arithmetic.  w[ADL_NW + 1] (last = phi.gamma), th[AWE_NTHETA0];
+// val[75] = [eq 53, ineq 19, power, beta2, beta3]; jac[75 * 127] row-major.
+int adl_node_eval_host(const double* w, const double* th, const double* consts, int n_consts, double* val,
+                       double* jac) {
+    if (!w || !th || !consts || !val || !jac) return fail(AWE_ERR_ARG, "null argument");
+    if (n_consts != ADL_NCONST) return fail(AWE_ERR_ARG, "consts must have ADL_NCONST entries");
+    struct In {
+        const double* w;
+        int dir;
+        awe::Dual operator()(int i) const { return awe::Dual(w[i], i == dir ? 1.0 : 0.0); }
+    };
+    struct Sink {
+        awe::Dual rows[kNRows];
+        void eq_row(int r, const awe::Dual& v) { rows[r] = v; }
+        void ineq_row(int r, const awe::Dual& v) { rows[ADL_N_EQ + r] = v; }
+        void power(const awe::Dual& v) { rows[kRowPower] = v; }
+        void beta(int k, const awe::Dual& v) { rows[kRowBeta0 + k] = v; }
+    };
+    for (int dir = 0; dir < kDirs; ++dir) {
+        Sink s;
+        awe::dual_node<awe::Dual>(In{w, dir}, awe::Dual(w[ADL_NW], dir == ADL_NW ? 1.0 : 0.0), th, consts, s, true);
+        for (int r = 0; r < kNRows; ++r) {
+            jac[r * kDirs + dir] = s.rows[r].d;
+            if (dir == 0) val[r] = s.rows[r].v;
+        }
+    }
+    return AWE_OK;
+}
+
+int adl_create(int n_k, int d, const double* consts, int n_consts, int batch, adl_handle* out) {
+    if (!consts || !out || batch < 1) return fail(AWE_ERR_ARG, "bad argument");
+    if (d < 2 || d > 5) return fail(AWE_ERR_ARG, "the dual-kite kernel is instantiated for 2 <= d <= 5");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(AWE_ERR_NODEVICE, "no HIP device");
+    auto* h = new adl_handle_s();
+    std::string err;
+    if (build_tables(n_k, d, consts, n_consts, h->t, err)) {
+        delete h;
+        return fail(AWE_ERR_ARG, err);
+    }
+    const Tables& T = h->t;
+    if (T.gslot.size() >= (1u << 31) || T.tang_total >= (1 << 21)) {
+        delete h;
+        return fail(AWE_ERR_ARG, "tables exceed the gather-code range");
+    }
+    h->batch = batch;
+    h->consts.assign(consts, consts + n_consts);
+#define ADL_UPLOAD(dst, src, n)                                                      \
+    ADL_TRY(hipMalloc((void**)&dst, sizeof(*dst) * (n)));                            \
+    ADL_TRY(hipMemcpy(dst, src, sizeof(*dst) * (n), hipMemcpyHostToDevice));
+    ADL_UPLOAD(h->d_cst, consts, n_consts);
+    ADL_UPLOAD(h->d_ct, &T.ct, 1);
+    ADL_UPLOAD(h->d_goff, T.goff.data(), T.goff.size());
+    ADL_UPLOAD(h->d_gslot, T.gslot.data(), T.gslot.size());
+    ADL_UPLOAD(h->d_gcode, T.gcode.data(), T.gcode.size());
+#undef ADL_UPLOAD
+    ADL_TRY(hipMalloc((void**)&h->d_part, sizeof(double) * (size_t)batch * n_k * kNPart));
+    for (auto& e : h->ev) ADL_TRY(hipEventCreate(&e));
+    *out = h;
+    return AWE_OK;
+}
+
+int adl_destroy(adl_handle h) {
+    if (!h) return AWE_OK;
+    void* bufs[] = {h->d_cst, h->d_ct, h->d_goff, h->d_gslot, h->d_gcode, h->d_part,
+                    h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete h;
+    return AWE_OK;
+}
+
+int adl_sizes(adl_handle h, int* n_v, int* n_g, int* n_p, int* nnz) {
+    if (!h) return fail(AWE_ERR_ARG, "null handle");
+    if (n_v) *n_v = h->t.lay.n_v;
+    if (n_g) *n_g = h->t.lay.n_g;
+    if (n_p) *n_p = h->t.lay.n_p;
+    if (nnz) *nnz = (int)h->t.row.size();
+    return AWE_OK;
+}
+
+int adl_sparsity_jac(adl_handle h, int* colind, int* row) {
+    if (!h || !colind || !row) return fail(AWE_ERR_ARG, "null argument");
+    std::memcpy(colind, h->t.colind.data(), sizeof(int) * h->t.colind.size());
+    std::memcpy(row, h->t.row.data(), sizeof(int) * h->t.row.size());
+    return AWE_OK;
+}
+
+int adl_eval_nlp(adl_handle h, const double* V, const double* P, double* f, double* g, double* grad_f, double* jac,
+                 void* stream) {
+    if (!h || !V || !P || !f || !g || !grad_f || !jac) return fail(AWE_ERR_ARG, "null argument");
+    const Tables& T = h->t;
+    const Layout& L = T.lay;
+    hipStream_t s = (hipStream_t)stream;
+    DArgs a{};
+    a.V = V; a.P = P; a.cst = h->d_cst;
+    for (int j = 0; j <= L.d; ++j) {
+        for (int r = 0; r <= L.d; ++r) a.coll.C[j * (L.d + 1) + r] = T.coll.C[j][r];
+        a.coll.D[j] = T.coll.D[j];
+    }
+    for (int j = 0; j < L.d; ++j) a.coll.w[j] = T.coll.w[j];
+    a.ct = h->d_ct; a.goff = h->d_goff; a.gslot = h->d_gslot; a.gcode = h->d_gcode;
+    for (size_t q = 0; q < T.kconst.size(); ++q) a.kconst[q] = T.kconst[q];
+    a.f = f; a.g = g; a.grad = grad_f; a.jac = jac; a.part = h->d_part;
+    a.n_k = L.n_k; a.d = L.d; a.n_v = L.n_v; a.n_g = L.n_g; a.n_p = L.n_p; a.nnz = (int)T.row.size();
+    a.stride = L.stride; a.v_int0 = L.v_int0; a.nkr = L.nk_reelout; a.single = L.single; a.n_thv = L.n_thv;
+    a.tang_total = T.tang_total;
+    const size_t dyn = sizeof(double) * (size_t)T.tang_total;
+    ADL_TRY(hipEventRecord(h->ev[0], s));
+    switch (L.d) {
+        case 2: launch<2>(a, h->batch, dyn, s); break;
+        case 3: launch<3>(a, h->batch, dyn, s); break;
+        case 4: launch<4>(a, h->batch, dyn, s); break;
+        case 5: launch<5>(a, h->batch, dyn, s); break;
+        default: return fail(AWE_ERR_ARG, "unsupported d");
+    }
+    ADL_TRY(hipGetLastError());
+    ADL_TRY(hipEventRecord(h->ev[1], s));
+    dual_finalize_kernel<<<dim3((unsigned)h->batch), 64, 0, s>>>(a);
+    ADL_TRY(hipGetLastError());
+    ADL_TRY(hipEventRecord(h->ev[2], s));
+    h->timed = true;
+    return AWE_OK;
+}
+
+int adl_last_kernel_ms(adl_handle h, float* ms_main, float* ms_fin) {
+    if (!h || !h->timed) return fail(AWE_ERR_ARG, "no timed evaluation yet");
+    ADL_TRY(hipEventSynchronize(h->ev[2]));
+    if (ms_main) ADL_TRY(hipEventElapsedTime(ms_main, h->ev[0], h->ev[1]));
+    if (ms_fin) ADL_TRY(hipEventElapsedTime(ms_fin, h->ev[1], h->ev[2]));
+    return AWE_OK;
+}
+
+int adl_eval_nlp_host(adl_handle h, const double* V, const double* P, double* f, double* g, double* grad_f,
+                      double* jac) {
+    if (!h || !V || !P || !f || !g || !grad_f || !jac) return fail(AWE_ERR_ARG, "null argument");
+    const Layout& L = h->t.lay;
+    const size_t nb = (size_t)h->batch, nnz = h->t.row.size();
+    if (!h->d_V) {
+        ADL_TRY(hipMalloc((void**)&h->d_V, sizeof(double) * nb * L.n_v));
+        ADL_TRY(hipMalloc((void**)&h->d_P, sizeof(double) * nb * L.n_p));
+        ADL_TRY(hipMalloc((void**)&h->d_f, sizeof(double) * nb));
+        ADL_TRY(hipMalloc((void**)&h->d_g, sizeof(double) * nb * L.n_g));
+        ADL_TRY(hipMalloc((void**)&h->d_grad, sizeof(double) * nb * L.n_v));
+        ADL_TRY(hipMalloc((void**)&h->d_jac, sizeof(double) * nb * nnz));
+    }
+    ADL_TRY(hipMemcpy(h->d_V, V, sizeof(double) * nb * L.n_v, hipMemcpyHostToDevice));
+    ADL_TRY(hipMemcpy(h->d_P, P, sizeof(double) * nb * L.n_p, hipMemcpyHostToDevice));
+    int rc = adl_eval_nlp(h, h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac, nullptr);
+    if (rc) return rc;
+    ADL_TRY(hipDeviceSynchronize());
+    ADL_TRY(hipMemcpy(f, h->d_f, sizeof(double) * nb, hipMemcpyDeviceToHost));
+    ADL_TRY(hipMemcpy(g, h->d_g, sizeof(double) * nb * L.n_g, hipMemcpyDeviceToHost));
+    ADL_TRY(hipMemcpy(grad_f, h->d_grad, sizeof(double) * nb * L.n_v, hipMemcpyDeviceToHost));
+    ADL_TRY(hipMemcpy(jac, h->d_jac, sizeof(double) * nb * nnz, hipMemcpyDeviceToHost));
+    auto finite = [](const double* x, size_t n) {
+        for (size_t i = 0; i < n; ++i)
+            if (!std::isfinite(x[i])) return false;
+        return true;
+    };
+    if (!finite(f, nb) || !finite(g, nb * L.n_g) || !finite(grad_f, nb * L.n_v) || !finite(jac, nb * nnz))
+        return fail(AWE_ERR_NONFINITE, "non-finite output");
+    return AWE_OK;
+}
+
+}  // extern "C"

@@ -169,6 +169,36 @@ AWE_HD Dep log(Dep a) { return a; }
 AWE_HD Dep sin(Dep a) { return a; }
 AWE_HD Dep cos(Dep a) { return a; }
 
+// Dep over <= 128 inputs (the multi-kite node has 126 variables + phi.gamma); host only.
+struct Dep2 {
+    uint64_t lo, hi;
+    AWE_HD Dep2() : lo(0), hi(0) {}
+    AWE_HD Dep2(double) : lo(0), hi(0) {}
+    AWE_HD static Dep2 bit(int i) {
+        Dep2 d;
+        if (i < 64) d.lo = (uint64_t)1 << i; else d.hi = (uint64_t)1 << (i - 64);
+        return d;
+    }
+    AWE_HD bool has(int i) const { return i < 64 ? ((lo >> i) & 1u) : ((hi >> (i - 64)) & 1u); }
+};
+AWE_HD Dep2 mk_dep2(uint64_t lo, uint64_t hi) { Dep2 d; d.lo = lo; d.hi = hi; return d; }
+AWE_HD Dep2 operator+(Dep2 a, Dep2 b) { return mk_dep2(a.lo | b.lo, a.hi | b.hi); }
+AWE_HD Dep2 operator-(Dep2 a, Dep2 b) { return mk_dep2(a.lo | b.lo, a.hi | b.hi); }
+AWE_HD Dep2 operator-(Dep2 a) { return a; }
+AWE_HD Dep2 operator*(Dep2 a, Dep2 b) { return mk_dep2(a.lo | b.lo, a.hi | b.hi); }
+AWE_HD Dep2 operator/(Dep2 a, Dep2 b) { return mk_dep2(a.lo | b.lo, a.hi | b.hi); }
+AWE_HD Dep2 operator+(Dep2 a, double) { return a; }
+AWE_HD Dep2 operator+(double, Dep2 b) { return b; }
+AWE_HD Dep2 operator-(Dep2 a, double) { return a; }
+AWE_HD Dep2 operator-(double, Dep2 b) { return b; }
+AWE_HD Dep2 operator*(Dep2 a, double) { return a; }
+AWE_HD Dep2 operator*(double, Dep2 b) { return b; }
+AWE_HD Dep2 operator/(Dep2 a, double) { return a; }
+AWE_HD Dep2 operator/(double, Dep2 b) { return b; }
+AWE_HD Dep2 sqrt(Dep2 a) { return a; }
+AWE_HD Dep2 exp(Dep2 a) { return a; }
+AWE_HD Dep2 log(Dep2 a) { return a; }
+
 AWE_HD double value(double a) { return a; }
 AWE_HD double sqrt(double a) { return ::sqrt(a); }
 AWE_HD double exp(double a) { return ::exp(a); }

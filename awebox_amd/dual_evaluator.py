@@ -1,0 +1,191 @@
+"""ctypes binding of ``libawedual.so`` (include/awedual.h): the multi-kite NLP oracle surface.
+
+``DualEvaluator`` serves ``nlp_f`` / ``nlp_g`` / ``nlp_grad_f`` / ``nlp_jac_g`` for the dual-kite
+power-cycle NLP (config 3) with CasADi's argument meaning (x = V, p = P) and J_g in CCS
+(awebox/opti/preparation.py:366-400), plus the batched device-pointer path used by the sweep
+driver and ``bench.py``.  No CPU fallback: a missing library or device raises
+``AwegpuUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import dual as du
+from .evaluator import AWE_ERR_NODEVICE, AWE_OK, AwegpuError, AwegpuUnavailable, _dptr
+
+_LIB = None
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libawedual.so")
+
+EXPORTED_SYMBOLS = ["adl_create", "adl_destroy", "adl_last_error", "adl_sizes", "adl_sparsity_jac",
+                    "adl_sparsity_jac_static", "adl_colour_counts", "adl_eval_nlp", "adl_eval_nlp_host",
+                    "adl_last_kernel_ms", "adl_node_eval_host"]
+
+
+def load_library(path: str = _LIB_PATH):
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise AwegpuUnavailable(f"{path} not built; run `python -m awebox_amd.build`")
+    lib = ctypes.CDLL(path)
+    dp = ctypes.POINTER(ctypes.c_double)
+    ip = ctypes.POINTER(ctypes.c_int)
+    h = ctypes.c_void_p
+    lib.adl_create.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(h)]
+    lib.adl_destroy.argtypes = [h]
+    lib.adl_last_error.restype = ctypes.c_char_p
+    lib.adl_sizes.argtypes = [h, ip, ip, ip, ip]
+    lib.adl_sparsity_jac.argtypes = [h, ip, ip]
+    lib.adl_sparsity_jac_static.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip]
+    lib.adl_colour_counts.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip, ip]
+    lib.adl_eval_nlp.argtypes = [h] + [ctypes.c_void_p] * 7
+    lib.adl_eval_nlp_host.argtypes = [h, dp, dp, dp, dp, dp, dp]
+    lib.adl_last_kernel_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.adl_node_eval_host.argtypes = [dp, dp, dp, ctypes.c_int, dp, dp]
+    _LIB = lib
+    return lib
+
+
+def _err(lib):
+    return lib.adl_last_error().decode()
+
+
+def sparsity_jac_static(consts: du.MultiConstants):
+    """CCS pattern (colind, row) of J_g derived on the CPU -- no device needed."""
+    lib = load_library()
+    cfg = consts.cfg
+    c = np.ascontiguousarray(consts.consts, dtype=np.float64)
+    nnz = ctypes.c_int()
+    ip = ctypes.POINTER(ctypes.c_int)
+    if lib.adl_sparsity_jac_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz), None, None) != AWE_OK:
+        raise AwegpuError(_err(lib))
+    lay = du.layout_for(consts)
+    colind = np.zeros(lay.n_v + 1, dtype=np.int32)
+    row = np.zeros(nnz.value, dtype=np.int32)
+    if lib.adl_sparsity_jac_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
+                                   colind.ctypes.data_as(ip), row.ctypes.data_as(ip)) != AWE_OK:
+        raise AwegpuError(_err(lib))
+    return colind, row
+
+
+def colour_counts(consts: du.MultiConstants):
+    """(colours at the shooting node, at a Radau node, tangent entries of each) -- CPU only."""
+    lib = load_library()
+    c = np.ascontiguousarray(consts.consts, dtype=np.float64)
+    out = [ctypes.c_int() for _ in range(4)]
+    if lib.adl_colour_counts(consts.cfg.n_k, consts.cfg.d, _dptr(c), c.size, *[ctypes.byref(o) for o in out]) != AWE_OK:
+        raise AwegpuError(_err(lib))
+    return tuple(o.value for o in out)
+
+
+def node_eval_host(w: np.ndarray, theta0: np.ndarray, consts: du.MultiConstants):
+    """Diagnostics (CPU): values [75] and Jacobian [75, 127] of one node of the HIP model's
+    source, evaluated on the host in dual arithmetic (the kernel's model code, not the oracle)."""
+    lib = load_library()
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    th = np.ascontiguousarray(theta0, dtype=np.float64)
+    c = np.ascontiguousarray(consts.consts, dtype=np.float64)
+    val = np.zeros(75)
+    jac = np.zeros((75, 127))
+    if lib.adl_node_eval_host(_dptr(w), _dptr(th), _dptr(c), c.size, _dptr(val), _dptr(jac)) != AWE_OK:
+        raise AwegpuError(_err(lib))
+    return val, jac
+
+
+class DualEvaluator:
+    """HIP evaluator of the dual-kite direct-collocation NLP for ``batch`` (V, P) instances."""
+
+    def __init__(self, consts: du.MultiConstants | None = None, batch: int = 1):
+        self.consts = consts or du.build_constants()
+        cfg = self.consts.cfg
+        self.layout = du.layout_for(self.consts)
+        self.batch = int(batch)
+        self._lib = load_library()
+        c = np.ascontiguousarray(self.consts.consts, dtype=np.float64)
+        handle = ctypes.c_void_p()
+        self._check(self._lib.adl_create(cfg.n_k, cfg.d, _dptr(c), c.size, self.batch, ctypes.byref(handle)))
+        self._h = handle
+        n_v, n_g, n_p, nnz = (ctypes.c_int() for _ in range(4))
+        self._check(self._lib.adl_sizes(self._h, ctypes.byref(n_v), ctypes.byref(n_g), ctypes.byref(n_p),
+                                        ctypes.byref(nnz)))
+        self.n_v, self.n_g, self.n_p, self.nnz = n_v.value, n_g.value, n_p.value, nnz.value
+        assert (self.n_v, self.n_g, self.n_p) == (self.layout.n_v, self.layout.n_g, self.layout.n_p)
+        self._colind = np.zeros(self.n_v + 1, dtype=np.int32)
+        self._row = np.zeros(self.nnz, dtype=np.int32)
+        ip = ctypes.POINTER(ctypes.c_int)
+        self._check(self._lib.adl_sparsity_jac(self._h, self._colind.ctypes.data_as(ip), self._row.ctypes.data_as(ip)))
+
+    def _check(self, rc):
+        if rc != AWE_OK:
+            msg = _err(self._lib)
+            if rc == AWE_ERR_NODEVICE:
+                raise AwegpuUnavailable(msg)
+            raise AwegpuError(f"awedual error {rc}: {msg}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.adl_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sparsity_jac(self):
+        return self._colind.copy(), self._row.copy()
+
+    def jac_csc(self, values):
+        import scipy.sparse as sp
+        return sp.csc_matrix((np.asarray(values), self._row, self._colind), shape=(self.n_g, self.n_v))
+
+    def eval_nlp_device(self, V, P, f, g, grad_f, jac, stream=None):
+        """f, g, grad f, J_g for all instances; contiguous float64 CUDA tensors [B, n_v], [B, n_p],
+        [B], [B, n_g], [B, n_v], [B, nnz]."""
+        import torch
+        for t, n in ((V, self.n_v), (P, self.n_p), (f, 1), (g, self.n_g), (grad_f, self.n_v), (jac, self.nnz)):
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
+                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.adl_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
+                                           grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
+
+    def last_kernel_ms(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        self._check(self._lib.adl_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def eval_nlp(self, V, P):
+        V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))
+        P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(self.batch, self.n_p))
+        f = np.zeros(self.batch)
+        g = np.zeros((self.batch, self.n_g))
+        grad = np.zeros((self.batch, self.n_v))
+        jac = np.zeros((self.batch, self.nnz))
+        self._check(self._lib.adl_eval_nlp_host(self._h, _dptr(V), _dptr(P), _dptr(f), _dptr(g), _dptr(grad),
+                                                _dptr(jac)))
+        return {"f": f, "g": g, "grad_f": grad, "jac": jac}
+
+    # ---- CasADi nlpsol oracle names (one instance) -----------------------------------
+    def _single(self, x, p):
+        if self.batch != 1:
+            raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
+        return self.eval_nlp(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1))
+
+    def nlp_f(self, x, p):
+        return float(self._single(x, p)["f"][0])
+
+    def nlp_g(self, x, p):
+        return self._single(x, p)["g"][0]
+
+    def nlp_grad_f(self, x, p):
+        out = self._single(x, p)
+        return float(out["f"][0]), out["grad_f"][0]
+
+    def nlp_jac_g(self, x, p):
+        out = self._single(x, p)
+        return out["g"][0], self.jac_csc(out["jac"][0])

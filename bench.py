@@ -43,10 +43,9 @@ def kernel_source_hash() -> str:
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "awebox_amd", "csrc")
-    for name in sorted(os.listdir(csrc)):
-        if name.endswith((".hip", ".hpp")):
-            with open(os.path.join(csrc, name), "rb") as fh:
-                h.update(name.encode() + fh.read())
+    for name in ("ap2_model.hpp", "ap2_tables.hpp", "awegpu.hip", "scalar.hpp"):   # the AP2 kernel's sources
+        with open(os.path.join(csrc, name), "rb") as fh:
+            h.update(name.encode() + fh.read())
     with open(os.path.join(ROOT, "include", "awegpu.h"), "rb") as fh:
         h.update(fh.read())
     return h.hexdigest()[:16]
@@ -75,6 +74,8 @@ def main():
     ap.add_argument("--no-hessian", action="store_true", help="skip the nlp_hess_l timing block")
     ap.add_argument("--mpc-batch", type=int, default=256,
                     help="MPC instances for the config-5 block (3-DOF tracking MPC, N=20 d=4; 0: skip)")
+    ap.add_argument("--dual-batch", type=int, default=128,
+                    help="dual-kite NLP instances for the config-3 block (N=60 d=4 single_reelout; 0: skip)")
     ap.add_argument("--sweep-points", type=int, default=2,
                     help="u_ref sweep points solved per GPU for the sweep block (0: skip)")
     args = ap.parse_args()
@@ -152,6 +153,9 @@ def main():
     torch.cuda.synchronize()
     finite = bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item())
 
+    dual = None
+    if args.dual_batch > 0:
+        dual = dual_block(args.dual_batch, rank, dev, dist, world)
     mpc = None
     if args.mpc_batch > 0:
         mpc = mpc_block(args.mpc_batch, rank, dev, dist, world)
@@ -204,6 +208,8 @@ def main():
                             "flops_per_launch": flops, "note": "FP64 VALU instructions x 64 lanes (FMA = 2), "
                             "from the PMC record; idle lanes of issued instructions count"}
         line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
+    if dual is not None:
+        line["dual"] = dual
     if mpc is not None:
         line["mpc"] = mpc
     if sweep is not None:
@@ -215,6 +221,71 @@ def main():
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def dual_block(B, rank, dev, dist, world, steps=20, warmup=3):
+    """Config 3: B dual-kite NLP instances per GPU (architecture {1:0, 2:1, 3:1},
+    N=60, d=4, single_reelout; examples/dual_kites_power_curve.py), synthetic members
+    V0 + 0.01 N(0,1) of the standard multi-kite initial guess; one step = one batched
+    {f, g, grad f, J_g} evaluation.  Weak scaling, max over ranks."""
+    import numpy as np
+    import torch
+
+    from awebox_amd import dual as du
+    from awebox_amd.dual_evaluator import DualEvaluator, colour_counts
+
+    c = du.build_constants()
+    lay = du.layout_for(c)
+    v0 = du.initial_guess(c, lay)
+    V = torch.tensor(np.stack([du.batch_member(v0, lay, rank * B + b) for b in range(B)]), device=dev)
+    P = torch.tensor(np.stack([du.pack_p(lay, c, v0)] * B), device=dev)
+    ev = DualEvaluator(c, batch=B)
+    f = torch.empty(B, dtype=torch.float64, device=dev)
+    g = torch.empty(B, ev.n_g, dtype=torch.float64, device=dev)
+    gr = torch.empty(B, ev.n_v, dtype=torch.float64, device=dev)
+    jac = torch.empty(B, ev.nnz, dtype=torch.float64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(warmup):
+        ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kms, fms = [], []
+    for _ in range(10):
+        ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
+        a, b_ = ev.last_kernel_ms()
+        kms.append(a)
+        fms.append(b_)
+    m = c.model
+    bytes_per_eval = 8 * (lay.n_v + lay.n_v + pb_ntheta0() + m.nw + 20 + lay.n_g + lay.n_v + ev.nnz + 1)
+    kernel_ms = float(np.mean(kms))
+    achieved = bytes_per_eval * B / (kernel_ms * 1e-3) / 1e9
+    ncol = colour_counts(c)
+    return {"metric": "dual-kite NLP f/g/Jacobian evals/sec, N=60 d=4 single_reelout (config 3)",
+            "value": B * steps * world / el, "unit": "evals/s", "instances_per_gpu": B,
+            "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": ev.nnz,
+            "colours_shooting_radau": [ncol[0], ncol[1]],
+            "finite": bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item()),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "kernel": "dual_interval_kernel<4>",
+                         "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)),
+                         "bytes_per_eval": bytes_per_eval}}
+
+
+def pb_ntheta0():
+    from awebox_amd import problem as pb
+    return pb.NTHETA0
 
 
 def mpc_block(B, rank, dev, dist, world, steps=50, warmup=5):

@@ -1,0 +1,187 @@
+"""Multi-kite (config 3, dual kites) host pipeline, oracle and HIP model source -- CPU only.
+
+* the generic multi-kite oracle reproduces the pinned AP2 oracle exactly at architecture {1: 0};
+* sizes, header contract and derived constants follow the reference formulas;
+* the HIP model source (dual_node, evaluated on the host through the library's diagnostics
+  entry in dual arithmetic) agrees with the oracle's automatic derivatives at node level;
+* the CPU-derived J_g pattern covers every oracle non-zero.
+"""
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+from torch.func import jacfwd
+
+from awebox_amd import dual as du
+from awebox_amd import problem as pb
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "awedual.h")
+
+
+def _defines():
+    return {m.group(1): int(m.group(2)) for m in re.finditer(r"#define (ADL_\w+) (\d+)", open(HEADER).read())}
+
+
+def test_sizes_match_survey():
+    mc = du.build_constants()
+    lay = du.layout_for(mc)
+    m = mc.model
+    # x=50, xdot=50, u=19, z=3, theta=4; eq 53, ineq 19; n_V=20104, n_g=20092
+    assert (m.nx, m.nu, m.nz, m.nth, m.n_eq, m.n_ineq) == (50, 19, 3, 4, 53, 19)
+    assert (lay.n_v, lay.n_g) == (20104, 20092)
+    assert lay.theta_names == ["diam_t", "t_f0", "t_f1", "l_s", "diam_s"]
+    assert lay.nk_reelout == 42
+
+
+def test_header_contract():
+    d = _defines()
+    mc = du.build_constants()
+    m = mc.model
+    assert (d["ADL_NX"], d["ADL_NU"], d["ADL_NZ"], d["ADL_NTH"], d["ADL_NW"]) == (m.nx, m.nu, m.nz, m.nth, m.nw)
+    assert (d["ADL_N_EQ"], d["ADL_N_INEQ"], d["ADL_NCONST"]) == (m.n_eq, m.n_ineq, du.NCONST)
+    for macro, val in d.items():
+        if macro.startswith("ADL_C_") and macro not in ("ADL_C_SCALING", "ADL_C_SD_LEN"):
+            assert du.CONST_NAMES[val] == macro[len("ADL_C_"):].lower(), macro
+    assert d["ADL_C_SCALING"] == du.CONST_IDX["scaling0"] and d["ADL_C_SD_LEN"] == du.CONST_IDX["sd_len0"]
+    # node-variable offsets used by dual_model.hpp (namespace dl)
+    off = {n: o for (vt, n), (o, s) in m.off.items() if vt != "xdot"}
+    assert (off["q21"], off["dq21"], off["omega21"], off["r21"], off["delta21"]) == (6, 9, 12, 15, 24)
+    assert (off["q31"], off["l_t"], off["f_fict21"], off["f_fict31"], off["ddl_t"]) == (27, 48, 100, 109, 118)
+    assert (off["lambda10"], off["diam_t"], off["t_f"], off["l_s"], off["diam_s"]) == (119, 122, 123, 124, 125)
+
+
+def test_derived_constants_follow_model_funcs():
+    mc = du.build_constants()
+    det, m, s = mc.details, mc.model, mc.scaling
+    cfg = mc.cfg
+    sl = lambda vt, n: s[m.sl(vt, n)]  # noqa: E731
+    # dq of the layer node by the wind at altitude, kites by the groundspeed (model_funcs.py:262-268)
+    u_alt = cfg.u_ref * (math.sqrt((200 * math.sin(math.pi / 4)) ** 2 + 1) / 10.0) ** 0.15
+    assert det["u_alt"] == pytest.approx(u_alt, rel=1e-14)
+    assert np.allclose(sl("x", "dq10"), u_alt) and np.allclose(sl("x", "dq21"), 15.0)
+    # lambda scaling tree (model_funcs.py:1093-1138): secondary = average force / n_kites / l_s
+    assert sl("z", "lambda10")[0] == pytest.approx(925.0 / 200.0)
+    assert sl("z", "lambda21")[0] == pytest.approx(925.0 / 2 / 50.0)
+    # xdot scaled like its integral variable; secondary tether from solver.initialization.theta
+    assert np.array_equal(sl("xdot", "ddq21"), sl("x", "dq21"))
+    assert (sl("theta", "l_s")[0], sl("theta", "diam_s")[0]) == (50.0, 5e-3)
+    # two kites: power estimate doubles, gravity estimate per kite (model_funcs.py:1010, 1282)
+    single = du.build_constants(du.ap2_single_config(n_k=60))
+    assert det["total_mass"] == pytest.approx(2 * 36.8 + math.pi * 2.5e-3 ** 2 * 200 * cfg.tether_rho
+                                              + 2 * math.pi * 2.5e-3 ** 2 * 50 * cfg.tether_rho)
+    assert mc.consts[du.CONST_IDX["norm_tracking"]] == 60 * 4 and mc.consts[du.CONST_IDX["norm_beta"]] == 60 * 2
+    assert single.consts[du.CONST_IDX["norm_tracking"]] == 60 * 2
+
+
+def test_single_kite_constants_equal_ap2_pipeline():
+    a = du.build_constants(du.ap2_single_config())
+    b = pb.build_constants()
+    assert np.array_equal(a.scaling, b.scaling) and np.array_equal(a.weights, b.weights)
+    assert a.details["energy"] == b.details["energy"] and a.details["f_scaling"] == b.details["f_scaling"]
+
+
+def test_multikite_oracle_reproduces_ap2_oracle():
+    from awebox_amd.initial_guess import batch_member, initial_guess
+    from oracle import ap2_oracle as ao
+    from oracle import multikite_oracle as mo
+    n_k, d = 3, 3
+    c0 = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+    lay0 = pb.NlpLayout(n_k, d)
+    v0 = initial_guess(c0, lay0)
+    V = batch_member(v0, lay0, 1)
+    P = pb.pack_p(lay0, c0, v0, "power1")
+    o0 = ao.from_problem(c0, n_k=n_k, d=d)
+    mc = du.build_constants(du.ap2_single_config(n_k, d))
+    lay1 = du.layout_for(mc)
+    o1 = mo.from_constants(mc, lay1)
+    th = mo.theta0_dict(P[lay0.p_theta0:])
+    assert np.array_equal(o0.nlp_g(V, P, lay0, pb.THETA0_OFF).numpy(), o1.nlp_g(V, P, lay1, th).numpy())
+    assert float(o0.nlp_f(V, P, lay0, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES)) == \
+        float(o1.nlp_f(V, P, lay1, th, pb.COST_NAMES, pb.PHI_NAMES))
+    assert np.array_equal(o0.nlp_grad_f(V, P, lay0, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES).numpy(),
+                          o1.nlp_grad_f(V, P, lay1, th, pb.COST_NAMES, pb.PHI_NAMES).numpy())
+    assert np.array_equal(o0.nlp_jac_g(V, P, lay0, pb.THETA0_OFF).toarray(), o1.nlp_jac_g(V, P, lay1, th))
+
+
+def test_initial_guess_geometry():
+    mc = du.build_constants(du.MultiConfig(n_k=6, d=3))
+    lay = du.layout_for(mc)
+    V0 = du.initial_guess(mc, lay)
+    m = mc.model
+    x = V0[lay.x(0)] * mc.scaling[:m.nx]
+    q10, q21, q31 = x[0:3], x[6:9], x[27:30]
+    assert np.linalg.norm(q10) == pytest.approx(200.0)                      # main tether along n_hat
+    assert np.linalg.norm(q21 - q10) == pytest.approx(50.0)                 # hypotenuse l_s
+    assert np.linalg.norm(q31 - q10) == pytest.approx(50.0)
+    # the two kites are half a revolution apart on the cone (tools.get_azimuthal_angle)
+    c = q10 + 50.0 * math.cos(math.radians(15)) * q10 / 200.0
+    assert np.dot(q21 - c, q31 - c) == pytest.approx(-(50.0 * math.sin(math.radians(15))) ** 2)
+    assert V0[lay.theta_index("t_f0")] == V0[lay.theta_index("t_f1")]
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from awebox_amd.build import LIB_DUAL, build_one
+    build_one(LIB_DUAL)
+    from awebox_amd.dual_evaluator import load_library
+    return load_library()
+
+
+def test_exports_every_header_symbol(lib):
+    from awebox_amd.build import LIB_DUAL
+    from awebox_amd.dual_evaluator import EXPORTED_SYMBOLS
+    declared = set(re.findall(r"^(?:int|const char\*)\s+(adl_\w+)\(", open(HEADER).read(), re.M))
+    assert declared <= set(EXPORTED_SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_DUAL], capture_output=True, text=True, check=True).stdout
+    assert set(EXPORTED_SYMBOLS) <= set(re.findall(r"\bT (adl_\w+)", out))
+
+
+def _small():
+    from oracle import multikite_oracle as mo
+    mc = du.build_constants(du.MultiConfig(n_k=5, d=3))
+    lay = du.layout_for(mc)
+    V0 = du.initial_guess(mc, lay)
+    P = du.pack_p(lay, mc, V0, "power1")
+    return mc, lay, V0, P, mo.from_constants(mc, lay), mo.theta0_dict(P[lay.p_theta0:])
+
+
+@pytest.mark.parametrize("member,k", [(0, 0), (3, 1), (5, 4)])
+def test_model_source_matches_oracle_at_node_level(lib, member, k):
+    """dual_node (the HIP model source, compiled for the host) against torch.func derivatives of
+    the oracle's Lagrangian, values and the full 75 x 127 node Jacobian."""
+    from awebox_amd.dual_evaluator import node_eval_host
+    mc, lay, V0, P, o, th = _small()
+    V = du.batch_member(V0, lay, member)
+    w = np.concatenate([V[lay.x(k)], V[lay.xdot(k)], V[lay.u(k)], V[lay.z(k)], V[lay.node_theta_index(k)],
+                        [V[lay.phi()[0]]]])
+    val, jac = node_eval_host(w, P[lay.p_theta0:], mc)
+
+    def nodef(wg):
+        eq, ineq, p, b = o.node(wg[:126], wg[126], th)
+        return torch.cat([eq, ineq, p.reshape(1), b])
+
+    wt = torch.as_tensor(w)
+    ref = nodef(wt).numpy()
+    J = jacfwd(nodef)(wt).numpy()
+    assert np.all(np.abs(val - ref) <= 1e-12 * np.maximum(1.0, np.abs(ref)))
+    scale = np.maximum(np.abs(J).max(axis=1, keepdims=True), 1e-300)
+    assert np.all(np.abs(jac - J) <= 1e-12 * scale)
+
+
+def test_static_sparsity_covers_oracle_pattern(lib):
+    import scipy.sparse as sp
+    from awebox_amd.dual_evaluator import colour_counts, sparsity_jac_static
+    mc, lay, V0, P, o, th = _small()
+    colind, row = sparsity_jac_static(mc)
+    assert colind[-1] == row.size and np.all(np.diff(colind) >= 0)
+    for c in range(lay.n_v):
+        assert np.all(np.diff(row[colind[c]:colind[c + 1]]) > 0)
+    J = o.nlp_jac_g(du.batch_member(V0, lay, 2), P, lay, th)
+    pat = sp.csc_matrix((np.ones(row.size), row, colind), shape=J.shape).toarray() != 0
+    assert not np.any((J != 0) & ~pat), "oracle non-zero outside the evaluator's CCS pattern"
+    n0, n1, t0, t1 = colour_counts(mc)
+    assert n0 <= 64 and n1 <= 64          # one wavefront per node
