@@ -123,8 +123,50 @@ struct DSink {
     __device__ __forceinline__ void beta(int k, const awe::Dual& v) { emit(kRowBeta0 + k, v); }
 };
 
+// Preaccumulated sub-model layout per node: main drag [3 values | 3 x 7 partials], then per kite
+// the secondary drag [6 values (up, lo) | 6 x 13 partials]; partials w.r.t. the SI inputs
+// (q10, dq10, diam_t) and (q10, dq10, q_k, dq_k, diam_s).
+constexpr int kPreMain = 3 + 3 * 7;
+constexpr int kPreSec = 6 + 6 * 13;
+constexpr int kPreStride = kPreMain + 2 * kPreSec;    // 192
+constexpr int kPreThreads = 7 + 2 * 13;               // one input direction per thread
+
+struct DualPreSubmodels {
+    const double* pre;   // this node's block
+    template <class T>
+    __device__ __forceinline__ void kite_atmosphere(const T& qz, const double* th, T& uw, T& rho) const {
+        uw = awe::wind_speed(qz, th);
+        rho = awe::isa_density(qz, th);
+    }
+    __device__ __forceinline__ void main_drag(const awe::Dual* q, const awe::Dual* v, const awe::Dual& diam,
+                                              const double*, const double*, awe::Dual up[3]) const {
+        const double t[7] = {q[0].d, q[1].d, q[2].d, v[0].d, v[1].d, v[2].d, diam.d};
+        for (int i = 0; i < 3; ++i) {
+            double d = 0.0;
+            for (int j = 0; j < 7; ++j) d += pre[3 + i * 7 + j] * t[j];
+            up[i] = awe::Dual(pre[i], d);
+        }
+    }
+    __device__ __forceinline__ void sec_drag(int k, const awe::Dual* qb, const awe::Dual* vb, const awe::Dual* qt,
+                                             const awe::Dual* vt, const awe::Dual& diam, const double*, const double*,
+                                             awe::Dual up[3], awe::Dual lo[3]) const {
+        const double* p = pre + kPreMain + k * kPreSec;
+        const double t[13] = {qb[0].d, qb[1].d, qb[2].d, vb[0].d, vb[1].d, vb[2].d, qt[0].d, qt[1].d, qt[2].d,
+                              vt[0].d, vt[1].d, vt[2].d, diam.d};
+        for (int i = 0; i < 6; ++i) {
+            double d = 0.0;
+            for (int j = 0; j < 13; ++j) d += p[6 + i * 13 + j] * t[j];
+            (i < 3 ? up[i] : lo[i - 3]) = awe::Dual(p[i], d);
+        }
+    }
+};
+
+#ifndef ADL_MIN_BLOCKS
+#define ADL_MIN_BLOCKS 1    // __launch_bounds__ minimum waves per SIMD
+#endif
+
 template <int D>
-__global__ __launch_bounds__(64 * (D + 1)) void dual_interval_kernel(DArgs a) {
+__global__ __launch_bounds__(64 * (D + 1), ADL_MIN_BLOCKS) void dual_interval_kernel(DArgs a) {
     constexpr int NN = D + 1;
     constexpr int NT = 64 * NN;
     constexpr int STRIDE = 2 * ADL_NX + ADL_NU + ADL_NZ + D * (ADL_NX + ADL_NZ);
@@ -140,6 +182,7 @@ __global__ __launch_bounds__(64 * (D + 1)) void dual_interval_kernel(DArgs a) {
     __shared__ double fterm[D][128];
     __shared__ double dumpbuf[NT];
     __shared__ int8_t colb[2][128];
+    __shared__ double pre[NN][kPreStride];      // preaccumulated tether drags
     extern __shared__ double tang[];            // [tang_total]
 
     const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
@@ -232,6 +275,48 @@ __global__ __launch_bounds__(64 * (D + 1)) void dual_interval_kernel(DArgs a) {
     }
     __syncthreads();
 
+    // ---- tether drags once per node, one SI input direction per thread ------------------------
+    {
+        const double* sc = a.cst + ADL_C_SCALING;
+        const awe::DualInlineSubmodels inl;
+        for (int t = tid; t < NN * kPreThreads; t += NT) {
+            const int n = t / kPreThreads, j = t % kPreThreads;
+            const double* wv = wn[n];
+            auto S = [&](int i, int seed) { return awe::Dual(wv[i] * sc[i], seed ? 1.0 : 0.0); };
+            awe::Dual q1[3], v1[3];
+            if (j < 7) {
+                for (int i = 0; i < 3; ++i) {
+                    q1[i] = S(awe::dl::kQ10 + i, j == i);
+                    v1[i] = S(awe::dl::kDQ10 + i, j == 3 + i);
+                }
+                awe::Dual up[3];
+                inl.main_drag(q1, v1, S(awe::dl::kDiamT, j == 6), th, a.cst, up);
+                for (int i = 0; i < 3; ++i) {
+                    pre[n][3 + i * 7 + j] = up[i].d;
+                    if (j == 0) pre[n][i] = up[i].v;
+                }
+            } else {
+                const int k = (j - 7) / 13, jj = (j - 7) % 13;
+                awe::Dual qk[3], vk[3];
+                for (int i = 0; i < 3; ++i) {
+                    q1[i] = S(awe::dl::kQ10 + i, jj == i);
+                    v1[i] = S(awe::dl::kDQ10 + i, jj == 3 + i);
+                    qk[i] = S(awe::dl::q(k) + i, jj == 6 + i);
+                    vk[i] = S(awe::dl::dq(k) + i, jj == 9 + i);
+                }
+                awe::Dual up[3], lo[3];
+                inl.sec_drag(k, q1, v1, qk, vk, S(awe::dl::kDiamS, jj == 12), th, a.cst, up, lo);
+                double* p = pre[n] + kPreMain + k * kPreSec;
+                for (int i = 0; i < 6; ++i) {
+                    const awe::Dual& o = i < 3 ? up[i] : lo[i - 3];
+                    p[6 + i * 13 + jj] = o.d;
+                    if (jj == 0) p[i] = o.v;
+                }
+            }
+        }
+    }
+    __syncthreads();
+
     // ---- model pass: wave = node, lane = colour ------------------------------------------
     {
         const int n = tid >> 6, lane = tid & 63;
@@ -243,7 +328,7 @@ __global__ __launch_bounds__(64 * (D + 1)) void dual_interval_kernel(DArgs a) {
             DSink sink{tang + toff + a.ct->off[kind][lane], gval[n], &dumpbuf[tid], a.ct->cm_lo[kind][lane],
                        a.ct->cm_hi[kind][lane], lane == 0};
             awe::Dual gamma(wn[n][126], colb[kind][126] == lane ? 1.0 : 0.0);
-            awe::dual_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0);
+            awe::dual_node<awe::Dual>(in, gamma, th, a.cst, sink, n == 0, DualPreSubmodels{pre[n]});
         }
     }
     __syncthreads();

@@ -94,6 +94,10 @@ AWE_HD double element_upper_share(int e, int n_el) {
     return (e == n_el - 1) ? (1.0 - 0.5 * ds) : (s0 + e * step);
 }
 
+// Sub-models that depend on few node variables: the kite-height wind and density (on q_kz), the
+// main-tether drag (on q10, dq10, diam_t: 7 inputs) and each secondary-tether drag (on q10, dq10,
+// q_k, dq_k, diam_s: 13 inputs).  The default provider evaluates them inline; the GPU kernel
+// substitutes one that returns values and partial derivatives preaccumulated once per node.
 struct DualInlineSubmodels {
     template <class T>
     AWE_HD void kite_atmosphere(const T& qz, const double* th, T& uw, T& rho) const {
@@ -116,8 +120,8 @@ struct DualInlineSubmodels {
     }
     // secondary tether node 1 -> kite: upper share to the kite, lower share to node 1
     template <class T>
-    AWE_HD void sec_drag(const T* qb, const T* vb, const T* qt, const T* vt, const T& diam, const double* th,
-                         const double* cst, T up[3], T lo[3]) const {
+    AWE_HD void sec_drag(int /*k*/, const T* qb, const T* vb, const T* qt, const T* vt, const T& diam,
+                         const double* th, const double* cst, T up[3], T lo[3]) const {
         const int n_el = (int)cst[ADL_C_N_ELEMENTS];
         for (int i = 0; i < 3; ++i) { up[i] = T(0.0); lo[i] = T(0.0); }
         for (int e = 0; e < n_el; ++e) {
@@ -133,6 +137,12 @@ struct DualInlineSubmodels {
 };
 
 // Sink protocol: eq_row(r, v) r < ADL_N_EQ, ineq_row(r, v) r < ADL_N_INEQ, power(v), beta(k, v).
+//
+// Phases are ordered so that no per-kite state outlives its kite: each kite's DCM, aerodynamics,
+// rotation, path rows and then its secondary tether segment (drag, Lagrange terms, translation
+// and holonomic rows) are evaluated in one loop body; only the node-1 accumulator (3 values)
+// crosses iterations.  Inputs are re-read through `in` where they are needed, keeping the
+// dual-number working set of one lane small.
 template <class T, class In, class Sink, class Sub = DualInlineSubmodels>
 AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const double* cst, Sink& out,
                       bool want_ineq, const Sub& sub = Sub()) {
@@ -140,9 +150,16 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
     const double* s = cst + ADL_C_SCALING;
     auto SI = [&](int i) -> T { return in(i) * s[i]; };
     const double pi = 3.14159265358979323846;
+    const double g_grav = th[AWE_TH_G];
+    const double m_k = th[AWE_TH_M_K];
+    const double rho_t = th[AWE_TH_RHO_TETHER];
+    const double kap = th[AWE_TH_KAPPA];
+    const double gs10 = cst[ADL_C_G_SCALING] * 10.0;
+    const double sm_s = pi * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * rho_t *
+                        cst[ADL_C_SCALING_LENGTH_S];
 
-    T Fk[2][3];     // per kite: gamma f_fict + aerodynamic force (earth frame)
-#pragma unroll
+    T acc1[3] = {T(0.0), T(0.0), T(0.0)};   // node 1: secondary-segment Lagrange terms - lower drag shares
+#pragma unroll 1
     for (int k = 0; k < 2; ++k) {
         // ---- DCM kinematics with orthonormality Baumgarte (lagr_dyn.py:236-254) ----------
         {
@@ -166,109 +183,165 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
             }
         }
         // ---- kite aerodynamics (kite_aero.py:63-117, six_dof_kite.py:165-201) -----------
-        T ua[3], ua_e1, ua_e2, ua_e3, uu, airspeed, rho_k;
+        T Fa[3];     // gamma f_fict + aerodynamic force, earth frame (forces.py:148-171)
         {
-            T uw;
-            sub.kite_atmosphere(SI(q(k) + 2), th, uw, rho_k);
-            ua[0] = uw - SI(dq(k));
-            ua[1] = -SI(dq(k) + 1);
-            ua[2] = -SI(dq(k) + 2);
-        }
-        ua_e1 = ua[0] * SI(r(k)) + ua[1] * SI(r(k) + 1) + ua[2] * SI(r(k) + 2);
-        ua_e2 = ua[0] * SI(r(k) + 3) + ua[1] * SI(r(k) + 4) + ua[2] * SI(r(k) + 5);
-        ua_e3 = ua[0] * SI(r(k) + 6) + ua[1] * SI(r(k) + 7) + ua[2] * SI(r(k) + 8);
-        uu = dot3(ua, ua);
-        airspeed = sqrt(uu);
-        T x_comp = sqrt(ua_e1 * ua_e1 + 1e-16);
-        T alpha = ua_e3 / x_comp;
-        T beta = ua_e2 / x_comp;
-        const double b_ref = th[AWE_TH_B_REF], c_ref = th[AWE_TH_C_REF], s_ref = th[AWE_TH_S_REF];
-        T coeff[6];
-        {
-            T inv2a = 1.0 / (2.0 * airspeed);
-            const double* sd = th + AWE_TH_STAB_DERIVS;
-            const double* sdl = cst + ADL_C_SD_LEN;
-            const double mf = th[AWE_TH_MOMENT_FACTOR];
-            T alpha2 = alpha * alpha;
-            for (int c = 0; c < 6; ++c) coeff[c] = T(0.0);
-            for (int i = 0; i < 9; ++i) {
-                T inp;
-                switch (i) {
-                    case 0: inp = T(1.0); break;
-                    case 1: inp = alpha; break;
-                    case 2: inp = -beta; break;
-                    case 3: inp = (-SI(om(k))) * inv2a * b_ref; break;
-                    case 4: inp = SI(om(k) + 1) * inv2a * c_ref; break;
-                    case 5: inp = (-SI(om(k) + 2)) * inv2a * b_ref; break;
-                    default: inp = SI(del(k) + i - 6); break;
-                }
-                T ia = inp * alpha, ia2 = inp * alpha2;
-                for (int c = 0; c < 6; ++c) {
-                    const int n = (int)sdl[c * 9 + i];
-                    if (n == 0) continue;
-                    const double* dv = sd + (c * 9 + i) * 3;
-                    T contrib = dv[0] * inp;
-                    if (n > 1) contrib = contrib + dv[1] * ia;
-                    if (n > 2) contrib = contrib + dv[2] * ia2;
-                    const double wgt = (c >= 3 && i >= 6) ? mf : 1.0;
-                    coeff[c] = coeff[c] + wgt * contrib;
+            T ua[3], ua_e1, ua_e2, ua_e3, uu, airspeed, rho_k;
+            {
+                T uw;
+                sub.kite_atmosphere(SI(q(k) + 2), th, uw, rho_k);
+                ua[0] = uw - SI(dq(k));
+                ua[1] = -SI(dq(k) + 1);
+                ua[2] = -SI(dq(k) + 2);
+            }
+            ua_e1 = ua[0] * SI(r(k)) + ua[1] * SI(r(k) + 1) + ua[2] * SI(r(k) + 2);
+            ua_e2 = ua[0] * SI(r(k) + 3) + ua[1] * SI(r(k) + 4) + ua[2] * SI(r(k) + 5);
+            ua_e3 = ua[0] * SI(r(k) + 6) + ua[1] * SI(r(k) + 7) + ua[2] * SI(r(k) + 8);
+            uu = dot3(ua, ua);
+            airspeed = sqrt(uu);
+            T x_comp = sqrt(ua_e1 * ua_e1 + 1e-16);
+            T alpha = ua_e3 / x_comp;
+            T beta = ua_e2 / x_comp;
+            const double b_ref = th[AWE_TH_B_REF], c_ref = th[AWE_TH_C_REF], s_ref = th[AWE_TH_S_REF];
+            T coeff[6];
+            {
+                T inv2a = 1.0 / (2.0 * airspeed);
+                const double* sd = th + AWE_TH_STAB_DERIVS;
+                const double* sdl = cst + ADL_C_SD_LEN;
+                const double mf = th[AWE_TH_MOMENT_FACTOR];
+                T alpha2 = alpha * alpha;
+                for (int c = 0; c < 6; ++c) coeff[c] = T(0.0);
+                for (int i = 0; i < 9; ++i) {
+                    T inp;
+                    switch (i) {
+                        case 0: inp = T(1.0); break;
+                        case 1: inp = alpha; break;
+                        case 2: inp = -beta; break;
+                        case 3: inp = (-SI(om(k))) * inv2a * b_ref; break;
+                        case 4: inp = SI(om(k) + 1) * inv2a * c_ref; break;
+                        case 5: inp = (-SI(om(k) + 2)) * inv2a * b_ref; break;
+                        default: inp = SI(del(k) + i - 6); break;
+                    }
+                    T ia = inp * alpha, ia2 = inp * alpha2;
+                    for (int c = 0; c < 6; ++c) {
+                        const int n = (int)sdl[c * 9 + i];
+                        if (n == 0) continue;
+                        const double* dv = sd + (c * 9 + i) * 3;
+                        T contrib = dv[0] * inp;
+                        if (n > 1) contrib = contrib + dv[1] * ia;
+                        if (n > 2) contrib = contrib + dv[2] * ia2;
+                        const double wgt = (c >= 3 && i >= 6) ? mf : 1.0;
+                        coeff[c] = coeff[c] + wgt * contrib;
+                    }
                 }
             }
+            T qs = (0.5 * rho_k * uu) * s_ref;
+            {
+                T fc0 = -(coeff[0] * qs), fc1 = coeff[1] * qs, fc2 = -(coeff[2] * qs);
+                for (int i = 0; i < 3; ++i)
+                    Fa[i] = gamma * SI(ffict(k) + i) +
+                            (SI(r(k) + i) * fc0 + SI(r(k) + 3 + i) * fc1 + SI(r(k) + 6 + i) * fc2);
+            }
+            // ---- rotational dynamics (lagr_dyn.py:207-234) ---------------------------------
+            {
+                T M_body[3];
+                M_body[0] = -(qs * (b_ref * coeff[3]));
+                M_body[1] = qs * (c_ref * coeff[4]);
+                M_body[2] = -(qs * (b_ref * coeff[5]));
+                const double* J = th + AWE_TH_J;
+                T w[3], Jw[3];
+                for (int i = 0; i < 3; ++i) w[i] = SI(om(k) + i);
+                for (int i = 0; i < 3; ++i) Jw[i] = J[i] * w[0] + J[3 + i] * w[1] + J[6 + i] * w[2];
+                T wxJw[3];
+                wxJw[0] = w[1] * Jw[2] - w[2] * Jw[1];
+                wxJw[1] = -(w[0] * Jw[2] - w[2] * Jw[0]);
+                wxJw[2] = w[0] * Jw[1] - w[1] * Jw[0];
+                const double inv_ms = 1.0 / cst[ADL_C_M_AERO_SCALING];
+                for (int i = 0; i < 3; ++i) {
+                    const int xw = kXD + om(k);
+                    T Jdw = J[i] * SI(xw) + J[3 + i] * SI(xw + 1) + J[6 + i] * SI(xw + 2);
+                    T M = gamma * SI(mfict(k) + i) + M_body[i];
+                    out.eq_row(row_rot(k) + i, (M - (Jdw + wxJw[i])) * inv_ms);
+                }
+            }
+            // ---- path inequalities of kite k ---------------------------------------------
+            if (want_ineq) {
+                T dd[3];
+                for (int i = 0; i < 3; ++i) dd[i] = SI(q(k) + i) - SI(kQ10 + i);
+                T nd = sqrt(dot3(dd, dd));
+                T tension = SI(lam(k)) * nd;                                   // dynamics.py:706-776
+                const double fscale = s[lam(k)] * cst[ADL_C_SCALING_LENGTH_S];
+                out.ineq_row(irow_force(k), (tension - th[AWE_TH_FORCE_LIMITS + 1]) / fscale);
+                out.ineq_row(irow_force(k) + 1, (th[AWE_TH_FORCE_LIMITS + 0] - tension) / fscale);
+                const double u_ref = th[AWE_TH_U_REF];
+                out.ineq_row(irow_airspeed(k), (airspeed - th[AWE_TH_AIRSPEED_LIMITS + 1]) / u_ref);
+                out.ineq_row(irow_airspeed(k) + 1, (th[AWE_TH_AIRSPEED_LIMITS + 0] - airspeed) / u_ref);
+                const double tight = cst[ADL_C_AERO_TIGHTNESS], aref = cst[ADL_C_AIRSPEED_REF];
+                const double amax = cst[ADL_C_ALPHA_MAX], amin = cst[ADL_C_ALPHA_MIN];
+                const double bmax = cst[ADL_C_BETA_MAX], bmin = cst[ADL_C_BETA_MIN];
+                out.ineq_row(irow_valid(k), (ua_e3 - ua_e1 * amax) * tight / aref / ::sqrt(amax * amax + 1e-16));
+                out.ineq_row(irow_valid(k) + 1, (-ua_e3 + ua_e1 * amin) * tight / aref / ::sqrt(amin * amin + 1e-16));
+                out.ineq_row(irow_valid(k) + 2, (ua_e2 - ua_e1 * bmax) * tight / aref / ::sqrt(bmax * bmax + 1e-16));
+                out.ineq_row(irow_valid(k) + 3, (-ua_e2 + ua_e1 * bmin) * tight / aref / ::sqrt(bmin * bmin + 1e-16));
+                const double cos_gmax = ::cos(th[AWE_TH_ROT_ANGLES + 2]);      // dynamics.py:1022-1052
+                T yaw = (dd[0] * SI(r(k) + 6) + dd[1] * SI(r(k) + 7) + dd[2] * SI(r(k) + 8) - cos_gmax * nd) /
+                        cst[ADL_C_SCALING_LENGTH_S];
+                out.ineq_row(irow_yaw(k), -1.0 * yaw);
+            }
+            out.beta(k, beta);
         }
-        T qs = (0.5 * rho_k * uu) * s_ref;
+        // ---- secondary tether segment node 1 -> kite k: drag, Lagrange terms, rows ---------
         {
-            T fc0 = -(coeff[0] * qs), fc1 = coeff[1] * qs, fc2 = -(coeff[2] * qs);
-            for (int i = 0; i < 3; ++i)
-                Fk[k][i] = gamma * SI(ffict(k) + i) +
-                           (SI(r(k) + i) * fc0 + SI(r(k) + 3 + i) * fc1 + SI(r(k) + 6 + i) * fc2);
-        }
-        // ---- rotational dynamics (lagr_dyn.py:207-234) -----------------------------------
-        {
-            T M_body[3];
-            M_body[0] = -(qs * (b_ref * coeff[3]));
-            M_body[1] = qs * (c_ref * coeff[4]);
-            M_body[2] = -(qs * (b_ref * coeff[5]));
-            const double* J = th + AWE_TH_J;
-            T w[3], Jw[3];
-            for (int i = 0; i < 3; ++i) w[i] = SI(om(k) + i);
-            for (int i = 0; i < 3; ++i) Jw[i] = J[i] * w[0] + J[3 + i] * w[1] + J[6 + i] * w[2];
-            T wxJw[3];
-            wxJw[0] = w[1] * Jw[2] - w[2] * Jw[1];
-            wxJw[1] = -(w[0] * Jw[2] - w[2] * Jw[0]);
-            wxJw[2] = w[0] * Jw[1] - w[1] * Jw[0];
-            const double inv_ms = 1.0 / cst[ADL_C_M_AERO_SCALING];
+            T q1[3], v1[3], qk[3], vk[3];
             for (int i = 0; i < 3; ++i) {
-                const int xw = kXD + om(k);
-                T Jdw = J[i] * SI(xw) + J[3 + i] * SI(xw + 1) + J[6 + i] * SI(xw + 2);
-                T M = gamma * SI(mfict(k) + i) + M_body[i];
-                out.eq_row(row_rot(k) + i, (M - (Jdw + wxJw[i])) * inv_ms);
+                q1[i] = SI(kQ10 + i);
+                v1[i] = SI(kDQ10 + i);
+                qk[i] = SI(q(k) + i);
+                vk[i] = SI(dq(k) + i);
             }
+            T diam = SI(kDiamS);
+            T up[3], lo[3];
+            sub.sec_drag(k, q1, v1, qk, vk, diam, th, cst, up, lo);
+            T d[3], wv[3];
+            for (int i = 0; i < 3; ++i) {
+                d[i] = qk[i] - q1[i];
+                wv[i] = vk[i] - v1[i];
+            }
+            T dd = dot3(d, d);
+            T L = sqrt(dd);
+            T invL = 1.0 / L;
+            T mu = (pi * (diam / 2.0) * (diam / 2.0)) * rho_t;
+            T m = mu * L;
+            T mdot6 = (mu * dot3(d, wv) * invL) / 6.0;
+            T m6 = m / 6.0;
+            T S = dot3(vk, vk) + dot3(v1, v1) + dot3(vk, v1);
+            T ge = g_grav * mu * (qk[2] + q1[2]) * 0.5 * invL;   // coefficient of d in dV/dq_k
+            T te = (mu / 6.0) * S * invL;                         // coefficient of d in dT/dq_k
+            T lamk = SI(lam(k));
+            T gm2 = g_grav * m * 0.5;
+            const double inv_fs = 1.0 / ((sm_s / 2.0 + m_k) * gs10);
+            T c2a(0.0);
+            for (int i = 0; i < 3; ++i) {
+                T ak = SI(kXD + dq(k) + i), a1 = SI(kDDQ10 + i);
+                c2a = c2a + d[i] * (ak - a1);
+                T common = (ge - te + lamk) * d[i];
+                T lk = m_k * ak + mdot6 * (2.0 * vk[i] + v1[i]) + m6 * (2.0 * ak + a1) + common;
+                T l1 = mdot6 * (2.0 * v1[i] + vk[i]) + m6 * (2.0 * a1 + ak) - common;
+                if (i == 2) {
+                    lk = lk + gm2 + g_grav * m_k;
+                    l1 = l1 + gm2;
+                }
+                acc1[i] = acc1[i] + (l1 - lo[i]);
+                out.eq_row(row_trans(k) + i, (lk - (Fa[i] + up[i])) * inv_fs);
+            }
+            // holonomic constraint of the secondary tether, l_s constant (theta)
+            T ls = SI(kLs);
+            T c0 = 0.5 * (dd - ls * ls);
+            T c1 = dot3(d, wv);
+            T c2 = dot3(wv, wv) + c2a;
+            const double hscale =
+                kap * kap * (cst[ADL_C_SCALING_LENGTH_S] * ((s[q(k)] + s[q(k) + 1] + s[q(k) + 2]) / 3.0));
+            out.eq_row(row_hol(k), (c2 + 2.0 * kap * c1 + kap * kap * c0) / hscale);
         }
-        // ---- path inequalities of kite k -----------------------------------------------
-        if (want_ineq) {
-            T dd[3];
-            for (int i = 0; i < 3; ++i) dd[i] = SI(q(k) + i) - SI(kQ10 + i);
-            T nd = sqrt(dot3(dd, dd));
-            T tension = SI(lam(k)) * nd;                                   // dynamics.py:706-776
-            const double fscale = s[lam(k)] * cst[ADL_C_SCALING_LENGTH_S];
-            out.ineq_row(irow_force(k), (tension - th[AWE_TH_FORCE_LIMITS + 1]) / fscale);
-            out.ineq_row(irow_force(k) + 1, (th[AWE_TH_FORCE_LIMITS + 0] - tension) / fscale);
-            const double u_ref = th[AWE_TH_U_REF];
-            out.ineq_row(irow_airspeed(k), (airspeed - th[AWE_TH_AIRSPEED_LIMITS + 1]) / u_ref);
-            out.ineq_row(irow_airspeed(k) + 1, (th[AWE_TH_AIRSPEED_LIMITS + 0] - airspeed) / u_ref);
-            const double tight = cst[ADL_C_AERO_TIGHTNESS], aref = cst[ADL_C_AIRSPEED_REF];
-            const double amax = cst[ADL_C_ALPHA_MAX], amin = cst[ADL_C_ALPHA_MIN];
-            const double bmax = cst[ADL_C_BETA_MAX], bmin = cst[ADL_C_BETA_MIN];
-            out.ineq_row(irow_valid(k), (ua_e3 - ua_e1 * amax) * tight / aref / ::sqrt(amax * amax + 1e-16));
-            out.ineq_row(irow_valid(k) + 1, (-ua_e3 + ua_e1 * amin) * tight / aref / ::sqrt(amin * amin + 1e-16));
-            out.ineq_row(irow_valid(k) + 2, (ua_e2 - ua_e1 * bmax) * tight / aref / ::sqrt(bmax * bmax + 1e-16));
-            out.ineq_row(irow_valid(k) + 3, (-ua_e2 + ua_e1 * bmin) * tight / aref / ::sqrt(bmin * bmin + 1e-16));
-            const double cos_gmax = ::cos(th[AWE_TH_ROT_ANGLES + 2]);      // dynamics.py:1022-1052
-            T yaw = (dd[0] * SI(r(k) + 6) + dd[1] * SI(r(k) + 7) + dd[2] * SI(r(k) + 8) - cos_gmax * nd) /
-                    cst[ADL_C_SCALING_LENGTH_S];
-            out.ineq_row(irow_yaw(k), -1.0 * yaw);
-        }
-        out.beta(k, beta);
     }
 
     // ---- trivial kinematics, sorted names (lagr_dyn.py:141-169) -------------------------
@@ -293,26 +366,20 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
     }
     out.power(SI(kLam10) * SI(kLT) * SI(kDLT) / cst[ADL_C_ENERGY_SCALING]);
 
-    // ---- translational Lagrangian dynamics + holonomic constraints -----------------------
-    const double g_grav = th[AWE_TH_G];
-    const double m_k = th[AWE_TH_M_K];
-    const double rho_t = th[AWE_TH_RHO_TETHER];
-    const double kap = th[AWE_TH_KAPPA];
-    const double sm_t = pi * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * rho_t *
-                        cst[ADL_C_SCALING_LENGTH_T];
-    const double sm_s = pi * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * rho_t *
-                        cst[ADL_C_SCALING_LENGTH_S];
-    const double gs10 = cst[ADL_C_G_SCALING] * 10.0;
-    T q1[3], v1[3], a1[3];
-    for (int i = 0; i < 3; ++i) {
-        q1[i] = SI(kQ10 + i);
-        v1[i] = SI(kDQ10 + i);
-        a1[i] = SI(kDDQ10 + i);
-    }
-    T lhs1[3], F1[3];
-    {   // main tether segment (energy.py:59-97) and its drag (upper share only)
+    // ---- main tether segment (energy.py:59-97), node-1 translation, main holonomic --------
+    {
+        const double sm_t = pi * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * rho_t *
+                            cst[ADL_C_SCALING_LENGTH_T];
+        const double inv_fs1 = 1.0 / ((sm_t / 2.0 + 2.0 * (sm_s / 2.0)) * gs10);   // mass.py:62-93
+        T q1[3], v1[3], a1[3];
+        for (int i = 0; i < 3; ++i) {
+            q1[i] = SI(kQ10 + i);
+            v1[i] = SI(kDQ10 + i);
+            a1[i] = SI(kDDQ10 + i);
+        }
         T diam = SI(kDiamT);
-        sub.main_drag(q1, v1, diam, th, cst, F1);
+        T F1[3];
+        sub.main_drag(q1, v1, diam, th, cst, F1);                  // upper share only
         T qq = dot3(q1, q1);
         T nq = sqrt(qq);
         T mu = (pi * (diam / 2.0) * (diam / 2.0)) * rho_t;
@@ -331,70 +398,18 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
         for (int i = 0; i < 3; ++i) {
             T ddt = cv * v1[i] + cq * q1[i] + ca * a1[i];
             T dLdq = kq * q1[i] + kv * v1[i] - pq * q1[i] - lam1 * q1[i];
-            lhs1[i] = ddt - dLdq - mass_flow * v1[i];
+            T lhs = ddt - dLdq - mass_flow * v1[i];
+            if (i == 2) lhs = lhs + g_grav * mu * nq * 0.5;
+            out.eq_row(kRowTrans1 + i, ((lhs - F1[i]) + acc1[i]) * inv_fs1);
         }
-        lhs1[2] = lhs1[2] + g_grav * mu * nq * 0.5;
         // holonomic constraint of the main tether (holonomics.py:204-312)
         T l_t = SI(kLT), dl_t = SI(kDLT), ldd = SI(kDDLT_U);
         T c0 = 0.5 * (qq - l_t * l_t);
         T c1 = sv - l_t * dl_t;
         T c2 = vv + qa - dl_t * dl_t - l_t * ldd;
-        const double hscale = kap * kap * (cst[ADL_C_SCALING_LENGTH_T] * ((s[kQ10] + s[kQ10 + 1] + s[kQ10 + 2]) / 3.0));
+        const double hscale =
+            kap * kap * (cst[ADL_C_SCALING_LENGTH_T] * ((s[kQ10] + s[kQ10 + 1] + s[kQ10 + 2]) / 3.0));
         out.eq_row(kRowHol1, (c2 + 2.0 * kap * c1 + kap * kap * c0) / hscale);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {   // secondary tether segment node 1 -> kite k
-        T qk[3], vk[3], ak[3];
-        for (int i = 0; i < 3; ++i) {
-            qk[i] = SI(q(k) + i);
-            vk[i] = SI(dq(k) + i);
-            ak[i] = SI(kXD + dq(k) + i);
-        }
-        T diam = SI(kDiamS);
-        T up[3], lo[3];
-        sub.sec_drag(q1, v1, qk, vk, diam, th, cst, up, lo);
-        T d[3], wv[3];
-        for (int i = 0; i < 3; ++i) {
-            d[i] = qk[i] - q1[i];
-            wv[i] = vk[i] - v1[i];
-        }
-        T dd = dot3(d, d);
-        T L = sqrt(dd);
-        T invL = 1.0 / L;
-        T mu = (pi * (diam / 2.0) * (diam / 2.0)) * rho_t;
-        T m = mu * L;
-        T mdot6 = (mu * dot3(d, wv) * invL) / 6.0;
-        T m6 = m / 6.0;
-        T S = dot3(vk, vk) + dot3(v1, v1) + dot3(vk, v1);
-        T zsum = qk[2] + q1[2];
-        T ge = g_grav * mu * zsum * 0.5 * invL;          // coefficient of d in dV/dq_k
-        T te = (mu / 6.0) * S * invL;                    // coefficient of d in dT/dq_k
-        T lamk = SI(lam(k));
-        T gm2 = g_grav * m * 0.5;
-        const double inv_fs = 1.0 / ((sm_s / 2.0 + m_k) * gs10);
-        for (int i = 0; i < 3; ++i) {
-            T common = (ge - te + lamk) * d[i];
-            T lk = m_k * ak[i] + mdot6 * (2.0 * vk[i] + v1[i]) + m6 * (2.0 * ak[i] + a1[i]) + common;
-            T l1 = mdot6 * (2.0 * v1[i] + vk[i]) + m6 * (2.0 * a1[i] + ak[i]) - common;
-            if (i == 2) {
-                lk = lk + gm2 + g_grav * m_k;
-                l1 = l1 + gm2;
-            }
-            lhs1[i] = lhs1[i] + l1;
-            F1[i] = F1[i] + lo[i];
-            out.eq_row(row_trans(k) + i, (lk - (Fk[k][i] + up[i])) * inv_fs);
-        }
-        // holonomic constraint of the secondary tether, l_s constant (theta)
-        T ls = SI(kLs);
-        T c0 = 0.5 * (dd - ls * ls);
-        T c1 = dot3(d, wv);
-        T c2 = dot3(wv, wv) + (d[0] * (ak[0] - a1[0]) + d[1] * (ak[1] - a1[1]) + d[2] * (ak[2] - a1[2]));
-        const double hscale = kap * kap * (cst[ADL_C_SCALING_LENGTH_S] * ((s[q(k)] + s[q(k) + 1] + s[q(k) + 2]) / 3.0));
-        out.eq_row(row_hol(k), (c2 + 2.0 * kap * c1 + kap * kap * c0) / hscale);
-    }
-    {
-        const double inv_fs1 = 1.0 / ((sm_t / 2.0 + 2.0 * (sm_s / 2.0)) * gs10);   // mass.py:62-93
-        for (int i = 0; i < 3; ++i) out.eq_row(kRowTrans1 + i, (lhs1[i] - F1[i]) * inv_fs1);
     }
 }
 
