@@ -131,6 +131,19 @@ constexpr int kPreSec = 6 + 6 * 13;
 constexpr int kPreStride = kPreMain + 2 * kPreSec;    // 192
 constexpr int kPreThreads = 7 + 2 * 13;               // one input direction per thread
 
+// Stage-A atmosphere of every tether element of a node: (uw, d uw/dz, rho, d rho/dz) at the
+// element midpoint height, [segment 0..2][element] (the transcendental part of the drag model).
+constexpr int kMaxElements = 8;
+struct PreAtmosphere {
+    const double* atm;   // this node's block [3][kMaxElements][4]
+    __device__ __forceinline__ void operator()(int seg, int e, const awe::Dual& zz, const double*, awe::Dual& uw,
+                                               awe::Dual& rho) const {
+        const double* p = atm + (seg * kMaxElements + e) * 4;
+        uw = awe::Dual(p[0], p[1] * zz.d);
+        rho = awe::Dual(p[2], p[3] * zz.d);
+    }
+};
+
 struct DualPreSubmodels {
     const double* pre;   // this node's block
     template <class T>
@@ -183,6 +196,7 @@ __global__ __launch_bounds__(64 * (D + 1), ADL_MIN_BLOCKS) void dual_interval_ke
     __shared__ double dumpbuf[NT];
     __shared__ int8_t colb[2][128];
     __shared__ double pre[NN][kPreStride];      // preaccumulated tether drags
+    __shared__ double atmo[NN][3 * kMaxElements * 4];
     extern __shared__ double tang[];            // [tang_total]
 
     const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
@@ -275,13 +289,34 @@ __global__ __launch_bounds__(64 * (D + 1), ADL_MIN_BLOCKS) void dual_interval_ke
     }
     __syncthreads();
 
-    // ---- tether drags once per node, one SI input direction per thread ------------------------
+    // ---- tether drags once per node -------------------------------------------------------
+    // stage A: wind and density (values and height derivatives) at every element midpoint,
+    // one (node, segment, element) per thread
+    const int n_el = (int)a.cst[ADL_C_N_ELEMENTS];
+    {
+        const double* sc = a.cst + ADL_C_SCALING;
+        for (int t = tid; t < NN * 3 * n_el; t += NT) {
+            const int n = t / (3 * n_el), sg = (t / n_el) % 3, e = t % n_el;
+            const double* wv = wn[n];
+            const double qtz = sg == 0 ? wv[awe::dl::kQ10 + 2] * sc[awe::dl::kQ10 + 2]
+                                       : wv[awe::dl::q(sg - 1) + 2] * sc[awe::dl::q(sg - 1) + 2];
+            const double qbz = sg == 0 ? 0.0 : wv[awe::dl::kQ10 + 2] * sc[awe::dl::kQ10 + 2];
+            const double zz = awe::element_height(e, n_el, qbz, qtz);
+            const awe::Dual z(zz, 1.0);
+            const awe::Dual uw = awe::wind_speed(z, th), rho = awe::isa_density(z, th);
+            double* p = &atmo[n][(sg * kMaxElements + e) * 4];
+            p[0] = uw.v; p[1] = uw.d; p[2] = rho.v; p[3] = rho.d;
+        }
+    }
+    __syncthreads();
+    // stage B: element algebra in dual arithmetic, one SI input direction per thread
     {
         const double* sc = a.cst + ADL_C_SCALING;
         const awe::DualInlineSubmodels inl;
         for (int t = tid; t < NN * kPreThreads; t += NT) {
             const int n = t / kPreThreads, j = t % kPreThreads;
             const double* wv = wn[n];
+            const PreAtmosphere atm{atmo[n]};
             auto S = [&](int i, int seed) { return awe::Dual(wv[i] * sc[i], seed ? 1.0 : 0.0); };
             awe::Dual q1[3], v1[3];
             if (j < 7) {
@@ -290,7 +325,7 @@ __global__ __launch_bounds__(64 * (D + 1), ADL_MIN_BLOCKS) void dual_interval_ke
                     v1[i] = S(awe::dl::kDQ10 + i, j == 3 + i);
                 }
                 awe::Dual up[3];
-                inl.main_drag(q1, v1, S(awe::dl::kDiamT, j == 6), th, a.cst, up);
+                inl.main_drag(q1, v1, S(awe::dl::kDiamT, j == 6), th, a.cst, up, atm);
                 for (int i = 0; i < 3; ++i) {
                     pre[n][3 + i * 7 + j] = up[i].d;
                     if (j == 0) pre[n][i] = up[i].v;
@@ -305,7 +340,7 @@ __global__ __launch_bounds__(64 * (D + 1), ADL_MIN_BLOCKS) void dual_interval_ke
                     vk[i] = S(awe::dl::dq(k) + i, jj == 9 + i);
                 }
                 awe::Dual up[3], lo[3];
-                inl.sec_drag(k, q1, v1, qk, vk, S(awe::dl::kDiamS, jj == 12), th, a.cst, up, lo);
+                inl.sec_drag(k, q1, v1, qk, vk, S(awe::dl::kDiamS, jj == 12), th, a.cst, up, lo, atm);
                 double* p = pre[n] + kPreMain + k * kPreSec;
                 for (int i = 0; i < 6; ++i) {
                     const awe::Dual& o = i < 3 ? up[i] : lo[i - 3];
@@ -607,6 +642,10 @@ int adl_create(int n_k, int d, const double* consts, int n_consts, int batch, ad
         return fail(AWE_ERR_ARG, err);
     }
     const Tables& T = h->t;
+    if ((int)consts[ADL_C_N_ELEMENTS] > kMaxElements) {
+        delete h;
+        return fail(AWE_ERR_ARG, "the dual-kite kernel supports at most 8 tether elements per segment");
+    }
     if (T.gslot.size() >= (1u << 31) || T.tang_total >= (1 << 21)) {
         delete h;
         return fail(AWE_ERR_ARG, "tables exceed the gather-code range");

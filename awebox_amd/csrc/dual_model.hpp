@@ -58,11 +58,30 @@ constexpr int kIrowAnticollision = 16;
 AWE_HD constexpr int irow_yaw(int k) { return 17 + k; }
 }  // namespace dl
 
-// One element of the 'multi' drag model of a tether segment from (qb, vb) to (qt, vt)
-// (element.py:60-146, segment.py:38-65): the element's drag vector, not yet split.
+// Height of the midpoint of element e of a segment whose end heights are qbz (lower) and qtz
+// (upper) (element.py:125-146): the wind and the air density of the element are taken there.
 template <class T>
-AWE_HD void segment_element_drag(int e, int n_el, const T* qb, const T* qt, const T* vb, const T* vt,
-                                 const T& diam, const double* th, T out[3]) {
+AWE_HD T element_height(int e, int n_el, const T& qbz, const T& qtz) {
+    const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
+    T dqs = qtz - qbz;
+    return ((qbz + dqs * up) + (qbz + dqs * lo)) / 2.0;
+}
+
+// wind speed and density at an element midpoint, evaluated in place
+struct InlineAtmosphere {
+    template <class T>
+    AWE_HD void operator()(int /*seg*/, int /*e*/, const T& zz, const double* th, T& uw, T& rho) const {
+        uw = wind_speed(zz, th);
+        rho = isa_density(zz, th);
+    }
+};
+
+// One element of the 'multi' drag model of a tether segment from (qb, vb) to (qt, vt)
+// (element.py:60-146, segment.py:38-65): the element's drag vector, not yet split.  `seg`
+// (0 main, 1 + k secondary of kite k) and `e` identify the element for the atmosphere provider.
+template <class T, class Atm = InlineAtmosphere>
+AWE_HD void segment_element_drag(int seg, int e, int n_el, const T* qb, const T* qt, const T* vb, const T* vt,
+                                 const T& diam, const double* th, T out[3], const Atm& atm = Atm()) {
     const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
     T qu[3], ql[3], vs[3], tv[3];
     for (int i = 0; i < 3; ++i) {
@@ -72,8 +91,9 @@ AWE_HD void segment_element_drag(int e, int n_el, const T* qb, const T* qt, cons
         vs[i] = (vb[i] + dvs * up) + (vb[i] + dvs * lo);
         tv[i] = qu[i] - ql[i];
     }
-    T zz = (qu[2] + ql[2]) / 2.0;
-    T uw = wind_speed(zz, th), rho = isa_density(zz, th);
+    T zz = element_height(e, n_el, qb[2], qt[2]);
+    T uw, rho;
+    atm(seg, e, zz, th, uw, rho);
     T ue[3];
     ue[0] = uw - vs[0] / 2.0;
     ue[1] = -(vs[1] / 2.0);
@@ -105,28 +125,28 @@ struct DualInlineSubmodels {
         rho = isa_density(qz, th);
     }
     // main tether: ground -> node 1; only the upper share is kept (tether_aero.py:85-95)
-    template <class T>
+    template <class T, class Atm = InlineAtmosphere>
     AWE_HD void main_drag(const T* q, const T* v, const T& diam, const double* th, const double* cst,
-                          T up[3]) const {
+                          T up[3], const Atm& atm = Atm()) const {
         const int n_el = (int)cst[ADL_C_N_ELEMENTS];
         T z3[3] = {T(0.0), T(0.0), T(0.0)};
         for (int i = 0; i < 3; ++i) up[i] = T(0.0);
         for (int e = 0; e < n_el; ++e) {
             T c[3];
-            segment_element_drag(e, n_el, z3, q, z3, v, diam, th, c);
+            segment_element_drag(0, e, n_el, z3, q, z3, v, diam, th, c, atm);
             const double sg = element_upper_share(e, n_el);
             for (int i = 0; i < 3; ++i) up[i] = up[i] + sg * c[i];
         }
     }
     // secondary tether node 1 -> kite: upper share to the kite, lower share to node 1
-    template <class T>
-    AWE_HD void sec_drag(int /*k*/, const T* qb, const T* vb, const T* qt, const T* vt, const T& diam,
-                         const double* th, const double* cst, T up[3], T lo[3]) const {
+    template <class T, class Atm = InlineAtmosphere>
+    AWE_HD void sec_drag(int k, const T* qb, const T* vb, const T* qt, const T* vt, const T& diam,
+                         const double* th, const double* cst, T up[3], T lo[3], const Atm& atm = Atm()) const {
         const int n_el = (int)cst[ADL_C_N_ELEMENTS];
         for (int i = 0; i < 3; ++i) { up[i] = T(0.0); lo[i] = T(0.0); }
         for (int e = 0; e < n_el; ++e) {
             T c[3];
-            segment_element_drag(e, n_el, qb, qt, vb, vt, diam, th, c);
+            segment_element_drag(1 + k, e, n_el, qb, qt, vb, vt, diam, th, c, atm);
             const double sg = element_upper_share(e, n_el);
             for (int i = 0; i < 3; ++i) {
                 up[i] = up[i] + sg * c[i];

@@ -10,7 +10,7 @@ CHILD = r'''
 import sys, time, json, numpy as np, torch
 sys.path.insert(0, ".")
 from awebox_amd import dual_evaluator as de, dual as du
-de._LIB_PATH = sys.argv[1]
+de.load_library(sys.argv[1])
 B = int(sys.argv[2])
 c = du.build_constants(); lay = du.layout_for(c); v0 = du.initial_guess(c, lay)
 ev = de.DualEvaluator(c, batch=B)
