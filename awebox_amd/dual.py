@@ -381,6 +381,10 @@ class MultiLayout:
         self.p_ref, self.p_weights = 0, self.n_v
         self.p_cost, self.p_theta0 = self.n_v + m.nw, self.n_v + m.nw + pb.NCOST
 
+    @property
+    def nx(self):
+        return self.model.nx
+
     def theta_index(self, name):
         return self.theta_names.index(name)
 

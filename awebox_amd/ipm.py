@@ -224,18 +224,19 @@ class StructuredKKT:
         N = ny + m
         self.N, self.dev = N, dev
         n_k, stride, v0, rows = lay.n_k, lay.interval_stride, lay.v_intervals, lay.rows_per_interval
+        nx = getattr(lay, "nx", pb.NX)                          # states per shooting node
         owner = np.full(N, -1, dtype=np.int64)                  # interval of an interior unknown
         for p, v in enumerate(nlp.free):
             if v >= v0:
                 k, o = divmod(v - v0, stride)
-                if k < n_k and o >= pb.NX:
+                if k < n_k and o >= nx:
                     owner[p] = k
         for i, r in enumerate(nlp.ineq):
             owner[n + i] = r // rows
         # interval rows, except the continuity rows: an interval has more rows than interior
         # unknowns (x[k], x[k+1] close the count), so their multipliers join the separators
         rr = np.arange(m)
-        owner[ny + rr] = np.where((rr < n_k * rows) & (rr % rows < rows - pb.NX), rr // rows, -1)
+        owner[ny + rr] = np.where((rr < n_k * rows) & (rr % rows < rows - nx), rr // rows, -1)
         self.owner = owner
         sep = np.where(owner < 0)[0]
         self.nS = len(sep)
