@@ -222,7 +222,8 @@ def optimize(mc: du.MultiConstants, ev, opts=None, device="cuda", v_init=None, v
                     opts=hippo_options(st.label, opts), device=device)
         out = outputs(mc, lay, res.x)
         rec = dict(step=st.label, status=res.status, iterations=res.iterations, f=res.f, kkt_error=res.kkt_error,
-                   constr_viol=res.constr_viol, seconds=time.perf_counter() - t0, **out)
+                   constr_viol=res.constr_viol, seconds=time.perf_counter() - t0, kkt_solves=res.kkt_solves,
+                   kkt_dense=res.kkt_dense, timing={k: round(v, 3) for k, v in res.timing.items()}, **out)
         summary.append(rec)
         if verbose:
             print(rec, flush=True)

@@ -232,7 +232,7 @@ class StructuredKKT:
                 if k < n_k and o >= nx:
                     owner[p] = k
         for i, r in enumerate(nlp.ineq):
-            owner[n + i] = r // rows
+            owner[n + i] = r // rows if r < n_k * rows else -1     # global rows (t_f bounds): separators
         # interval rows, except the continuity rows: an interval has more rows than interior
         # unknowns (x[k], x[k+1] close the count), so their multipliers join the separators
         rr = np.arange(m)

@@ -1,4 +1,6 @@
-"""Wind-speed sweep of the AP2 power cycle, sharded across GPUs.
+"""Wind-speed sweeps of the power cycle, sharded across GPUs: the AP2
+single kite (``arch='single'``) and the dual kites of config 4 (``arch='dual'``,
+examples/dual_kites_power_curve.py).
 
 The reference sweeps the trial over ``user_options.wind.u_ref`` sequentially, warm-starting each
 point from the previous one (awebox/sweep.py:120-163, examples/dual_kites_power_curve.py:48-52).
@@ -37,8 +39,61 @@ from .trajectory import hippo_options, optimize
 N_OUT = 6   # u_ref, avg power, period, iterations, status ok, seconds
 
 
+class _Ap2:
+    """The AP2 single-kite problem behind the sweep (problem.py, homotopy.py, trajectory.py)."""
+
+    def __init__(self, n_k, d):
+        self.consts = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+        self.lay = pb.NlpLayout(n_k, d)
+        self.nconst = pb.NCONST
+
+    def initial_guess(self):
+        return initial_guess(self.consts, self.lay)
+
+    def final_step(self, v0):
+        return hm.schedule(self.consts, self.lay, v0)[-1]
+
+    def pack_p(self, v0, step, u):
+        return pb.pack_p(self.lay, self.consts, v0, step=step, u_ref=u)
+
+    def outputs(self, V):
+        return hm.outputs(self.consts, self.lay, V)
+
+    def optimize(self, ev, opts, device, v0, u):
+        return optimize(self.consts, ev, opts, device=device, v_init=v0, u_ref=u)
+
+
+class _Dual:
+    """The dual-kite problem of config 4 (dual.py, dual_homotopy.py)."""
+
+    def __init__(self, n_k, d):
+        from . import dual as du
+        self.du = du
+        self.consts = du.build_constants(du.MultiConfig(n_k=n_k, d=d))
+        self.lay = du.layout_for(self.consts)
+        self.nconst = du.NCONST
+
+    def initial_guess(self):
+        return self.du.initial_guess(self.consts, self.lay)
+
+    def final_step(self, v0):
+        from . import dual_homotopy as dh
+        return dh.schedule(self.consts, self.lay, v0)[-1]
+
+    def pack_p(self, v0, step, u):
+        return self.du.pack_p(self.lay, self.consts, v0, step=step, u_ref=u)
+
+    def outputs(self, V):
+        from . import dual_homotopy as dh
+        return dh.outputs(self.consts, self.lay, V)
+
+    def optimize(self, ev, opts, device, v0, u):
+        from . import dual_homotopy as dh
+        return dh.optimize(self.consts, ev, opts, device=device, v_init=v0, u_ref=u)
+
+
 def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda", opts: IpmOptions | None = None,
-              verbose=False, point_solver=None):
+              verbose=False, point_solver=None, arch="single"):
     """Returns (on rank 0) dict with per-point outputs, V_opt [P, n_v] and timing; None elsewhere.
 
     ``point_solver(u, prev) -> (V, outputs, iterations, ok, prev)`` replaces the per-point solve
@@ -46,21 +101,20 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     coll_dev = torch.device(device)
-    cfg = pb.Ap2Config(n_k=n_k, d=d)
-    consts = pb.build_constants(cfg)
-    lay = pb.NlpLayout(n_k, d)
+    prob = _Dual(n_k, d) if arch == "dual" else _Ap2(n_k, d)
+    consts, lay, nconst = prob.consts, prob.lay, prob.nconst
     n_pts = len(u_refs)
     per = -(-n_pts // world)
 
     # ---- template broadcast: model constants + initial guess (rank 0 -> all) ----------------
-    tmpl = torch.zeros(pb.NCONST + lay.n_v, dtype=torch.float64, device=coll_dev)
+    tmpl = torch.zeros(nconst + lay.n_v, dtype=torch.float64, device=coll_dev)
     if rank == 0:
-        tmpl[:pb.NCONST] = torch.tensor(consts.consts)
-        tmpl[pb.NCONST:] = torch.tensor(initial_guess(consts, lay))
+        tmpl[:nconst] = torch.tensor(consts.consts)
+        tmpl[nconst:] = torch.tensor(prob.initial_guess())
     if dist is not None:
         dist.broadcast(tmpl, src=0)
-    consts.consts = tmpl[:pb.NCONST].cpu().numpy().copy()
-    v0 = tmpl[pb.NCONST:].cpu().numpy().copy()
+    consts.consts = tmpl[:nconst].cpu().numpy().copy()
+    v0 = tmpl[nconst:].cpu().numpy().copy()
 
     # ---- seed scatter ---------------------------------------------------------------------------
     seeds = torch.full((per,), float("nan"), dtype=torch.float64, device=coll_dev)
@@ -78,18 +132,18 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     # ---- local solves ---------------------------------------------------------------------------
     if point_solver is None:
         ev = make_evaluator(consts)
-        final = hm.schedule(consts, lay, v0)[-1]
+        final = prob.final_step(v0)
         lbg, ubg = lay.g_bounds()
         done = ("solve_succeeded", "solved_to_acceptable_level")
 
         def point_solver(u, prev):
             if prev is None:
-                V, summary, out, res = optimize(consts, ev, opts, device=device, v_init=v0, u_ref=u)
+                V, summary, out, res = prob.optimize(ev, opts, device, v0, u)
                 return V, out, sum(r["iterations"] for r in summary), all(r["status"] in done for r in summary), res
-            P = pb.pack_p(lay, consts, v0, step=final.cost_step, u_ref=u)
+            P = prob.pack_p(v0, final.cost_step, u)
             res = solve(ev, P, prev.x, final.lbx, final.ubx, lbg, ubg, lam0=prev.lam_g, zl0=prev.zl, zu0=prev.zu,
                         opts=hippo_options("final", opts), device=device)
-            return res.x, hm.outputs(consts, lay, res.x), res.iterations, res.status in done, res
+            return res.x, prob.outputs(res.x), res.iterations, res.status in done, res
 
     res_v = torch.zeros(per, lay.n_v, dtype=torch.float64, device=coll_dev)
     res_o = torch.full((per, N_OUT), float("nan"), dtype=torch.float64, device=coll_dev)
@@ -137,6 +191,8 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=64)
+    ap.add_argument("--arch", choices=["single", "dual"], default="single",
+                    help="single: AP2 power curve; dual: dual-kite power curve (config 4)")
     ap.add_argument("--u-min", type=float, default=5.0)
     ap.add_argument("--u-max", type=float, default=8.0)
     ap.add_argument("--n-k", type=int, default=40)
@@ -159,12 +215,18 @@ def main():
     if dist is not None:
         dist.barrier()
     u = np.linspace(args.u_min, args.u_max, args.points)
-    res = run_sweep(u, n_k=args.n_k, d=args.d, make_evaluator=lambda c: Ap2Evaluator(c, batch=1), dist=dist,
-                    device=f"cuda:{local_rank}", opts=IpmOptions(max_iter=args.max_iter), verbose=args.verbose)
+    if args.arch == "dual":
+        from .dual_homotopy import make_evaluator
+        mk = lambda c: make_evaluator(c, device=f"cuda:{local_rank}")  # noqa: E731
+    else:
+        mk = lambda c: Ap2Evaluator(c, batch=1)  # noqa: E731
+    res = run_sweep(u, n_k=args.n_k, d=args.d, make_evaluator=mk, dist=dist, device=f"cuda:{local_rank}",
+                    opts=IpmOptions(max_iter=args.max_iter), verbose=args.verbose, arch=args.arch)
     if res is not None:
         res = dict(res)
         res.pop("V_opt")
-        res.update(n_k=args.n_k, d=args.d, metric="sweep trials/sec, AP2 power curve", gpus=world)
+        res.update(n_k=args.n_k, d=args.d, arch=args.arch, gpus=world,
+                   metric=f"sweep trials/sec, {'dual-kite' if args.arch == 'dual' else 'AP2'} power curve")
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as fh:
             json.dump(res, fh, indent=1)

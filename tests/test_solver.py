@@ -117,24 +117,30 @@ def _fake_point_solver(n_v):
     return solve_point
 
 
-def _sweep_worker(rank, world, port, q):
+def _sweep_worker(rank, world, port, q, arch="single"):
     import os
 
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from awebox_amd.sweep import run_sweep
-    n_v = pb.NlpLayout(4, 2).n_v
+    if arch == "dual":
+        from awebox_amd import dual as du
+        n_v = du.layout_for(du.build_constants(du.MultiConfig(n_k=4, d=2))).n_v
+    else:
+        n_v = pb.NlpLayout(4, 2).n_v
     res = run_sweep([5.0, 5.5, 6.0, 6.5, 7.0], n_k=4, d=2, dist=dist, device="cpu",
-                    point_solver=_fake_point_solver(n_v))
+                    point_solver=_fake_point_solver(n_v), arch=arch)
     if rank == 0:
         q.put({k: (v.tolist() if hasattr(v, "tolist") else v) for k, v in res.items()})
     dist.destroy_process_group()
 
 
-def test_sweep_collectives_over_two_ranks():
+@pytest.mark.parametrize("arch", ["single", "dual"])
+def test_sweep_collectives_over_two_ranks(arch):
     """world_size 2 over gloo: template broadcast, seeds scattered in contiguous blocks (3 + 2
-    points, padded), solutions gathered to rank 0 in point order, warm-start chains per shard."""
+    points, padded), solutions gathered to rank 0 in point order, warm-start chains per shard
+    (AP2 and the dual-kite problem of config 4)."""
     import socket
 
     import torch.multiprocessing as mp
@@ -143,7 +149,7 @@ def test_sweep_collectives_over_two_ranks():
         port = s_.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_sweep_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sweep_worker, args=(r, 2, port, q, arch)) for r in range(2)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)

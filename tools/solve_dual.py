@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--final-step", default=None)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "solve_dual.json"))
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--profile", action="store_true")
     args = ap.parse_args()
     import torch
     from awebox_amd import dual as du
@@ -30,7 +31,7 @@ def main():
     mc = du.build_constants(du.MultiConfig(n_k=args.n_k, d=args.d, u_ref=args.u_ref))
     ev = dh.make_evaluator(mc)
     t0 = time.perf_counter()
-    V, summary, out, _ = dh.optimize(mc, ev, IpmOptions(max_iter=args.max_iter, verbose=args.verbose),
+    V, summary, out, _ = dh.optimize(mc, ev, IpmOptions(max_iter=args.max_iter, verbose=args.verbose, profile=args.profile),
                                      verbose=True, final_step=args.final_step)
     rec = {"n_k": args.n_k, "d": args.d, "u_ref": args.u_ref, "seconds": time.perf_counter() - t0,
            "steps": summary, "outputs": out, "device": torch.cuda.get_device_name(0)}
