@@ -2,7 +2,8 @@
 
 * ``awebox_amd/libawegpu.so`` -- the AP2 collocation evaluator (include/awegpu.h);
 * ``awebox_amd/libawempc.so`` -- the 3-DOF tracking-MPC evaluator (include/awempc.h);
-* ``awebox_amd/libawedual.so`` -- the dual-kite (multi-kite) evaluator (include/awedual.h).
+* ``awebox_amd/libawedual.so`` -- the dual-kite (multi-kite) evaluator (include/awedual.h);
+* ``awebox_amd/libawelu.so`` -- batched LU of the structured KKT solve's interval blocks.
 
 Plain ``hipcc -shared -fPIC`` (no JIT cache): the .so files live next to this file so that they
 travel with the repository snapshot to the GPU box.
@@ -19,6 +20,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libawegpu.so")
 LIB_MPC = os.path.join(HERE, "libawempc.so")
 LIB_DUAL = os.path.join(HERE, "libawedual.so")
+LIB_LU = os.path.join(HERE, "libawelu.so")
 _COMMON = [os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
     os.path.join(INCLUDE, "awegpu.h")]
 TARGETS = {
@@ -29,6 +31,7 @@ TARGETS = {
     LIB_DUAL: ([os.path.join(CSRC, "awedual.hip")],
                _COMMON + [os.path.join(CSRC, f) for f in ("dual_model.hpp", "dual_tables.hpp")]
                + [os.path.join(INCLUDE, "awedual.h")]),
+    LIB_LU: ([os.path.join(CSRC, "batched_lu.hip")], []),
 }
 ARCH = os.environ.get("AWE_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wno-unused-value",

@@ -63,6 +63,7 @@ class IpmOptions:
     alpha_min_frac: float = 0.05
     max_backtracks: int = 40
     kkt: str = "structured"          # "structured" (interval elimination + Schur) or "dense"
+    lu_backend: str = "awelu"        # interval-block LU: "awelu" (batched_lu.hip) or "torch" (rocSOLVER)
     profile: bool = False            # synchronise and time the solver's phases (IpmResult.timing)
     verbose: bool = False
 
@@ -219,8 +220,9 @@ class StructuredKKT:
         S = K_SS - sum_k K_SI^k (K_II^k)^-1 K_IS^k,
     about 5 GFLOP at N=40 instead of the 1.3 TFLOP of a dense LU of the whole system."""
 
-    def __init__(self, nlp, lay, dev):
+    def __init__(self, nlp, lay, dev, lu_backend="awelu"):
         n, ny, m = nlp.n, nlp.ny, nlp.m
+        self.lu_backend = lu_backend
         N = ny + m
         self.N, self.dev = N, dev
         n_k, stride, v0, rows = lay.n_k, lay.interval_stride, lay.v_intervals, lay.rows_per_interval
@@ -310,7 +312,11 @@ class StructuredKKT:
         KIS = KIS.view(n_k, nI, L)
         S = torch.zeros((nS + 1) * (nS + 1), **f64)
         S.index_put_((self.dst_ss,), vals[self.sel_ss], accumulate=True)
-        self.LU_I, self.piv_I = torch.linalg.lu_factor(KII)
+        if self.lu_backend == "awelu" and KII.is_cuda:      # the CPU test harness uses LAPACK
+            from .batched_lu import lu_factor
+            self.LU_I, self.piv_I = lu_factor(KII)
+        else:
+            self.LU_I, self.piv_I = torch.linalg.lu_factor(KII)
         self.X = torch.linalg.lu_solve(self.LU_I, self.piv_I, KIS)            # K_II^-1 K_IS
         T = KIS.transpose(1, 2) @ self.X                                       # [n_k, L, L]
         S.index_put_((self.schur_flat,), -T.reshape(-1), accumulate=True)
@@ -445,7 +451,7 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
     skkt = None
     if opts.kkt == "structured" and getattr(ev, "layout", None) is not None:
         try:
-            skkt = StructuredKKT(nlp, ev.layout, dev)
+            skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend)
         except ValueError:
             skkt = None
     K = torch.zeros(N, N, **f64) if skkt is None else None
