@@ -76,6 +76,8 @@ def main():
                     help="MPC instances for the config-5 block (3-DOF tracking MPC, N=20 d=4; 0: skip)")
     ap.add_argument("--dual-batch", type=int, default=128,
                     help="dual-kite NLP instances for the config-3 block (N=60 d=4 single_reelout; 0: skip)")
+    ap.add_argument("--dual-sweep-points", type=int, default=2,
+                    help="dual-kite u_ref sweep points per GPU (config 4 recipe, example discretization N=20; 0: skip)")
     ap.add_argument("--sweep-points", type=int, default=2,
                     help="u_ref sweep points solved per GPU for the sweep block (0: skip)")
     args = ap.parse_args()
@@ -162,6 +164,9 @@ def main():
     sweep = None
     if args.sweep_points > 0:
         sweep = sweep_block(args.sweep_points, world, dist, dev, consts)
+    dual_sweep = None
+    if args.dual_sweep_points > 0:
+        dual_sweep = dual_sweep_block(args.dual_sweep_points, world, dist, dev)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -214,6 +219,8 @@ def main():
         line["mpc"] = mpc
     if sweep is not None:
         line["sweep"] = sweep
+    if dual_sweep is not None:
+        line["dual_sweep"] = dual_sweep
     if not args.no_hessian:
         line["hessian"] = hessian_block(ev, V, P, B, lay, dev)
     if world == 1 and not args.no_cpu_baseline:
@@ -371,6 +378,37 @@ def sweep_block(per_gpu, world, dist, dev, consts):
             "avg_power_W": [round(p, 1) for p in res["avg_power_W"]],
             "period_s": [round(t, 2) for t in res["period_s"]], "scaling": "weak",
             "solver": "GPU interior point (awebox_amd/ipm.py), structured KKT, exact Hessian"}
+
+
+def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
+    """Config 4: the dual-kite power curve (examples/dual_kites_power_curve.py: architecture
+    {1:0, 2:1, 3:1}, N=20 d=4 as in the example, u_ref = linspace(5, 8)), `per_gpu` points per
+    rank in contiguous blocks (weak scaling), template broadcast / seed scatter / solution gather
+    over RCCL; per point the GPU interior-point solver with the HIP dual-kite evaluator and the
+    coloured central-difference Hessian.  Timed by run_sweep between barriers, max over ranks."""
+    import numpy as np
+    import torch
+
+    from awebox_amd.dual_homotopy import make_evaluator
+    from awebox_amd.ipm import IpmOptions
+    from awebox_amd.sweep import run_sweep
+
+    n_pts = per_gpu * world
+    u = np.linspace(5.0, 8.0, n_pts)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    res = run_sweep(u, n_k=n_k, d=d, make_evaluator=lambda c: make_evaluator(c, device=str(dev)), dist=dist,
+                    device=str(dev), opts=IpmOptions(max_iter=1500), arch="dual")
+    if res is None:
+        return None
+    return {"metric": f"sweep trials/sec, dual-kite power curve N={n_k} d={d} (config 4)",
+            "value": res["trials_per_s"], "unit": "trials/s", "points": n_pts, "points_per_gpu": per_gpu,
+            "wall_s": res["wall_s"], "all_converged": bool(all(res["ok"])), "iterations": res["iterations"],
+            "avg_power_W": [round(p, 1) for p in res["avg_power_W"]],
+            "period_s": [round(t, 2) for t in res["period_s"]], "scaling": "weak",
+            "solver": "GPU interior point (awebox_amd/ipm.py), structured KKT with batched LU (batched_lu.hip), "
+                      "Hessian by coloured central differences of the HIP gradient (fd_hessian.py)"}
 
 
 def hessian_block(ev, V, P, B, lay, dev, steps=10):
