@@ -157,7 +157,8 @@ def main():
 
     dual = None
     if args.dual_batch > 0:
-        dual = dual_block(args.dual_batch, rank, dev, dist, world)
+        dual = dual_block(args.dual_batch, rank, dev, dist, world,
+                          cpu_seconds=0.0 if (args.no_cpu_baseline or world > 1) else args.cpu_seconds / 2)
     mpc = None
     if args.mpc_batch > 0:
         mpc = mpc_block(args.mpc_batch, rank, dev, dist, world)
@@ -230,7 +231,7 @@ def main():
         dist.destroy_process_group()
 
 
-def dual_block(B, rank, dev, dist, world, steps=20, warmup=3):
+def dual_block(B, rank, dev, dist, world, steps=20, warmup=3, cpu_seconds=0.0):
     """Config 3: B dual-kite NLP instances per GPU (architecture {1:0, 2:1, 3:1},
     N=60, d=4, single_reelout; examples/dual_kites_power_curve.py), synthetic members
     V0 + 0.01 N(0,1) of the standard multi-kite initial guess; one step = one batched
@@ -279,6 +280,28 @@ def dual_block(B, rank, dev, dist, world, steps=20, warmup=3):
     kernel_ms = float(np.mean(kms))
     achieved = bytes_per_eval * B / (kernel_ms * 1e-3) / 1e9
     ncol = colour_counts(c)
+    cpu = None
+    if cpu_seconds > 0 and rank == 0:
+        from oracle.dual_cpu_port import DualCpuPort
+        port = DualCpuPort(c)
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+
+        def rate(nb, nthreads):
+            Vh = np.stack([du.batch_member(v0, lay, b) for b in range(nb)])
+            Ph = np.stack([du.pack_p(lay, c, v0)] * nb)
+            port.eval_nlp(Vh, Ph, threads=nthreads)
+            n, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < cpu_seconds:
+                port.eval_nlp(Vh, Ph, threads=nthreads)
+                n += nb
+            return n / (time.perf_counter() - t0), n
+
+        r_all, n_all = rate(max(threads, 4), threads)
+        r_one, n_one = rate(1, 1)
+        cpu = {"value": r_all, "unit": "evals/s", "cores": threads, "kind": "port", "value_1core": r_one,
+               "sample": f"C++ CPU port of the dual-kite evaluator (oracle/cpu/dual_cpu.cpp, the kernel's algorithm, "
+                         f"OpenMP over (instance, interval)): {n_all} evaluations on {threads} threads and {n_one} "
+                         f"on 1 thread, ~{cpu_seconds:.0f} s each"}
     return {"metric": "dual-kite NLP f/g/Jacobian evals/sec, N=60 d=4 single_reelout (config 3)",
             "value": B * steps * world / el, "unit": "evals/s", "instances_per_gpu": B,
             "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": ev.nnz,
@@ -287,7 +310,8 @@ def dual_block(B, rank, dev, dist, world, steps=20, warmup=3):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "kernel": "dual_interval_kernel<4>",
                          "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)),
-                         "bytes_per_eval": bytes_per_eval}}
+                         "bytes_per_eval": bytes_per_eval},
+            "cpu_baseline": cpu}
 
 
 def pb_ntheta0():

@@ -11,6 +11,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 LIB = os.path.join(HERE, "libap2cpu.so")
+LIB_DUAL = os.path.join(HERE, "libdualcpu.so")
+DUAL_SOURCES = [os.path.join(HERE, "dual_cpu.cpp")]
+DUAL_HEADERS = [os.path.join(ROOT, "awebox_amd", "csrc", f) for f in
+                ("dual_model.hpp", "dual_tables.hpp", "ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
+    os.path.join(ROOT, "include", f) for f in ("awedual.h", "awegpu.h")]
 SOURCES = [os.path.join(HERE, "ap2_cpu.cpp")]
 HEADERS = [os.path.join(HERE, "dualn.hpp")] + [
     os.path.join(ROOT, "awebox_amd", "csrc", f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
@@ -19,21 +24,27 @@ FLAGS = ["-O3", "-march=x86-64-v3", "-fopenmp", "-fPIC", "-shared", "-std=c++17"
          "-I", os.path.join(ROOT, "awebox_amd", "csrc"), "-I", os.path.join(ROOT, "include")]
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def _stale(lib=LIB, deps=None) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(p) > t for p in (deps or SOURCES + HEADERS))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
-    cmd = [os.environ.get("CXX", "g++"), *FLAGS, *SOURCES, "-o", LIB + ".tmp"]
+def _compile(lib, sources, verbose):
+    cmd = [os.environ.get("CXX", "g++"), *FLAGS, *sources, "-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib + ".tmp", lib)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Both CPU ports: libap2cpu.so (AP2) and libdualcpu.so (dual kites); returns the AP2 path."""
+    if force or _stale():
+        _compile(LIB, SOURCES, verbose)
+    if force or _stale(LIB_DUAL, DUAL_SOURCES + DUAL_HEADERS):
+        _compile(LIB_DUAL, DUAL_SOURCES, verbose)
     return LIB
 
 

@@ -29,8 +29,6 @@ def test_lu_factor_matches_definition(gpu, batch, n):
     x = torch.linalg.lu_solve(LU, piv, rhs)
     res = (A @ x - rhs).abs().max() / (A.abs().max() * x.abs().max() + rhs.abs().max())
     assert res.item() < 1e-12
-    # partial pivoting like LAPACK's (largest magnitude): the pivot sequences agree except where
-    # rounding differences of the trailing updates flip a near-tie late in the factorisation
-    LU_ref, piv_ref = torch.linalg.lu_factor(A)
-    agree = (piv.to(piv_ref.dtype) == piv_ref).double().mean().item()
-    assert agree >= 0.99, agree
+    # partial pivoting: every multiplier is bounded by 1 in magnitude (the pivot sequence itself may
+    # differ from LAPACK's where rounding flips a near-tie; then all later choices differ too)
+    assert L.abs().max().item() <= 1.0 + 1e-12

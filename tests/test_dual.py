@@ -185,3 +185,28 @@ def test_static_sparsity_covers_oracle_pattern(lib):
     assert not np.any((J != 0) & ~pat), "oracle non-zero outside the evaluator's CCS pattern"
     n0, n1, t0, t1 = colour_counts(mc)
     assert n0 <= 64 and n1 <= 64          # one wavefront per node
+
+
+@pytest.mark.parametrize("n_k,d,member", [(5, 3, 0), (4, 4, 2)])
+def test_cpu_port_matches_oracle(n_k, d, member):
+    """The kernel's algorithm on the host (oracle/cpu/dual_cpu.cpp: colouring, objective
+    directional derivatives, gradient assembly, gather list) against the oracle."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_gpu_parity import _close, _close_jac
+    from oracle import multikite_oracle as mo
+    from oracle.dual_cpu_port import DualCpuPort
+    mc = du.build_constants(du.MultiConfig(n_k=n_k, d=d))
+    lay = du.layout_for(mc)
+    V0 = du.initial_guess(mc, lay)
+    V = du.batch_member(V0, lay, member)
+    P = du.pack_p(lay, mc, V0, "power1")
+    o = mo.from_constants(mc, lay)
+    th = mo.theta0_dict(P[lay.p_theta0:])
+    port = DualCpuPort(mc)
+    out = port.eval_nlp(V, P, threads=2)
+    f = float(o.nlp_f(V, P, lay, th, pb.COST_NAMES, pb.PHI_NAMES))
+    assert abs(out["f"][0] - f) <= 1e-12 * abs(f)
+    _close(out["g"][0], o.nlp_g(V, P, lay, th).numpy(), "g")
+    _close(out["grad_f"][0], o.nlp_grad_f(V, P, lay, th, pb.COST_NAMES, pb.PHI_NAMES).numpy(), "grad_f")
+    _close_jac(port.jac_csc(out["jac"][0]), o.nlp_jac_g(V, P, lay, th))
