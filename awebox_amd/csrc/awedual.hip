@@ -6,13 +6,14 @@
 // nlpsol (awebox/opti/preparation.py:366-400).
 //
 // Execution model (the AP2 evaluator's design, awegpu.hip, scaled to the 126-variable node):
-//   * one workgroup per (NLP instance, shooting interval), ONE wavefront per node (d + 1 waves);
+//   * one workgroup per (NLP instance, shooting interval), 256 threads;
 //   * the interval's slice of V and of P.p.ref plus the effective objective weights are staged
 //     in LDS with coalesced loads;
 //   * model pass, compressed forward mode: the 127 seed directions of a node are coloured on the
-//     host into <= 64 groups with disjoint row sets (37 at the shooting node, 39 at a Radau node),
-//     so lane c of the node's wavefront evaluates dual_node in dual arithmetic along colour c and
-//     the wavefront recovers the whole node Jacobian block.  The collocation chain rule
+//     host into <= 64 groups with disjoint row sets (37 at the shooting node, 39 at a Radau node);
+//     one thread per (node, colour) evaluates dual_node in dual arithmetic along its colour (the
+//     193 tasks at d = 4 are packed into 4 wavefronts), recovering every node Jacobian block.  The
+//     collocation chain rule
 //     xdot = C X / (h t_f(k)) is folded into the seeds (dual_tables.hpp);
 //   * rows stream from the lanes into a compressed LDS tangent buffer (branch-free sink);
 //   * objective pass: one thread per (Radau node, direction) forms the directional derivative
@@ -174,14 +175,19 @@ struct DualPreSubmodels {
     }
 };
 
+// Workgroup size: the (node, colour) tasks of the model pass (37 + d x 39 at d = 4) are packed
+// into 4 wavefronts instead of one wavefront per node, so that two workgroups fit a CU at the
+// kernel's register budget (256 VGPRs = 2 waves per SIMD: 8 waves per CU).
+constexpr int kBlock = 256;
+
 #ifndef ADL_MIN_BLOCKS
-#define ADL_MIN_BLOCKS 1    // __launch_bounds__ minimum waves per SIMD
+#define ADL_MIN_BLOCKS 2    // __launch_bounds__ minimum waves per SIMD: two workgroups per CU
 #endif
 
 template <int D>
-__global__ __launch_bounds__(64 * (D + 1), ADL_MIN_BLOCKS) void dual_interval_kernel(DArgs a) {
+__global__ __launch_bounds__(kBlock, ADL_MIN_BLOCKS) void dual_interval_kernel(DArgs a) {
     constexpr int NN = D + 1;
-    constexpr int NT = 64 * NN;
+    constexpr int NT = kBlock;
     constexpr int STRIDE = 2 * ADL_NX + ADL_NU + ADL_NZ + D * (ADL_NX + ADL_NZ);
     constexpr int NLOC = ADL_NTHV + 7 + STRIDE + ADL_NX;
     __shared__ double vloc[NLOC];               // theta_v, phi, x[k], u, xdot, z, coll.., x[k+1]
@@ -352,11 +358,14 @@ __global__ __launch_bounds__(64 * (D + 1), ADL_MIN_BLOCKS) void dual_interval_ke
     }
     __syncthreads();
 
-    // ---- model pass: wave = node, lane = colour ------------------------------------------
+    // ---- model pass: one (node, colour) task per thread, packed across the workgroup ----------
     {
-        const int n = tid >> 6, lane = tid & 63;
+        const int n0c = a.ct->ncol[0], n1c = a.ct->ncol[1];
+        int n, lane;
+        if (tid < n0c) { n = 0; lane = tid; }
+        else { n = 1 + (tid - n0c) / n1c; lane = (tid - n0c) % n1c; }
         const int kind = n > 0;
-        if (lane < a.ct->ncol[kind]) {
+        if (n < NN) {
             const int toff = n == 0 ? 0 : a.ct->tsize[0] + (n - 1) * a.ct->tsize[1];
             DLaneIn in{wn[n], colb[kind], lane, n > 0 ? C[n * NN + n] * ihtf : 0.0,
                        (n > 0 && colb[1][awe::dl::kTf] == lane) ? -1.0 / tf : 0.0};
@@ -551,7 +560,7 @@ __global__ __launch_bounds__(64) void dual_finalize_kernel(DArgs a) {
 
 template <int D>
 int launch(const DArgs& a, int batch, size_t dyn, hipStream_t s) {
-    dual_interval_kernel<D><<<dim3((unsigned)(batch * a.n_k)), 64 * (D + 1), dyn, s>>>(a);
+    dual_interval_kernel<D><<<dim3((unsigned)(batch * a.n_k)), kBlock, dyn, s>>>(a);
     return 0;
 }
 
@@ -642,6 +651,10 @@ int adl_create(int n_k, int d, const double* consts, int n_consts, int batch, ad
         return fail(AWE_ERR_ARG, err);
     }
     const Tables& T = h->t;
+    if (T.ct.ncol[0] + d * T.ct.ncol[1] > kBlock) {
+        delete h;
+        return fail(AWE_ERR_ARG, "more (node, colour) tasks than threads per workgroup");
+    }
     if ((int)consts[ADL_C_N_ELEMENTS] > kMaxElements) {
         delete h;
         return fail(AWE_ERR_ARG, "the dual-kite kernel supports at most 8 tether elements per segment");
