@@ -19,6 +19,9 @@ def load_library(path: str = _PATH):
         lib = ctypes.CDLL(path)
         lib.awelu_factor_batched.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p]
+        lib.awelu_solve_batched.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        lib.awelu_btd_solve_batched.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 3
         lib.awelu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
@@ -42,3 +45,59 @@ def lu_factor(A):
     if rc != 0:
         raise RuntimeError(f"awelu_factor_batched: {lib.awelu_last_error().decode()}")
     return (LU[0], piv[0]) if squeeze else (LU, piv)
+
+
+def lu_solve(LU, piv, B):
+    """A^-1 B from lu_factor's (LU, piv): LU [batch, n, n], piv int32 [batch, n], B [batch, n, nrhs]
+    float64 CUDA tensors (also unbatched [n, n], [n], [n, nrhs]); returns a new tensor."""
+    import torch
+    if LU.dtype != torch.float64 or B.dtype != torch.float64 or piv.dtype != torch.int32 or not LU.is_cuda:
+        raise ValueError("lu_solve needs float64 CUDA factors / right-hand sides and int32 pivots")
+    squeeze = LU.dim() == 2
+    LU3 = (LU.unsqueeze(0) if squeeze else LU).contiguous()
+    piv2 = (piv.unsqueeze(0) if squeeze else piv).contiguous()
+    X = (B.unsqueeze(0) if squeeze else B).contiguous().clone()
+    b, n, _ = LU3.shape
+    if X.dim() != 3 or X.shape[0] != b or X.shape[1] != n or piv2.shape != (b, n):
+        raise ValueError(f"shape mismatch: LU {tuple(LU3.shape)}, piv {tuple(piv2.shape)}, B {tuple(X.shape)}")
+    lib = load_library()
+    s = torch.cuda.current_stream(LU3.device).cuda_stream
+    rc = lib.awelu_solve_batched(n, X.shape[2], b, ctypes.c_void_p(LU3.data_ptr()), ctypes.c_void_p(piv2.data_ptr()),
+                                 ctypes.c_void_p(X.data_ptr()), ctypes.c_void_p(s))
+    if rc != 0:
+        raise RuntimeError(f"awelu_solve_batched: {lib.awelu_last_error().decode()}")
+    return X[0] if squeeze else X
+
+
+def btd_solve(T, X):
+    """Block-tridiagonal solve: T [batch, nb, 3, m, m] (sub-, main, super-diagonal block of every
+    block row), X [batch, nb, m, nrhs]; float64 CUDA tensors, m <= 32, nrhs <= 8.  Returns the
+    solution (new tensor); T is not modified."""
+    import torch
+    if T.dtype != torch.float64 or X.dtype != torch.float64 or not T.is_cuda or not X.is_cuda:
+        raise ValueError("btd_solve needs float64 CUDA tensors")
+    if T.dim() != 5 or T.shape[2] != 3 or T.shape[3] != T.shape[4] or X.dim() != 4 or \
+            X.shape[:3] != (T.shape[0], T.shape[1], T.shape[3]):
+        raise ValueError(f"shape mismatch: T {tuple(T.shape)}, X {tuple(X.shape)}")
+    b, nb, _, m, _ = T.shape
+    Tw = T.contiguous().clone()
+    Xw = X.contiguous().clone()
+    lib = load_library()
+    s = torch.cuda.current_stream(T.device).cuda_stream
+    rc = lib.awelu_btd_solve_batched(nb, m, X.shape[3], b, ctypes.c_void_p(Tw.data_ptr()), ctypes.c_void_p(Xw.data_ptr()),
+                                     ctypes.c_void_p(s))
+    if rc != 0:
+        raise RuntimeError(f"awelu_btd_solve_batched: {lib.awelu_last_error().decode()}")
+    return Xw
+
+
+def btd_dense(T):
+    """The dense matrices [batch, nb m, nb m] of block-tridiagonal T [batch, nb, 3, m, m]."""
+    import torch
+    b, nb, _, m, _ = T.shape
+    A = torch.zeros(b, nb * m, nb * m, dtype=T.dtype, device=T.device)
+    for k in range(nb):
+        for s_, dk in ((0, -1), (1, 0), (2, 1)):
+            if 0 <= k + dk < nb:
+                A[:, k * m:(k + 1) * m, (k + dk) * m:(k + dk + 1) * m] = T[:, k, s_]
+    return A

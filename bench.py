@@ -365,13 +365,55 @@ def mpc_block(B, rank, dev, dist, world, steps=50, warmup=5):
     bytes_per_eval = 8 * (lay.n_v + lay.n_p + lay.n_g + lay.n_v + ev.nnz + 1)
     kernel_ms = float(np.mean(kms))
     achieved = bytes_per_eval * B / (kernel_ms * 1e-3) / 1e9
+    finite = bool(torch.isfinite(jac).all().item())
+    nnz = ev.nnz
+    del ev, f, g, gr, jac
+    rti = rti_block(c, B, dev, dist, world)
     return {"metric": "MPC NLP f/g/Jacobian evals/sec, 3-DOF AP2 tracking MPC N=20 d=4 (config 5)",
             "value": B * steps * world / el, "unit": "evals/s", "instances_per_gpu": B,
-            "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": ev.nnz,
-            "finite": bool(torch.isfinite(jac).all().item()),
+            "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": nnz,
+            "finite": finite,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "kernel": "mpc_interval_kernel<4>",
-                         "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval}}
+                         "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval},
+            "rti": rti}
+
+
+def rti_block(c, B, dev, dist, world, steps=10, warmup=3):
+    """Config 5 closed loop: B tracking-MPC loops per GPU, each advanced by one real-time
+    iteration per sampling time (awebox_amd/rti.py: batched linearisation on the HIP evaluator,
+    Gauss-Newton KKT solve by interval elimination on the awelu kernel, radau-collocation plant
+    step, horizon shift).  value = loop-steps/s (loops x sampling times), max over ranks."""
+    import torch
+
+    from awebox_amd.rti import BatchedRti
+
+    r = BatchedRti(c, B, device=str(dev))
+    r.start(seed=99 + dist.get_rank() * B if dist is not None else 99)
+    for _ in range(warmup):
+        r.step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = r.step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return {"metric": "closed-loop real-time iterations/sec (loops x sampling times), 3-DOF tracking MPC N=20 d=4",
+            "value": B * steps * world / el, "unit": "loop-steps/s", "loops_per_gpu": B,
+            "ms_per_step": el / steps * 1e3, "sampling_time_s": c.cfg.ts,
+            "realtime_factor": c.cfg.ts / (el / steps),
+            "kkt_blocks": {"interval": [B * r.nk, r.nI], "separator": [B, r.nS]},
+            "plant_residual_max": float(out["plant_residual"].max()),
+            "eq_residual_median": float(out["eq_residual"].median()),
+            "finite": bool(torch.isfinite(r.V).all().item())}
 
 
 def sweep_block(per_gpu, world, dist, dev, consts):

@@ -1,0 +1,41 @@
+/* awelu -- batched dense LU factorisation and solve of many mid-sized fp64 matrices on MI355X
+ * (awebox_amd/csrc/batched_lu.hip, libawelu.so).
+ *
+ * Not an entry point of the reference's NLP oracle: these replace the linear algebra under
+ * IPOPT's KKT solve (MA27/MUMPS inside `cas.nlpsol(..., 'ipopt')`, opti/preparation.py:366-400)
+ * for the GPU solvers (awebox_amd/ipm.py StructuredKKT, awebox_amd/rti.py), which factorise
+ * the interval blocks of the structured KKT system as one batch.
+ *
+ * Convention = LAPACK getrf / torch.linalg.lu_factor: row-major A[b][n][n] overwritten by the unit
+ * lower factor (below the diagonal) and the upper factor (on and above); piv[b][n] 1-based, row k
+ * exchanged with row piv[k] - 1 at step k.  All pointers are device pointers; calls are
+ * asynchronous on `stream` (a hipStream_t, NULL = default stream).  Return 0 on success,
+ * non-zero with awelu_last_error() describing the failure.
+ */
+#ifndef AWELU_H
+#define AWELU_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* In-place LU with partial pivoting of `batch` n x n matrices, 1 <= n <= 1024. */
+int awelu_factor_batched(int n, int batch, double* A, int* piv, void* stream);
+
+/* X[b] <- A[b]^-1 X[b] from the factors of awelu_factor_batched; X[b][n][nrhs] row-major. */
+int awelu_solve_batched(int n, int nrhs, int batch, const double* LU, const int* piv, double* X, void* stream);
+
+/* Block-tridiagonal systems (the stage-ordered separator system of the structured KKT):
+ * T[b][nb][3][m][m] = (block (k, k-1), block (k, k), block (k, k+1)) of each block row,
+ * X[b][nb][m][nrhs] right-hand sides solved in place; T is overwritten.  m <= 32, nrhs <= 8.
+ * Block LU without interchanges between block rows (partial pivoting inside each diagonal block). */
+int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, double* T, double* X, void* stream);
+
+/* Message of the last failed call on this thread. */
+const char* awelu_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

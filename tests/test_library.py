@@ -71,3 +71,14 @@ def test_static_hessian_sparsity_equals_cpu_port(lib):
     assert (row <= cols).all()
     for c in range(len(colind) - 1):
         assert (np.diff(row[colind[c]:colind[c + 1]]) > 0).all()
+
+
+def test_awelu_exports_every_header_symbol():
+    """libawelu.so (batched LU + solve) exports what include/awelu.h declares."""
+    from awebox_amd.build import LIB_LU, build_one
+    build_one(LIB_LU)
+    hdr = os.path.join(os.path.dirname(HEADER), "awelu.h")
+    declared = set(re.findall(r"^(?:int|const char\*)\s+(awelu_\w+)\(", open(hdr).read(), re.M))
+    assert declared == {"awelu_factor_batched", "awelu_solve_batched", "awelu_btd_solve_batched", "awelu_last_error"}
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_LU], capture_output=True, text=True, check=True).stdout
+    assert declared <= set(re.findall(r"\bT (awelu_\w+)", out))
