@@ -9,6 +9,7 @@ import os
 _LIB = None
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libawelu.so")
 MAX_N = 1024
+BTD_MAX_M = 56                  # block size limit of the block-tridiagonal kernels (LDS)
 
 
 def load_library(path: str = _PATH):
@@ -21,7 +22,8 @@ def load_library(path: str = _PATH):
                                              ctypes.c_void_p]
         lib.awelu_solve_batched.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_void_p]
-        lib.awelu_btd_solve_batched.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 3
+        lib.awelu_btd_factor_batched.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3
+        lib.awelu_btd_solve_batched.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 4
         lib.awelu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
@@ -69,22 +71,36 @@ def lu_solve(LU, piv, B):
     return X[0] if squeeze else X
 
 
-def btd_solve(T, X):
-    """Block-tridiagonal solve: T [batch, nb, 3, m, m] (sub-, main, super-diagonal block of every
-    block row), X [batch, nb, m, nrhs]; float64 CUDA tensors, m <= 32, nrhs <= 8.  Returns the
-    solution (new tensor); T is not modified."""
+def btd_factor(T):
+    """Factor block-tridiagonal systems T [batch, nb, 3, m, m] (sub-, main, super-diagonal block of
+    every block row; float64 CUDA, m <= 56).  Returns (F, Dinv): F = T with W_k in the super-diagonal
+    slots, Dinv [batch, nb, m, m] the inverted pivot blocks; T is not modified."""
     import torch
-    if T.dtype != torch.float64 or X.dtype != torch.float64 or not T.is_cuda or not X.is_cuda:
-        raise ValueError("btd_solve needs float64 CUDA tensors")
-    if T.dim() != 5 or T.shape[2] != 3 or T.shape[3] != T.shape[4] or X.dim() != 4 or \
-            X.shape[:3] != (T.shape[0], T.shape[1], T.shape[3]):
-        raise ValueError(f"shape mismatch: T {tuple(T.shape)}, X {tuple(X.shape)}")
+    if T.dtype != torch.float64 or not T.is_cuda or T.dim() != 5 or T.shape[2] != 3 or T.shape[3] != T.shape[4]:
+        raise ValueError(f"btd_factor needs a float64 CUDA tensor [batch, nb, 3, m, m], got {tuple(T.shape)}")
     b, nb, _, m, _ = T.shape
-    Tw = T.contiguous().clone()
-    Xw = X.contiguous().clone()
+    F = T.contiguous().clone()
+    Dinv = torch.empty(b, nb, m, m, dtype=torch.float64, device=T.device)
     lib = load_library()
     s = torch.cuda.current_stream(T.device).cuda_stream
-    rc = lib.awelu_btd_solve_batched(nb, m, X.shape[3], b, ctypes.c_void_p(Tw.data_ptr()), ctypes.c_void_p(Xw.data_ptr()),
+    rc = lib.awelu_btd_factor_batched(nb, m, b, ctypes.c_void_p(F.data_ptr()), ctypes.c_void_p(Dinv.data_ptr()),
+                                      ctypes.c_void_p(s))
+    if rc != 0:
+        raise RuntimeError(f"awelu_btd_factor_batched: {lib.awelu_last_error().decode()}")
+    return F, Dinv
+
+
+def btd_solve(F, Dinv, X):
+    """T^-1 X with btd_factor's (F, Dinv); X [batch, nb, m, nrhs] float64 CUDA.  Returns a new tensor."""
+    import torch
+    b, nb, _, m, _ = F.shape
+    if X.dtype != torch.float64 or not X.is_cuda or X.dim() != 4 or X.shape[:3] != (b, nb, m):
+        raise ValueError(f"shape mismatch: F {tuple(F.shape)}, X {tuple(X.shape)}")
+    Xw = X.contiguous().clone()
+    lib = load_library()
+    s = torch.cuda.current_stream(F.device).cuda_stream
+    rc = lib.awelu_btd_solve_batched(nb, m, X.shape[3], b, ctypes.c_void_p(F.data_ptr()),
+                                     ctypes.c_void_p(Dinv.data_ptr()), ctypes.c_void_p(Xw.data_ptr()),
                                      ctypes.c_void_p(s))
     if rc != 0:
         raise RuntimeError(f"awelu_btd_solve_batched: {lib.awelu_last_error().decode()}")

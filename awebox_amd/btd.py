@@ -1,0 +1,137 @@
+"""Bordered block-tridiagonal separator systems of the structured KKT solve.
+
+After the interval interiors are eliminated (ipm.StructuredKKT, rti.BatchedRti), the separators
+are the shooting states x[k], the multipliers c[k] of the continuity rows and a few global
+unknowns (free globals such as t_f, the multipliers of the periodicity and global rows).  In
+stages [c[k-1], x[k]] the separator matrix is block tridiagonal -- interval k's Schur complement
+touches only (x[k], c[k]) and the globals, the continuity row k couples c[k] with x[k+1] -- apart
+from the globals, which form a border:
+    S = [T  E]      T block tridiagonal (nb = N + 1 blocks of 2 n_x),
+        [F  C]      E, F, C the couplings with the n_G border unknowns.
+Pairing x[k] with c[k-1] is the Riccati structure of the stage-wise KKT and keeps the sweep's pivot
+blocks regular; the finer order x[0], c[0], x[1], ... breaks down at N=40.
+Solve:  Z = T^-1 E,  C' = C - F Z,  x_G = C'^-1 (r_G - F T^-1 r_T),  x_T = T^-1 r_T - Z x_G,
+with T factorised once per KKT matrix by the awelu block sweep (awelu_btd_factor_batched) and
+C' (n_G x n_G) by the awelu LU.  This replaces a dense LU of S (n_S = 1,886 at AP2 N=40,
+2,100 for the dual kites at N=20), whose library factorisation is dominated by host-side launch
+overhead (~17 ms of CPU time against 1.4 ms of GPU time per factorisation on MI355X,
+profiles/r01/ipm_profile_n40_awelu_solve.log).
+
+Host tensors (the CPU test harness) take the same assembly and solve the blocks with dense
+LAPACK calls; device tensors use the awelu kernels and fail loudly without them.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+class BorderedBtd:
+    """Separator system with ``stage_of[q]`` (block index, -1 = border) and ``pos_of[q]`` (row
+    within the block) for the n_S separators; the matrix entries arrive as value vectors aligned
+    with the coordinate lists given at construction (duplicates are summed)."""
+
+    def __init__(self, stage_of, pos_of, nb, m, rows, cols, dev):
+        stage_of, pos_of = np.asarray(stage_of), np.asarray(pos_of)
+        rows, cols = np.asarray(rows), np.asarray(cols)
+        nS = len(stage_of)
+        valid = (rows < nS) & (cols < nS)
+        gid = np.full(nS, -1, dtype=np.int64)
+        border = np.where(stage_of < 0)[0]
+        gid[border] = np.arange(len(border))
+        self.nS, self.nb, self.m, self.nG, self.dev = nS, nb, m, len(border), dev
+        slot = np.where(stage_of >= 0, stage_of * m + pos_of, -1)
+        r_ok, c_ok = np.where(valid, rows, 0), np.where(valid, cols, 0)
+        sr, sc = stage_of[r_ok], stage_of[c_ok]
+        tt = valid & (sr >= 0) & (sc >= 0)
+        if np.any(np.abs(sr[tt] - sc[tt]) > 1):
+            raise ValueError("separator couplings are not block tridiagonal in stage order")
+        tg = valid & (sr >= 0) & (sc < 0)
+        gt = valid & (sr < 0) & (sc >= 0)
+        gg = valid & (sr < 0) & (sc < 0)
+        n_t = nb * m
+        t = lambda a: torch.tensor(a, dtype=torch.int64, device=dev)  # noqa: E731
+        self.src_tt, self.dst_tt = t(np.where(tt)[0]), t(((sr[tt] * 3 + 1 + sc[tt] - sr[tt]) * m + pos_of[r_ok[tt]]) * m
+                                                           + pos_of[c_ok[tt]])
+        self.src_tg, self.dst_tg = t(np.where(tg)[0]), t(slot[r_ok[tg]] * self.nG + gid[c_ok[tg]])
+        self.src_gt, self.dst_gt = t(np.where(gt)[0]), t(gid[r_ok[gt]] * n_t + slot[c_ok[gt]])
+        self.src_gg, self.dst_gg = t(np.where(gg)[0]), t(gid[r_ok[gg]] * self.nG + gid[c_ok[gg]])
+        used = np.zeros((nb, m), dtype=bool)
+        used[stage_of[stage_of >= 0], pos_of[stage_of >= 0]] = True
+        if used.sum() != (stage_of >= 0).sum():
+            raise ValueError("two separators share a block position")
+        T0 = np.zeros((nb, 3, m, m))
+        a_, i_ = np.where(~used)
+        T0[a_, 1, i_, i_] = 1.0                           # unused block positions (fixed variables)
+        self.T0 = torch.tensor(T0.reshape(-1), dtype=torch.float64, device=dev)
+        sep_t = np.where(stage_of >= 0)[0]
+        self.sep_t, self.slot_t = t(sep_t), t(slot[sep_t])
+        self.sep_g = t(border)
+
+    # ---------------------------------------------------------------------------------------
+    def factor(self, vals):
+        """vals [n_entries] (or [B, n_entries]): the separator matrix entries."""
+        squeeze = vals.dim() == 1
+        v = vals.unsqueeze(0) if squeeze else vals
+        B, nb, m, nG = v.shape[0], self.nb, self.m, self.nG
+        n_t = nb * m
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        T = self.T0.repeat(B, 1)
+        T.index_add_(1, self.dst_tt, v[:, self.src_tt])
+        E = torch.zeros(B, n_t * nG, **f64)
+        E.index_add_(1, self.dst_tg, v[:, self.src_tg])
+        Fm = torch.zeros(B, nG * n_t, **f64)
+        Fm.index_add_(1, self.dst_gt, v[:, self.src_gt])
+        C = torch.zeros(B, nG * nG, **f64)
+        C.index_add_(1, self.dst_gg, v[:, self.src_gg])
+        T = T.view(B, nb, 3, m, m)
+        self.B = B
+        self.squeeze = squeeze
+        if T.is_cuda:
+            from .batched_lu import btd_factor
+            self.Tf = btd_factor(T)
+        else:
+            from .batched_lu import btd_dense
+            self.Tf = torch.linalg.lu_factor(btd_dense(T))
+        self.Fm = Fm.view(B, nG, n_t)
+        if nG:
+            self.Z = self._t_solve(E.view(B, n_t, nG))                     # T^-1 E
+            Cp = C.view(B, nG, nG) - self.Fm @ self.Z
+            self.Cf = self._lu(Cp)
+
+    def _t_solve(self, X):
+        B, nb, m = self.B, self.nb, self.m
+        if X.is_cuda:
+            from .batched_lu import btd_solve
+            F, Dinv = self.Tf
+            return btd_solve(F, Dinv, X.reshape(B, nb, m, -1)).view(B, nb * m, -1)
+        return torch.linalg.lu_solve(*self.Tf, X)
+
+    @staticmethod
+    def _lu(A):
+        if A.is_cuda:
+            from .batched_lu import lu_factor
+            return lu_factor(A)
+        return torch.linalg.lu_factor(A)
+
+    def _c_solve(self, X):
+        if X.is_cuda:
+            from .batched_lu import lu_solve
+            return lu_solve(*self.Cf, X)
+        return torch.linalg.lu_solve(*self.Cf, X)
+
+    def solve(self, r):
+        """r [n_S] (or [B, n_S]) -> S^-1 r."""
+        r2 = r.unsqueeze(0) if r.dim() == 1 else r
+        B, n_t = r2.shape[0], self.nb * self.m
+        rT = torch.zeros(B, n_t, dtype=torch.float64, device=r.device)
+        rT[:, self.slot_t] = r2[:, self.sep_t]
+        z = self._t_solve(rT.unsqueeze(-1)).squeeze(-1)
+        x = torch.empty_like(r2)
+        if self.nG:
+            rG = r2[:, self.sep_g] - (self.Fm @ z.unsqueeze(-1)).squeeze(-1)
+            xG = self._c_solve(rG.unsqueeze(-1)).squeeze(-1)
+            z = z - (self.Z @ xG.unsqueeze(-1)).squeeze(-1)
+            x[:, self.sep_g] = xG
+        x[:, self.sep_t] = z[:, self.slot_t]
+        return x[0] if r.dim() == 1 else x

@@ -212,65 +212,77 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
 }
 
 constexpr size_t kSolveLds = 144 * 1024;
-constexpr int kBtdMaxM = 32;
-constexpr int kBtdMaxRhs = 8;
 constexpr int kWaveMaxN = 64;
 
-// Block-tridiagonal solve, one workgroup per system: nb diagonal blocks of m x m,
-// T[b][k][3][m][m] holding (sub-diagonal block (k, k-1), diagonal block (k, k), super-diagonal
-// block (k, k+1)), right-hand sides X[b][k][m][nrhs].  Block forward sweep (the Riccati recursion
-// of the stage-wise KKT; no interchanges between block rows):
-//   D'_k = D_k - L_k W_{k-1},  [W_k | Y_k] = D'_k^-1 [U_k | X_k - L_k Y_{k-1}],
-// then x_{nb-1} = Y_{nb-1}, x_k = Y_k - W_k x_{k+1}.  D'_k^-1 [U | X] comes from Gauss-Jordan
-// elimination with partial pivoting on the augmented block in LDS: m steps, each a pivot search
-// by wave shuffles and an elimination of ~m (2m + nrhs) entries.  The 256 threads are a 4 x 64
-// grid (row group, column), so the per-step loops carry no integer division.  W_k overwrites U_k,
-// Y_k and then x_k overwrite X_k.
-__global__ __launch_bounds__(kThreads) void btd_solve_kernel(int nb, int m, int nrhs, double* __restrict__ Ts,
-                                                            double* __restrict__ Xs) {
-    constexpr int kW = 2 * kBtdMaxM + kBtdMaxRhs + 1;
-    constexpr int kRG = kThreads / 64;                        // row groups
+// Block-tridiagonal systems, one workgroup per system: nb diagonal blocks of m x m (m <= 56),
+// T[b][k][3][m][m] = (sub-diagonal block L_k = (k, k-1), diagonal block D_k, super-diagonal block
+// U_k = (k, k+1)).  This is the separator system of the structured KKT in stage order (shooting
+// states and continuity multipliers alternate), and the sweep below is its Riccati recursion;
+// there are no interchanges between block rows, partial pivoting inside each diagonal block.
+//
+// btd_factor_kernel:  D'_k = D_k - L_k W_{k-1},  [W_k | D'_k^-1] = D'_k^-1 [U_k | I]
+//   by Gauss-Jordan on the augmented block [D'_k | U_k | I] in LDS (per column: a pivot search by
+//   wave shuffles, one row interchange, the elimination of every other row; the 256 threads are a
+//   4 x 64 grid of (row group, column), so no integer division in the inner loops).  W_k
+//   overwrites U_k; D'_k^-1 goes to Dinv[b][k][m][m]; W_{k-1} stays in LDS for the next stage
+//   (the augmented block, L_k and W_{k-1} take 127 KB at m = 56).
+//   D'_k itself replaces D_k in T.
+// btd_apply_kernel:   Y_k = D'_k^-1 (X_k - L_k Y_{k-1}),  then x_k = Y_k - W_k x_{k+1}: matrix
+//   products streamed stage by stage, right-hand sides [j0, j0 + w) of X[b][nb m][ldx].  The
+//   explicit inverse alone leaves a backward error of cond(D'_k) eps (the KKT's pivot blocks reach
+//   cond ~1e11), so every block solve takes one refinement step with D'_k: Y += D'^-1 (Z - D' Y).
+// The factorisation is reused by every solve of an interior-point iteration (iterative
+// refinement), and the apply is one launch per solve instead of a library LU's dozens.
+constexpr int kBtdMaxM = 56;
+constexpr int kBtdMaxRhs = 64;
+constexpr int kRG = kThreads / 64;                            // row groups of the 4 x 64 grid
+
+__global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, double* __restrict__ Ts,
+                                                             double* __restrict__ Dinvs) {
+    __shared__ double R[kBtdMaxM][3 * kBtdMaxM + 1];          // [D | U | I] -> [. | W | D^-1]
     __shared__ double Lk[kBtdMaxM][kBtdMaxM + 1];
-    __shared__ double R[kBtdMaxM][kW];                        // [D | U | X] -> [. | W | Y]
-    __shared__ double P[kBtdMaxM][kBtdMaxM + kBtdMaxRhs + 1]; // [W_{k-1} | Y_{k-1}]
+    __shared__ double Wp[kBtdMaxM][kBtdMaxM + 1];             // W_{k-1}
     __shared__ int piv_s;
     const int tid = threadIdx.x, tj = tid & 63, ti = tid >> 6;
     const size_t mm = (size_t)m * m;
     double* T = Ts + (size_t)blockIdx.x * nb * 3 * mm;
-    double* X = Xs + (size_t)blockIdx.x * nb * m * nrhs;
-    const int nc = m + nrhs;                                  // columns of [W | Y]
-    const int na = m + nc;                                    // columns of the augmented block
+    double* Dinv = Dinvs + (size_t)blockIdx.x * nb * mm;
+    const int na = 3 * m;
 
     for (int k = 0; k < nb; ++k) {
         const double* Lg = T + ((size_t)k * 3 + 0) * mm;
-        const double* Dg = T + ((size_t)k * 3 + 1) * mm;
+        double* Dg = T + ((size_t)k * 3 + 1) * mm;
         double* Ug = T + ((size_t)k * 3 + 2) * mm;
-        double* Xg = X + (size_t)k * m * nrhs;
         const bool last = k == nb - 1;
         for (int i = ti; i < m; i += kRG) {
             for (int j = tj; j < m; j += 64) {
                 R[i][j] = Dg[i * m + j];
                 R[i][m + j] = last ? 0.0 : Ug[i * m + j];
-                Lk[i][j] = k > 0 ? Lg[i * m + j] : 0.0;
+                R[i][2 * m + j] = i == j ? 1.0 : 0.0;
+                if (k > 0) Lk[i][j] = Lg[i * m + j];
             }
-            for (int j = tj; j < nrhs; j += 64) R[i][2 * m + j] = Xg[i * nrhs + j];
         }
         __syncthreads();
-        if (k > 0) {                                          // D -= L W_{k-1},  X -= L Y_{k-1}
+        if (k > 0) {                                          // D -= L_k W_{k-1}
             for (int i = ti; i < m; i += kRG) {
-                for (int j = tj; j < nc; j += 64) {
-                    const int jr = j < m ? j : m + j;         // column of R
-                    double acc = R[i][jr];
-                    for (int c = 0; c < m; ++c) acc -= Lk[i][c] * P[c][j];
-                    R[i][jr] = acc;
+                for (int j = tj; j < m; j += 64) {
+                    double acc = R[i][j];
+                    for (int c = 0; c < m; ++c) acc -= Lk[i][c] * Wp[c][j];
+                    R[i][j] = acc;
                 }
             }
             __syncthreads();
         }
-        for (int c = 0; c < m; ++c) {                         // Gauss-Jordan with partial pivoting
+        for (int i = ti; i < m; i += kRG)                     // keep D'_k for the solves' refinement
+            for (int j = tj; j < m; j += 64) Dg[i * m + j] = R[i][j];
+        for (int c = 0; c < m; ++c) {                         // Gauss-Jordan, partial pivoting
             if (ti == 0) {
-                double best = (tj >= c && tj < m) ? fabs(R[tj][c]) : -1.0;
-                int bi = tj;
+                double best = -1.0;
+                int bi = c;
+                for (int r = c + tj; r < m; r += 64) {
+                    const double v = fabs(R[r][c]);
+                    if (v > best) { best = v; bi = r; }
+                }
                 for (int off = 32; off > 0; off >>= 1) {
                     const double ob = __shfl_xor(best, off);
                     const int oi = __shfl_xor(bi, off);
@@ -289,8 +301,8 @@ __global__ __launch_bounds__(kThreads) void btd_solve_kernel(int nb, int m, int 
                 __syncthreads();
             }
             const double rd = 1.0 / R[c][c];
-            for (int i = ti; i < m; i += kRG) {               // rows != c: eliminate with the
-                if (i == c) continue;                         // unscaled pivot row
+            for (int i = ti; i < m; i += kRG) {
+                if (i == c) continue;
                 const double f = R[i][c] * rd;
                 for (int j = c + 1 + tj; j < na; j += 64) R[i][j] -= f * R[c][j];
             }
@@ -299,37 +311,101 @@ __global__ __launch_bounds__(kThreads) void btd_solve_kernel(int nb, int m, int 
             __syncthreads();
         }
         for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < nc; j += 64) {
-                const double v = R[i][m + j];
-                P[i][j] = v;
-                if (j < m) {
-                    if (!last) Ug[i * m + j] = v;
-                } else {
-                    Xg[i * nrhs + (j - m)] = v;
-                }
+            for (int j = tj; j < m; j += 64) {
+                Wp[i][j] = R[i][m + j];
+                if (!last) Ug[i * m + j] = R[i][m + j];
+                Dinv[(size_t)k * mm + i * m + j] = R[i][2 * m + j];
             }
         }
         __syncthreads();
     }
-    // back substitution: P holds Y_{nb-1} = x_{nb-1} in its right-hand-side columns
-    for (int k = nb - 2; k >= 0; --k) {
-        const double* Wg = T + ((size_t)k * 3 + 2) * mm;
-        double* Xg = X + (size_t)k * m * nrhs;
-        for (int i = ti; i < m; i += kRG)
-            for (int j = tj; j < m; j += 64) Lk[i][j] = Wg[i * m + j];
+}
+
+__global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int ldx, int j0, int w,
+                                                            const double* __restrict__ Ts,
+                                                            const double* __restrict__ Dinvs,
+                                                            double* __restrict__ Xs) {
+    __shared__ double A[kBtdMaxM][kBtdMaxM + 1];
+    __shared__ double Dp[kBtdMaxM][kBtdMaxM + 1];
+    __shared__ double Y[kBtdMaxM][kBtdMaxRhs + 1];
+    __shared__ double Z[kBtdMaxM][kBtdMaxRhs + 1];
+    __shared__ double Q[kBtdMaxM][kBtdMaxRhs + 1];
+    const int tid = threadIdx.x, tj = tid & 63, ti = tid >> 6;
+    const size_t mm = (size_t)m * m;
+    const double* T = Ts + (size_t)blockIdx.x * nb * 3 * mm;
+    const double* Dinv = Dinvs + (size_t)blockIdx.x * nb * mm;
+    double* X = Xs + (size_t)blockIdx.x * nb * m * ldx + j0;
+
+    for (int k = 0; k < nb; ++k) {                            // forward: Y_k
+        double* Xk = X + (size_t)k * m * ldx;
+        for (int i = ti; i < m; i += kRG) {
+            for (int j = tj; j < w; j += 64) Z[i][j] = Xk[(size_t)i * ldx + j];
+            if (k > 0)
+                for (int j = tj; j < m; j += 64) A[i][j] = T[((size_t)k * 3 + 0) * mm + i * m + j];
+        }
+        __syncthreads();
+        if (k > 0) {
+            for (int i = ti; i < m; i += kRG) {
+                for (int j = tj; j < w; j += 64) {
+                    double acc = Z[i][j];
+                    for (int c = 0; c < m; ++c) acc -= A[i][c] * Y[c][j];
+                    Z[i][j] = acc;
+                }
+            }
+            __syncthreads();
+        }
+        for (int i = ti; i < m; i += kRG) {
+            for (int j = tj; j < m; j += 64) {
+                A[i][j] = Dinv[(size_t)k * mm + i * m + j];
+                Dp[i][j] = T[((size_t)k * 3 + 1) * mm + i * m + j];
+            }
+        }
+        __syncthreads();
+        for (int i = ti; i < m; i += kRG) {                   // Y = D'^-1 Z
+            for (int j = tj; j < w; j += 64) {
+                double acc = 0.0;
+                for (int c = 0; c < m; ++c) acc += A[i][c] * Z[c][j];
+                Y[i][j] = acc;
+            }
+        }
+        __syncthreads();
+        for (int i = ti; i < m; i += kRG) {                   // one refinement step: Q = Z - D' Y
+            for (int j = tj; j < w; j += 64) {
+                double acc = Z[i][j];
+                for (int c = 0; c < m; ++c) acc -= Dp[i][c] * Y[c][j];
+                Q[i][j] = acc;
+            }
+        }
+        __syncthreads();
+        for (int i = ti; i < m; i += kRG) {                   // Y += D'^-1 Q
+            for (int j = tj; j < w; j += 64) {
+                double acc = Y[i][j];
+                for (int c = 0; c < m; ++c) acc += A[i][c] * Q[c][j];
+                Y[i][j] = acc;
+                Xk[(size_t)i * ldx + j] = acc;
+            }
+        }
+        __syncthreads();
+    }
+    for (int k = nb - 2; k >= 0; --k) {                       // backward: x_k = Y_k - W_k x_{k+1}
+        double* Xk = X + (size_t)k * m * ldx;
+        for (int i = ti; i < m; i += kRG) {
+            for (int j = tj; j < m; j += 64) A[i][j] = T[((size_t)k * 3 + 2) * mm + i * m + j];
+            for (int j = tj; j < w; j += 64) Z[i][j] = Xk[(size_t)i * ldx + j];
+        }
         __syncthreads();
         for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < nrhs; j += 64) {
-                double acc = Xg[i * nrhs + j];
-                for (int c = 0; c < m; ++c) acc -= Lk[i][c] * P[c][m + j];
-                R[i][j] = acc;
+            for (int j = tj; j < w; j += 64) {
+                double acc = Z[i][j];
+                for (int c = 0; c < m; ++c) acc -= A[i][c] * Y[c][j];
+                Z[i][j] = acc;
             }
         }
         __syncthreads();
         for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < nrhs; j += 64) {
-                P[i][m + j] = R[i][j];
-                Xg[i * nrhs + j] = R[i][j];
+            for (int j = tj; j < w; j += 64) {
+                Y[i][j] = Z[i][j];
+                Xk[(size_t)i * ldx + j] = Z[i][j];
             }
         }
         __syncthreads();
@@ -480,15 +556,36 @@ int awelu_solve_batched(int n, int nrhs, int batch, const double* LU, const int*
     return 0;
 }
 
-// Block-tridiagonal systems: T[b][nb][3][m][m] (sub-, main, super-diagonal block of each block
-// row; the sub-diagonal block of row 0 and the super-diagonal block of row nb-1 are ignored),
-// X[b][nb][m][nrhs] right-hand sides, solved in place; T is overwritten.  m <= 32, nrhs <= 8.
-int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, double* T, double* X, void* stream) {
-    if (nb < 1 || m < 1 || m > kBtdMaxM || nrhs < 1 || nrhs > kBtdMaxRhs || batch < 1 || !T || !X) {
-        g_err = "need nb >= 1, 1 <= m <= 32, 1 <= nrhs <= 8, batch >= 1 and device pointers";
+// Block-tridiagonal factorisation: T[b][nb][3][m][m] (sub-, main, super-diagonal block of each
+// block row; the sub-diagonal block of row 0 and the super-diagonal block of row nb-1 are
+// ignored), m <= 56.  In place: the super-diagonal blocks become W_k = D'_k^-1 U_k; Dinv[b][nb][m][m]
+// receives the inverted pivot blocks D'_k^-1.
+int awelu_btd_factor_batched(int nb, int m, int batch, double* T, double* Dinv, void* stream) {
+    if (nb < 1 || m < 1 || m > kBtdMaxM || batch < 1 || !T || !Dinv) {
+        g_err = "need nb >= 1, 1 <= m <= 56, batch >= 1 and device pointers";
         return 1;
     }
-    btd_solve_kernel<<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, nrhs, T, X);
+    btd_factor_kernel<<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, T, Dinv);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// X[b] <- T[b]^-1 X[b] with the factors of awelu_btd_factor_batched; X[b][nb m][nrhs] row-major,
+// solved in place (64 right-hand sides per pass).
+int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, const double* T, const double* Dinv, double* X,
+                            void* stream) {
+    if (nb < 1 || m < 1 || m > kBtdMaxM || nrhs < 1 || batch < 1 || !T || !Dinv || !X) {
+        g_err = "need nb >= 1, 1 <= m <= 56, nrhs >= 1, batch >= 1 and device pointers";
+        return 1;
+    }
+    for (int j0 = 0; j0 < nrhs; j0 += kBtdMaxRhs) {
+        const int w = std::min(kBtdMaxRhs, nrhs - j0);
+        btd_apply_kernel<<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, nrhs, j0, w, T, Dinv, X);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

@@ -64,6 +64,7 @@ class IpmOptions:
     max_backtracks: int = 40
     kkt: str = "structured"          # "structured" (interval elimination + Schur) or "dense"
     lu_backend: str = "awelu"        # interval-block LU: "awelu" (batched_lu.hip) or "torch" (rocSOLVER)
+    separators: str = "dense"        # separator system: "dense" LU or "btd" (awebox_amd/btd.py block sweep)
     profile: bool = False            # synchronise and time the solver's phases (IpmResult.timing)
     verbose: bool = False
 
@@ -220,7 +221,7 @@ class StructuredKKT:
         S = K_SS - sum_k K_SI^k (K_II^k)^-1 K_IS^k,
     about 5 GFLOP at N=40 instead of the 1.3 TFLOP of a dense LU of the whole system."""
 
-    def __init__(self, nlp, lay, dev, lu_backend="awelu"):
+    def __init__(self, nlp, lay, dev, lu_backend="awelu", separators="btd"):
         n, ny, m = nlp.n, nlp.ny, nlp.m
         self.lu_backend = lu_backend
         N = ny + m
@@ -292,6 +293,38 @@ class StructuredKKT:
         self.schur_flat = (r_idx * (nS + 1) + c_idx).reshape(-1)
         int_p = np.where(owner >= 0)[0]
         self.int_p = torch.tensor(int_p, device=dev)
+        # separators in stages [c[k-1], x[k]] (block tridiagonal, globals as border): pairing each
+        # shooting state with the multipliers of the continuity row that defines it keeps the block
+        # sweep's pivot blocks regular -- the finer order x[0], c[0], x[1], ... meets near-singular
+        # pivot blocks at N=40 (cond 3e17 on the AP2 KKT); the paired one stays at cond <= 1e13
+        # with |W_k| <= 60, a backward error of 2e-21 (emulated on the CPU)
+        self.btd = None
+        self.force_btd = False                                  # CPU tests: the BTD path on host
+        from .batched_lu import BTD_MAX_M
+        if lu_backend == "awelu" and separators == "btd" and 2 * nx <= BTD_MAX_M:
+            stage_of = np.full(self.nS, -1, dtype=np.int64)
+            pos_of = np.zeros(self.nS, dtype=np.int64)
+            free = np.asarray(nlp.free.cpu().numpy() if torch.is_tensor(nlp.free) else nlp.free)
+            for q, p in enumerate(sep):
+                if p < n:
+                    v = int(free[p])
+                    if v >= v0:
+                        k, o = divmod(v - v0, stride)
+                        if o < nx and k <= n_k:
+                            stage_of[q], pos_of[q] = k, nx + o
+                elif p >= ny:
+                    r = p - ny
+                    if r < n_k * rows and r % rows >= rows - nx:
+                        stage_of[q], pos_of[q] = r // rows + 1, r % rows - (rows - nx)
+            ss_r, ss_c = sep_id[P_[ss]], sep_id[Q_[ss]]
+            sch_r, sch_c = lsep_arr[:, :, None].repeat(L, 2), lsep_arr[:, None, :].repeat(L, 1)
+            from .btd import BorderedBtd
+            try:
+                self.btd = BorderedBtd(stage_of, pos_of, n_k + 1, 2 * nx,
+                                       np.concatenate([ss_r, sch_r.reshape(-1)]),
+                                       np.concatenate([ss_c, sch_c.reshape(-1)]), dev)
+            except ValueError:
+                self.btd = None                                 # not stage-structured: dense S
         self.int_flat = torch.tensor(owner[int_p] * nI + loc[int_p], device=dev)
         self.sep_p = torch.tensor(sep, device=dev)
 
@@ -310,21 +343,27 @@ class StructuredKKT:
         KIS = torch.zeros(n_k * nI * L, **f64)
         KIS.index_put_((self.dst_is,), vals[self.sel_is], accumulate=True)
         KIS = KIS.view(n_k, nI, L)
-        S = torch.zeros((nS + 1) * (nS + 1), **f64)
-        S.index_put_((self.dst_ss,), vals[self.sel_ss], accumulate=True)
-        if self.lu_backend == "awelu" and KII.is_cuda:      # the CPU test harness uses LAPACK
+        self.awelu = self.lu_backend == "awelu" and KII.is_cuda   # the CPU test harness uses LAPACK
+        if self.awelu:
             from .batched_lu import lu_factor
             self.LU_I, self.piv_I = lu_factor(KII)
         else:
             self.LU_I, self.piv_I = torch.linalg.lu_factor(KII)
-        self.X = torch.linalg.lu_solve(self.LU_I, self.piv_I, KIS)            # K_II^-1 K_IS
+        self.X = self._block_solve(KIS)                                        # K_II^-1 K_IS
         T = KIS.transpose(1, 2) @ self.X                                       # [n_k, L, L]
+        self.KIS = KIS
+        if self.btd is not None and (KII.is_cuda or self.force_btd):
+            self.btd.factor(torch.cat([vals[self.sel_ss], -T.reshape(-1)]))
+            self.use_btd = True
+            return
+        self.use_btd = False
+        S = torch.zeros((nS + 1) * (nS + 1), **f64)
+        S.index_put_((self.dst_ss,), vals[self.sel_ss], accumulate=True)
         S.index_put_((self.schur_flat,), -T.reshape(-1), accumulate=True)
         S = S.view(nS + 1, nS + 1)
         S[nS, :] = 0.0
         S[:, nS] = 0.0
         S[nS, nS] = 1.0
-        self.KIS = KIS
         self.LU_S, self.piv_S = torch.linalg.lu_factor(S)
 
     def matvec(self, x):
@@ -339,12 +378,15 @@ class StructuredKKT:
         self.n_solve += 1
         x = self._solve(rhs)
         b_norm = float(rhs.abs().max().item())
+        self.backward = []
         for _ in range(refine + 1):
             r = rhs - self.matvec(x)
             err = float(r.abs().max().item())
             if not math.isfinite(err):
                 break
-            if err <= rtol * (self.k_norm * float(x.abs().max().item()) + b_norm):
+            scale = self.k_norm * float(x.abs().max().item()) + b_norm
+            self.backward.append(err / scale)
+            if err <= rtol * scale:
                 return x
             x = x + self._solve(r)
         # ill-conditioned interior pivots: one dense LU of the assembled K for this system
@@ -352,6 +394,16 @@ class StructuredKKT:
         K = torch.zeros(self.N * self.N, dtype=torch.float64, device=self.dev)
         K.index_put_((self.P_ * self.N + self.Q_,), self.vals, accumulate=True)
         return torch.linalg.solve(K.view(self.N, self.N), rhs)
+
+    def _block_solve(self, B):
+        """K_II^-1 B for all interval blocks: the awelu solve kernel (LDS-resident right-hand
+        sides) for a few right-hand sides on the device; rocBLAS trsm for the many columns of
+        K_IS (the LDS-resident kernel re-streams the factors once per 12-68 columns, which loses to
+        trsm at n = 640); LAPACK in the CPU harness."""
+        if self.awelu and B.shape[-1] <= 8:
+            from .batched_lu import lu_solve
+            return lu_solve(self.LU_I, self.piv_I, B)
+        return torch.linalg.lu_solve(self.LU_I, self.piv_I, B)
 
     def _solve(self, rhs):
         f64 = dict(dtype=torch.float64, device=self.dev)
@@ -361,11 +413,15 @@ class StructuredKKT:
         rI = rI.view(n_k, nI, 1)
         rS = torch.zeros(nS + 1, **f64)
         rS[:nS] = rhs[self.sep_p]
-        z = torch.linalg.lu_solve(self.LU_I, self.piv_I, rI)                  # [n_k, nI, 1]
+        z = self._block_solve(rI)                                              # [n_k, nI, 1]
         upd = (self.KIS.transpose(1, 2) @ z).reshape(-1)                      # [n_k * L]
         rS = rS.index_add(0, self.lsep.reshape(-1), -upd)
         rS[nS] = 0.0
-        xS = torch.linalg.lu_solve(self.LU_S, self.piv_S, rS.view(-1, 1)).view(-1)
+        if self.use_btd:
+            xS = torch.zeros(nS + 1, **f64)
+            xS[:nS] = self.btd.solve(rS[:nS])
+        else:
+            xS = torch.linalg.lu_solve(self.LU_S, self.piv_S, rS.view(-1, 1)).view(-1)
         xI = z.view(n_k, nI) - (self.X @ xS[self.lsep].unsqueeze(-1)).view(n_k, nI)
         sol = torch.empty(self.N, **f64)
         sol[self.int_p] = xI.reshape(-1)[self.int_flat]
@@ -451,7 +507,7 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
     skkt = None
     if opts.kkt == "structured" and getattr(ev, "layout", None) is not None:
         try:
-            skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend)
+            skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators)
         except ValueError:
             skkt = None
     K = torch.zeros(N, N, **f64) if skkt is None else None

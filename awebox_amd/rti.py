@@ -323,9 +323,10 @@ class BatchedRti:
 
     @staticmethod
     def _btd(T, X):
-        from .batched_lu import btd_dense, btd_solve
+        from .batched_lu import btd_dense, btd_factor, btd_solve
         if T.is_cuda:
-            return btd_solve(T, X)
+            F, Dinv = btd_factor(T)
+            return btd_solve(F, Dinv, X)
         b, nb, m, nrhs = X.shape
         return torch.linalg.solve(btd_dense(T), X.reshape(b, nb * m, nrhs)).view(b, nb, m, nrhs)
 

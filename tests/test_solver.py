@@ -36,9 +36,57 @@ def test_homotopy_on_cpu_port():
     _check_solution(consts, lay, V, summary)
 
 
-@pytest.mark.parametrize("delta_c", [0.0, 1e-6])
-def test_structured_kkt_matches_dense(delta_c):
-    """Interval elimination + Schur complement solves the same KKT system as a dense LU."""
+def _kkt_case(device, evaluator, n_k=5, d=3):
+    import torch
+    from awebox_amd.ipm import DeviceNlp, StructuredKKT, _dense_A
+    consts = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+    lay = pb.NlpLayout(n_k, d)
+    v0 = initial_guess(consts, lay)
+    st = hm.schedule(consts, lay, v0)[0]
+    lbg, ubg = lay.g_bounds()
+    nlp = DeviceNlp(evaluator(consts), pb.pack_p(lay, consts, v0, step=st.cost_step), st.lbx, st.ubx,
+                    lbg, ubg, device)
+    sk = StructuredKKT(nlp, lay, device)
+    gen = torch.Generator().manual_seed(1)
+    f64 = dict(dtype=torch.float64)
+    hv = torch.randn(len(nlp.h_keep), generator=gen, **f64).to(device)
+    jv = torch.randn(len(nlp.j_row), generator=gen, **f64).to(device)
+    diag = (torch.rand(nlp.ny, generator=gen, **f64) + 1.0).to(device)
+    N, ny = sk.N, nlp.ny
+    K = torch.zeros(N, N, dtype=torch.float64, device=device)
+    K[nlp.h_r, nlp.h_c] = hv
+    K[nlp.h_c[nlp.h_offdiag], nlp.h_r[nlp.h_offdiag]] = hv[nlp.h_offdiag]
+    i = torch.arange(ny, device=device)
+    K[i, i] += diag
+    _dense_A(nlp, jv, ny, K)
+    rhs = torch.randn(N, generator=gen, **f64).to(device)
+    return nlp, sk, hv, jv, diag, K, rhs
+
+
+@pytest.mark.gpu
+def test_structured_kkt_btd_on_gpu():
+    """The GPU separator path (awelu block sweep + border) against the dense LU of the same KKT
+    matrix, without refinement: the first elimination solve's backward error."""
+    import torch
+    from awebox_amd.evaluator import Ap2Evaluator
+    nlp, sk, hv, jv, diag, K, rhs = _kkt_case("cuda", lambda c: Ap2Evaluator(c, batch=1))
+    sk.factor(hv, diag, jv, 0.0, nlp.mI)
+    assert sk.use_btd
+    x = sk._solve(rhs)
+    backward = (K @ x - rhs).abs().max().item() / (K.abs().sum(1).max().item() * x.abs().max().item()
+                                                    + rhs.abs().max().item())
+    x_ref = torch.linalg.solve(K.cpu(), rhs.cpu())
+    fwd = (x.cpu() - x_ref).abs().max().item() / x_ref.abs().max().item()
+    print(f"backward {backward:.3e} forward {fwd:.3e}")
+    assert backward <= 1e-12
+    assert fwd <= 1e-6
+
+
+@pytest.mark.parametrize("delta_c,btd", [(0.0, False), (1e-6, False), (0.0, True), (1e-6, True)])
+def test_structured_kkt_matches_dense(delta_c, btd):
+    """Interval elimination + Schur complement solves the same KKT system as a dense LU; with
+    btd=True the separators go through the bordered block-tridiagonal path (awebox_amd/btd.py,
+    its host fallback), which the GPU solver uses."""
     import torch
     from oracle.cpu_device import CpuDeviceEvaluator
     from awebox_amd.ipm import DeviceNlp, StructuredKKT, _dense_A
@@ -52,6 +100,8 @@ def test_structured_kkt_matches_dense(delta_c):
                     lbg, ubg, "cpu")
     sk = StructuredKKT(nlp, lay, "cpu")
     assert sk.nS < sk.N // 4
+    assert sk.btd is not None and sk.btd.nb == n_k + 1 and sk.btd.m == 2 * pb.NX and sk.btd.nG < 2 * pb.NX
+    sk.force_btd = btd
     gen = torch.Generator().manual_seed(1)
     f64 = dict(dtype=torch.float64)
     hv = torch.randn(len(nlp.h_keep), generator=gen, **f64)
@@ -69,7 +119,7 @@ def test_structured_kkt_matches_dense(delta_c):
     rhs = torch.randn(N, generator=gen, **f64)
     sk.factor(hv, diag, jv, delta_c, nlp.mI)
     x = sk.solve(rhs)
-    assert sk.n_dense == 0
+    assert sk.n_dense == 0 and sk.use_btd == btd
     backward = (K @ x - rhs).abs().max().item() / (K.abs().sum(1).max().item() * x.abs().max().item()
                                                     + rhs.abs().max().item())
     assert backward <= 1e-12

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--kkt", default="structured")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--separators", default="dense", help="separator solve of the structured KKT: dense | btd")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -39,14 +40,15 @@ def main():
     st = hm.schedule(consts, lay, v0)[0]
     lbg, ubg = lay.g_bounds()
     P = pb.pack_p(lay, consts, v0, step=st.cost_step)
-    opts = hippo_options("initial", IpmOptions(max_iter=args.iters, kkt=args.kkt, profile=True))
+    opts = hippo_options("initial", IpmOptions(max_iter=args.iters, kkt=args.kkt, profile=True,
+                                                      separators=args.separators))
     res = solve(ev, P, v0, st.lbx, st.ubx, lbg, ubg, opts=opts, device=args.device)
     out = {"iterations": res.iterations, "status": res.status, "seconds": res.seconds,
            "timing": res.timing, "kkt_solves": res.kkt_solves, "kkt_dense": res.kkt_dense}
     print(json.dumps(out, indent=1), flush=True)
     # one factor + solve in isolation
     nlp = DeviceNlp(ev, P, st.lbx, st.ubx, lbg, ubg, args.device)
-    sk = StructuredKKT(nlp, lay, args.device)
+    sk = StructuredKKT(nlp, lay, args.device, separators=args.separators)
     x = torch.tensor(v0[nlp.free], device=args.device)
     f, grad, g, jv = nlp.eval_all(x)
     hv = nlp.hess(x, torch.zeros(nlp.m, dtype=torch.float64, device=args.device))
@@ -55,6 +57,8 @@ def main():
     for _ in range(2):
         sk.factor(hv, diag, jv, 0.0, nlp.mI)
         sk.solve(rhs)
+    print(json.dumps({"separator_path": "btd" if getattr(sk, "use_btd", False) else "dense",
+                      "backward_errors": sk.backward, "n_dense": sk.n_dense}), flush=True)
     sync = torch.cuda.synchronize if args.device == "cuda" else (lambda: None)
     sync()
     t = time.perf_counter()
