@@ -6,8 +6,8 @@
 // the KKT factorisation 85 % of a dual-kite interior-point iteration.  Here one workgroup
 // factorises one matrix with a right-looking blocked algorithm:
 //   * panel of NB = 16 columns staged in LDS (n x 16 doubles, <= 128 KB for n <= 1024), factorised
-//     there with partial pivoting (column max by a workgroup reduction, row swap, scale, rank-1
-//     update of the panel);
+//     there with partial pivoting (column max by wave shuffles and one exchange of the four wave
+//     maxima through LDS, row swap, scale, rank-1 update of the panel: three barriers per column);
 //   * the panel's row interchanges applied to the rest of the row (global memory);
 //   * one thread per trailing column: the column's 16 U12 entries by forward substitution with
 //     L11 (LDS, broadcast reads), then the trailing update A22 -= L21 U12 of that column with
@@ -31,8 +31,8 @@ thread_local std::string g_err;
 
 __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __restrict__ As, int* __restrict__ pivs) {
     extern __shared__ double panel[];                   // [n][kNB], row-major
-    __shared__ double red_v[kThreads];
-    __shared__ int red_i[kThreads];
+    __shared__ double red_v[kThreads / 64];
+    __shared__ int red_i[kThreads / 64];
     __shared__ int piv_loc[kNB];
     double* A = As + (size_t)blockIdx.x * n * n;
     int* piv = pivs + (size_t)blockIdx.x * n;
@@ -55,18 +55,22 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
                 const double v = fabs(panel[r * kNB + c]);
                 if (v > best) { best = v; bi = r; }
             }
-            red_v[tid] = best;
-            red_i[tid] = bi;
-            __syncthreads();
-            for (int s = kThreads / 2; s > 0; s >>= 1) {
-                if (tid < s) {
-                    const double o = red_v[tid + s];
-                    const int oi = red_i[tid + s];
-                    if (o > red_v[tid] || (o == red_v[tid] && oi < red_i[tid])) { red_v[tid] = o; red_i[tid] = oi; }
-                }
-                __syncthreads();
+            for (int off = 32; off > 0; off >>= 1) {         // wave reduction by shuffles
+                const double ob = __shfl_xor(best, off);
+                const int oi = __shfl_xor(bi, off);
+                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
             }
-            const int p = red_i[0];
+            if ((tid & 63) == 0) {
+                red_v[tid >> 6] = best;
+                red_i[tid >> 6] = bi;
+            }
+            __syncthreads();
+            best = red_v[0];
+            bi = red_i[0];
+            for (int w = 1; w < kThreads / 64; ++w) {         // the 4 wave results, same order everywhere
+                if (red_v[w] > best || (red_v[w] == best && red_i[w] < bi)) { best = red_v[w]; bi = red_i[w]; }
+            }
+            const int p = bi;
             if (tid == 0) piv_loc[c] = p;
             if (p != c && tid < kb) {                        // swap panel rows c and p
                 const double a = panel[c * kNB + tid];
@@ -89,17 +93,16 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
             A[(size_t)(k0 + r) * n + k0 + c] = panel[r * kNB + c];
         }
         if (tid < kb) piv[k0 + tid] = k0 + piv_loc[tid] + 1;
-        for (int c = 0; c < kb; ++c) {
-            const int p = piv_loc[c];
-            if (p == c) continue;
-            const size_t ra = (size_t)(k0 + c) * n, rb = (size_t)(k0 + p) * n;
-            for (int j = tid; j < n; j += kThreads) {
-                if (j >= k0 && j < k0 + kb) continue;
+        for (int j = tid; j < n; j += kThreads) {            // interchanges outside the panel: each
+            if (j >= k0 && j < k0 + kb) continue;            // thread owns its columns, no barriers
+            for (int c = 0; c < kb; ++c) {
+                const int p = piv_loc[c];
+                if (p == c) continue;
+                const size_t ra = (size_t)(k0 + c) * n, rb = (size_t)(k0 + p) * n;
                 const double a = A[ra + j];
                 A[ra + j] = A[rb + j];
                 A[rb + j] = a;
             }
-            __syncthreads();
         }
         __syncthreads();
         // ---- U12 (forward substitution with L11) and the trailing update, one column per thread --
@@ -212,7 +215,6 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
 }
 
 constexpr size_t kSolveLds = 144 * 1024;
-constexpr int kWaveMaxN = 64;
 
 // Block-tridiagonal systems, one workgroup per system: nb diagonal blocks of m x m (m <= 56),
 // T[b][k][3][m][m] = (sub-diagonal block L_k = (k, k-1), diagonal block D_k, super-diagonal block
@@ -412,94 +414,6 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
     }
 }
 
-// Single-wavefront variant of lu_batched_kernel for n <= 64 (the RTI plant's collocation blocks,
-// n = 60), where three of a 4-wave workgroup's waves would idle: the pivot search is a shuffle
-// reduction and the row interchanges need no barriers (each lane owns its columns).  Measured on
-// MI355X at n = 126 (5,120 blocks) it is slower than the 4-wave kernel (3.19 vs 2.74 ms), at
-// n = 60 (256 blocks) equal (0.150 vs 0.157 ms), hence the cut-off.
-__global__ __launch_bounds__(64) void lu_wave_kernel(int n, double* __restrict__ As, int* __restrict__ pivs) {
-    extern __shared__ double panel[];                   // [n][kNB]
-    __shared__ int piv_loc[kNB];
-    double* A = As + (size_t)blockIdx.x * n * n;
-    int* piv = pivs + (size_t)blockIdx.x * n;
-    const int lane = threadIdx.x;
-
-    for (int k0 = 0; k0 < n; k0 += kNB) {
-        const int kb = min(kNB, n - k0), rows = n - k0;
-        for (int t = lane; t < rows * kb; t += 64) {
-            const int r = t / kb, c = t % kb;
-            panel[r * kNB + c] = A[(size_t)(k0 + r) * n + k0 + c];
-        }
-        __syncthreads();
-        for (int c = 0; c < kb; ++c) {
-            double best = -1.0;
-            int bi = c;
-            for (int r = c + lane; r < rows; r += 64) {
-                const double v = fabs(panel[r * kNB + c]);
-                if (v > best) { best = v; bi = r; }
-            }
-            for (int off = 32; off > 0; off >>= 1) {
-                const double ob = __shfl_xor(best, off);
-                const int oi = __shfl_xor(bi, off);
-                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-            }
-            const int p = bi;
-            if (lane == 0) piv_loc[c] = p;
-            if (p != c && lane < kb) {
-                const double a = panel[c * kNB + lane];
-                panel[c * kNB + lane] = panel[p * kNB + lane];
-                panel[p * kNB + lane] = a;
-            }
-            __syncthreads();
-            const double rd = 1.0 / panel[c * kNB + c];
-            for (int r = c + 1 + lane; r < rows; r += 64) {
-                const double l = panel[r * kNB + c] * rd;
-                panel[r * kNB + c] = l;
-                for (int j = c + 1; j < kb; ++j) panel[r * kNB + j] -= l * panel[c * kNB + j];
-            }
-            __syncthreads();
-        }
-        for (int t = lane; t < rows * kb; t += 64) {
-            const int r = t / kb, c = t % kb;
-            A[(size_t)(k0 + r) * n + k0 + c] = panel[r * kNB + c];
-        }
-        if (lane < kb) piv[k0 + lane] = k0 + piv_loc[lane] + 1;
-        for (int j = lane; j < n; j += 64) {                 // interchanges outside the panel
-            if (j >= k0 && j < k0 + kb) continue;
-            for (int c = 0; c < kb; ++c) {
-                const int p = piv_loc[c];
-                if (p == c) continue;
-                const size_t ra = (size_t)(k0 + c) * n, rb = (size_t)(k0 + p) * n;
-                const double a = A[ra + j];
-                A[ra + j] = A[rb + j];
-                A[rb + j] = a;
-            }
-        }
-        __syncthreads();
-        for (int j = k0 + kb + lane; j < n; j += 64) {
-            double u[kNB];
-#pragma unroll
-            for (int r = 0; r < kNB; ++r) {
-                if (r < kb) {
-                    double v = A[(size_t)(k0 + r) * n + j];
-                    for (int c = 0; c < r; ++c) v -= panel[r * kNB + c] * u[c];
-                    u[r] = v;
-                    A[(size_t)(k0 + r) * n + j] = v;
-                } else {
-                    u[r] = 0.0;
-                }
-            }
-            for (int i = kb; i < rows; ++i) {
-                double acc = A[(size_t)(k0 + i) * n + j];
-#pragma unroll
-                for (int c = 0; c < kNB; ++c) acc -= panel[i * kNB + c] * u[c];
-                A[(size_t)(k0 + i) * n + j] = acc;
-            }
-        }
-        __syncthreads();
-    }
-}
-
 }  // namespace
 
 extern "C" {
@@ -514,10 +428,7 @@ int awelu_factor_batched(int n, int batch, double* A, int* piv, void* stream) {
         return 1;
     }
     const size_t lds = sizeof(double) * (size_t)n * kNB;
-    if (n <= kWaveMaxN)
-        lu_wave_kernel<<<dim3((unsigned)batch), 64, lds, (hipStream_t)stream>>>(n, A, piv);
-    else
-        lu_batched_kernel<<<dim3((unsigned)batch), kThreads, lds, (hipStream_t)stream>>>(n, A, piv);
+    lu_batched_kernel<<<dim3((unsigned)batch), kThreads, lds, (hipStream_t)stream>>>(n, A, piv);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);
