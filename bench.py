@@ -51,6 +51,43 @@ def kernel_source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+SOURCES = {   # the files each evaluator kernel is built from (a PMC record is tied to their hash)
+    "ap2": ["awebox_amd/csrc/ap2_model.hpp", "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/awegpu.hip",
+            "awebox_amd/csrc/scalar.hpp", "include/awegpu.h"],
+    "dual": ["awebox_amd/csrc/dual_model.hpp", "awebox_amd/csrc/dual_tables.hpp", "awebox_amd/csrc/awedual.hip",
+             "awebox_amd/csrc/ap2_model.hpp", "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/scalar.hpp",
+             "include/awedual.h", "include/awegpu.h"],
+    "mpc": ["awebox_amd/csrc/kite3_model.hpp", "awebox_amd/csrc/kite3_tables.hpp", "awebox_amd/csrc/awempc.hip",
+            "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/scalar.hpp", "include/awempc.h", "include/awegpu.h"],
+}
+PMC_RECORD_CONFIGS = os.path.join(ROOT, "profiles", "pmc_traffic_configs.json")
+
+
+def sources_hash(which: str) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for rel in SOURCES[which]:
+        with open(os.path.join(ROOT, rel), "rb") as fh:
+            h.update(os.path.basename(rel).encode() + fh.read())
+    return h.hexdigest()[:16]
+
+
+def config_traffic(which: str, batch: int, kernel_ms: float):
+    """HBM traffic of the config-3 / config-5 kernels from their committed PMC record (2 x FETCH_SIZE
+    + WRITE_SIZE per dispatch, the gfx950 correction of MI355X_MICROARCH.md), or None when the
+    record is missing or was taken on other sources or another batch size."""
+    try:
+        with open(PMC_RECORD_CONFIGS) as fh:
+            rec = json.load(fh).get(which)
+    except (OSError, ValueError):
+        return None
+    if not rec or rec.get("source_hash") != sources_hash(which) or rec.get("batch") != batch:
+        return None
+    b = (2.0 * rec["FETCH_SIZE_kB"] + rec["WRITE_SIZE_kB"]) * 1024
+    return {"traffic": b / (kernel_ms * 1e-3) / 1e9, "traffic_bytes_per_launch": b,
+            "pmc_record": os.path.relpath(PMC_RECORD_CONFIGS, ROOT)}
+
+
 def pmc_record(batch: int):
     """The committed PMC record for these sources and batch size, or None."""
     try:
@@ -307,10 +344,11 @@ def dual_block(B, rank, dev, dist, world, steps=20, warmup=3, cpu_seconds=0.0):
             "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": ev.nnz,
             "colours_shooting_radau": [ncol[0], ncol[1]],
             "finite": bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item()),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "kernel": "dual_interval_kernel<4>",
-                         "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)),
-                         "bytes_per_eval": bytes_per_eval},
+            "roofline": dict({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": achieved / HBM_PEAK_GBS, "kernel": "dual_interval_kernel<4>",
+                              "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)),
+                              "bytes_per_eval": bytes_per_eval, "traffic": None},
+                             **(config_traffic("dual", B, kernel_ms) or {})),
             "cpu_baseline": cpu}
 
 
@@ -373,9 +411,10 @@ def mpc_block(B, rank, dev, dist, world, steps=50, warmup=5):
             "value": B * steps * world / el, "unit": "evals/s", "instances_per_gpu": B,
             "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": nnz,
             "finite": finite,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "kernel": "mpc_interval_kernel<4>",
-                         "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval},
+            "roofline": dict({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": achieved / HBM_PEAK_GBS, "kernel": "mpc_interval_kernel<4>",
+                              "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval, "traffic": None},
+                             **(config_traffic("mpc", B, kernel_ms) or {})),
             "rti": rti}
 
 

@@ -1,0 +1,50 @@
+"""Short driver for PMC passes over the config-3 and config-5 evaluators (no solver, no sweep):
+5 batched evaluations of the dual-kite NLP (B=128) and of the tracking-MPC NLP (B=256).
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_cfg_fetch -o run --output-format csv -- python tools/pmc_kernels.py
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import numpy as np
+    import torch
+
+    from awebox_amd import dual as du
+    from awebox_amd import kite3 as k3
+    from awebox_amd.dual_evaluator import DualEvaluator
+    from awebox_amd.mpc import MpcEvaluator
+
+    dev = torch.device("cuda:0")
+    c = du.build_constants()
+    lay = du.layout_for(c)
+    v0 = du.initial_guess(c, lay)
+    B = 128
+    V = torch.tensor(np.stack([du.batch_member(v0, lay, b) for b in range(B)]), device=dev)
+    P = torch.tensor(np.stack([du.pack_p(lay, c, v0)] * B), device=dev)
+    ev = DualEvaluator(c, batch=B)
+    out = [torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, ev.n_g, dtype=torch.float64, device=dev),
+           torch.empty(B, ev.n_v, dtype=torch.float64, device=dev), torch.empty(B, ev.nnz, dtype=torch.float64, device=dev)]
+    for _ in range(5):
+        ev.eval_nlp_device(V, P, *out)
+    torch.cuda.synchronize()
+    c3 = k3.build_constants()
+    lay3 = k3.MpcLayout(c3.cfg.n_k, c3.cfg.d)
+    B = 256
+    inst = [k3.batch_instance(c3, lay3, i, B) for i in range(B)]
+    V = torch.tensor(np.stack([v for v, _ in inst]), device=dev)
+    P = torch.tensor(np.stack([p for _, p in inst]), device=dev)
+    ev3 = MpcEvaluator(c3, batch=B)
+    out = [torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, ev3.n_g, dtype=torch.float64, device=dev),
+           torch.empty(B, ev3.n_v, dtype=torch.float64, device=dev), torch.empty(B, ev3.nnz, dtype=torch.float64, device=dev)]
+    for _ in range(5):
+        ev3.eval_nlp_device(V, P, *out)
+    torch.cuda.synchronize()
+    print("pmc_kernels done", flush=True)
+
+
+if __name__ == "__main__":
+    main()
