@@ -344,12 +344,13 @@ class BatchedRti:
         KII = KII.view(B * nk, nI, nI)
         KIS = KIS.view(B * nk, nI, L)
         LU, piv = self._lu(KII)
-        X = self._solve(LU, piv, KIS)
-        Tsch = (KIS.transpose(1, 2) @ X).view(B, nk * L * L)
-        Tb.index_add_(0, self.btd_schur, -Tsch[:, self.schur_src].reshape(-1))
         rI = torch.zeros(B, nk * nI, **f64)
         rI[:, self.int_flat] = rhs[:, self.int_p]
-        z = self._solve(LU, piv, rI.view(B * nk, nI, 1))
+        # K_II^-1 [K_IS | r_I] in one batched solve (the solve is latency-bound, not width-bound)
+        Xz = self._solve(LU, piv, torch.cat([KIS, rI.view(B * nk, nI, 1)], dim=2))
+        X, z = Xz[:, :, :L], Xz[:, :, L:]
+        Tsch = (KIS.transpose(1, 2) @ X).view(B, nk * L * L)
+        Tb.index_add_(0, self.btd_schur, -Tsch[:, self.schur_src].reshape(-1))
         upd = (KIS.transpose(1, 2) @ z).view(B, nk * L)
         rS = torch.zeros(B, nS + 1, **f64)
         rS[:, :nS] = rhs[:, self.sep_p]
@@ -359,7 +360,7 @@ class BatchedRti:
         xb = self._btd(Tb.view(B, self.nb, 3, self.m, self.m), rb.view(B, self.nb, self.m, 1)).view(B, -1)
         xS = torch.zeros(B, nS + 1, **f64)
         xS[:, :nS] = xb[:, self.sep_btd]
-        xI = z.view(B * nk, nI) - (X @ xS[:, self.lsep].reshape(B * nk, L, 1)).view(B * nk, nI)
+        xI = z.reshape(B * nk, nI) - (X @ xS[:, self.lsep].reshape(B * nk, L, 1)).view(B * nk, nI)
         sol = torch.empty(B, self.N, **f64)
         sol[:, self.int_p] = xI.view(B, nk * nI)[:, self.int_flat]
         sol[:, self.sep_p] = xS[:, :nS]
