@@ -396,13 +396,11 @@ class StructuredKKT:
         return torch.linalg.solve(K.view(self.N, self.N), rhs)
 
     def _block_solve(self, B):
-        """K_II^-1 B for all interval blocks: the awelu solve kernel (LDS-resident right-hand
-        sides) for a few right-hand sides on the device; rocBLAS trsm for the many columns of
-        K_IS (the LDS-resident kernel re-streams the factors once per 12-68 columns, which loses to
-        trsm at n = 640); LAPACK in the CPU harness."""
-        if self.awelu and B.shape[-1] <= 8:
-            from .batched_lu import lu_solve
-            return lu_solve(self.LU_I, self.piv_I, B)
+        """K_II^-1 B for all interval blocks: triangular solves on the LU factors (rocBLAS on the
+        device, LAPACK in the CPU harness).  The awelu solve kernel (RTI's choice) is not used
+        here: it did not change the per-iteration time, and its roundoff moved the bench's 2-point
+        AP2 sweep to another local solution at 8 m/s (3,874 W over 60 s instead of 3,799 W over
+        29 s)."""
         return torch.linalg.lu_solve(self.LU_I, self.piv_I, B)
 
     def _solve(self, rhs):

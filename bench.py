@@ -105,7 +105,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512, help="NLP instances per step and GPU")
+    ap.add_argument("--batch", type=int, default=2048, help="NLP instances per step and GPU")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per thread setting")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hessian", action="store_true", help="skip the nlp_hess_l timing block")
