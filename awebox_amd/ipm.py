@@ -65,6 +65,7 @@ class IpmOptions:
     kkt: str = "structured"          # "structured" (interval elimination + Schur) or "dense"
     lu_backend: str = "awelu"        # interval-block LU: "awelu" (batched_lu.hip) or "torch" (rocSOLVER)
     separators: str = "dense"        # separator system: "dense" LU or "btd" (awebox_amd/btd.py block sweep)
+    deterministic: bool = True       # KKT assembly by gather-sum tables instead of atomic scatter-adds
     profile: bool = False            # synchronise and time the solver's phases (IpmResult.timing)
     verbose: bool = False
 
@@ -196,6 +197,36 @@ class _Csr:
         return (A @ x.unsqueeze(1)).squeeze(1)
 
 
+class _ScatterSum:
+    """out[dst[i]] += vals[i] for a fixed index pattern, deterministically and without atomics:
+    the duplicates of every destination are pre-grouped on the host into gather tables (one per
+    power-of-two bucket of the multiplicity, padding -> a zero slot), so a few gathers, row sums
+    and plain indexed stores replace index_put_(accumulate=True), whose atomics add duplicates in
+    a run-dependent order (the homotopy path is sensitive to that roundoff)."""
+
+    def __init__(self, dst, dev):
+        dst = np.asarray(dst, dtype=np.int64)
+        order = np.argsort(dst, kind="stable")
+        uniq, start, count = np.unique(dst[order], return_index=True, return_counts=True)
+        self.buckets = []
+        lo, width = 0, 1
+        while lo < (count.max() if len(count) else 0):
+            sel = np.where((count > lo) & (count <= width))[0]
+            if len(sel):
+                table = np.full((len(sel), width), len(dst), dtype=np.int64)
+                for w in range(width):
+                    has = count[sel] > w
+                    table[has, w] = order[start[sel][has] + w]
+                self.buckets.append((torch.tensor(uniq[sel], device=dev), torch.tensor(table, device=dev)))
+            lo, width = width, 2 * width
+
+    def add_into(self, out, vals):
+        ext = torch.cat([vals, vals.new_zeros(1)])
+        for d, table in self.buckets:
+            out[d] += ext[table].sum(dim=1)
+        return out
+
+
 def _dense_A(nlp, jv, N0, K):
     """Write A = [J | -I_slack] into rows N0.. and its transpose (in place)."""
     n, mI = nlp.n, nlp.mI
@@ -221,7 +252,7 @@ class StructuredKKT:
         S = K_SS - sum_k K_SI^k (K_II^k)^-1 K_IS^k,
     about 5 GFLOP at N=40 instead of the 1.3 TFLOP of a dense LU of the whole system."""
 
-    def __init__(self, nlp, lay, dev, lu_backend="awelu", separators="btd"):
+    def __init__(self, nlp, lay, dev, lu_backend="awelu", separators="btd", deterministic=False):
         n, ny, m = nlp.n, nlp.ny, nlp.m
         self.lu_backend = lu_backend
         N = ny + m
@@ -293,6 +324,10 @@ class StructuredKKT:
         self.schur_flat = (r_idx * (nS + 1) + c_idx).reshape(-1)
         int_p = np.where(owner >= 0)[0]
         self.int_p = torch.tensor(int_p, device=dev)
+        self.sc = None
+        if deterministic:
+            self.sc = [_ScatterSum(t.cpu().numpy(), dev) for t in (self.dst_ii, self.dst_is, self.dst_ss,
+                                                                    self.schur_flat)]
         # separators in stages [c[k-1], x[k]] (block tridiagonal, globals as border): pairing each
         # shooting state with the multipliers of the continuity row that defines it keeps the block
         # sweep's pivot blocks regular -- the finer order x[0], c[0], x[1], ... meets near-singular
@@ -337,11 +372,17 @@ class StructuredKKT:
         self.k_norm = float(self.csr.mv(vals.abs(), torch.ones(self.N, **f64)).max().item())
         nI, L, nS, n_k = self.nI, self.L, self.nS, self.n_k
         KII = torch.zeros(n_k * nI * nI, **f64)
-        KII.index_put_((self.dst_ii,), vals[self.sel_ii], accumulate=True)
+        if self.sc:
+            self.sc[0].add_into(KII, vals[self.sel_ii])
+        else:
+            KII.index_put_((self.dst_ii,), vals[self.sel_ii], accumulate=True)
         KII[self.pad_flat] = 1.0
         KII = KII.view(n_k, nI, nI)
         KIS = torch.zeros(n_k * nI * L, **f64)
-        KIS.index_put_((self.dst_is,), vals[self.sel_is], accumulate=True)
+        if self.sc:
+            self.sc[1].add_into(KIS, vals[self.sel_is])
+        else:
+            KIS.index_put_((self.dst_is,), vals[self.sel_is], accumulate=True)
         KIS = KIS.view(n_k, nI, L)
         self.awelu = self.lu_backend == "awelu" and KII.is_cuda   # the CPU test harness uses LAPACK
         if self.awelu:
@@ -358,8 +399,12 @@ class StructuredKKT:
             return
         self.use_btd = False
         S = torch.zeros((nS + 1) * (nS + 1), **f64)
-        S.index_put_((self.dst_ss,), vals[self.sel_ss], accumulate=True)
-        S.index_put_((self.schur_flat,), -T.reshape(-1), accumulate=True)
+        if self.sc:
+            self.sc[2].add_into(S, vals[self.sel_ss])
+            self.sc[3].add_into(S, -T.reshape(-1))
+        else:
+            S.index_put_((self.dst_ss,), vals[self.sel_ss], accumulate=True)
+            S.index_put_((self.schur_flat,), -T.reshape(-1), accumulate=True)
         S = S.view(nS + 1, nS + 1)
         S[nS, :] = 0.0
         S[:, nS] = 0.0
@@ -505,7 +550,8 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
     skkt = None
     if opts.kkt == "structured" and getattr(ev, "layout", None) is not None:
         try:
-            skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators)
+            skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators,
+                                 deterministic=opts.deterministic)
         except ValueError:
             skkt = None
     K = torch.zeros(N, N, **f64) if skkt is None else None

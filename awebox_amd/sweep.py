@@ -202,6 +202,8 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--separators", choices=["dense", "btd"], default="dense",
                     help="separator solve of the structured KKT (awebox_amd/btd.py for btd)")
+    ap.add_argument("--atomic-assembly", action="store_true",
+                    help="KKT assembly by atomic scatter-adds instead of the deterministic gather-sum")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -223,7 +225,8 @@ def main():
     else:
         mk = lambda c: Ap2Evaluator(c, batch=1)  # noqa: E731
     res = run_sweep(u, n_k=args.n_k, d=args.d, make_evaluator=mk, dist=dist, device=f"cuda:{local_rank}",
-                    opts=IpmOptions(max_iter=args.max_iter, separators=args.separators), verbose=args.verbose, arch=args.arch)
+                    opts=IpmOptions(max_iter=args.max_iter, separators=args.separators,
+                                    deterministic=not args.atomic_assembly), verbose=args.verbose, arch=args.arch)
     if res is not None:
         res = dict(res)
         res.pop("V_opt")

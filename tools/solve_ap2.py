@@ -15,9 +15,11 @@ def main():
     ap.add_argument("--n-k", type=int, default=40)
     ap.add_argument("--d", type=int, default=4)
     ap.add_argument("--u-ref", type=float, default=10.0)
-    ap.add_argument("--max-iter", type=int, default=500)
+    ap.add_argument("--max-iter", type=int, default=1000)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "solve_ap2.json"))
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--atomic-assembly", action="store_true",
+                    help="KKT assembly by atomic scatter-adds instead of the deterministic gather-sum")
     args = ap.parse_args()
     import torch
     from awebox_amd import problem as pb
@@ -29,7 +31,8 @@ def main():
     consts = pb.build_constants(pb.Ap2Config(n_k=args.n_k, d=args.d, u_ref=args.u_ref))
     ev = Ap2Evaluator(consts, batch=1)
     t0 = time.perf_counter()
-    V, summary, out, _ = optimize(consts, ev, IpmOptions(max_iter=args.max_iter, verbose=args.verbose),
+    V, summary, out, _ = optimize(consts, ev, IpmOptions(max_iter=args.max_iter, verbose=args.verbose,
+                                                   deterministic=not args.atomic_assembly),
                                verbose=True)
     rec = {"n_k": args.n_k, "d": args.d, "u_ref": args.u_ref, "seconds": time.perf_counter() - t0,
            "steps": summary, "outputs": out, "device": torch.cuda.get_device_name(0)}
