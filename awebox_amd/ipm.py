@@ -328,6 +328,7 @@ class StructuredKKT:
         if deterministic:
             self.sc = [_ScatterSum(t.cpu().numpy(), dev) for t in (self.dst_ii, self.dst_is, self.dst_ss,
                                                                     self.schur_flat)]
+            self.sc_mv = _ScatterSum(P_, dev)
         # separators in stages [c[k-1], x[k]] (block tridiagonal, globals as border): pairing each
         # shooting state with the multipliers of the continuity row that defines it keeps the block
         # sweep's pivot blocks regular -- the finer order x[0], c[0], x[1], ... meets near-singular
@@ -369,7 +370,7 @@ class StructuredKKT:
         vals = torch.cat([hv, hv[self.off_mask], diag, jv, jv, -torch.ones(2 * mI, **f64),
                           torch.full((m,), -float(delta_c), **f64)])
         self.vals = vals
-        self.k_norm = float(self.csr.mv(vals.abs(), torch.ones(self.N, **f64)).max().item())
+        self.k_norm = float(self._mv(vals.abs(), torch.ones(self.N, **f64)).max().item())
         nI, L, nS, n_k = self.nI, self.L, self.nS, self.n_k
         KII = torch.zeros(n_k * nI * nI, **f64)
         if self.sc:
@@ -411,8 +412,14 @@ class StructuredKKT:
         S[nS, nS] = 1.0
         self.LU_S, self.piv_S = torch.linalg.lu_factor(S)
 
+    def _mv(self, vals, x):
+        """K(vals) x: a fixed-order gather-sum when deterministic, rocSPARSE CSR otherwise."""
+        if self.sc:
+            return self.sc_mv.add_into(torch.zeros(self.N, dtype=torch.float64, device=self.dev), vals * x[self.Q_])
+        return self.csr.mv(vals, x)
+
     def matvec(self, x):
-        return self.csr.mv(self.vals, x)
+        return self._mv(self.vals, x)
 
     def solve(self, rhs, refine=3, rtol=1e-12):
         """Elimination solve with iterative refinement on the sparse residual.  The interior
