@@ -7,16 +7,20 @@ available here, so this module restates the IPOPT algorithm (Waechter & Biegler,
 
 * NLP functions, gradient, Jacobian and the exact Hessian of the Lagrangian come from the HIP
   evaluator (awebox_amd.evaluator) on device tensors;
-* the primal-dual KKT system [W + Sigma + dw I, A^T; A, -dc I] is assembled densely in HBM and
-  factorised in fp64 by rocSOLVER through torch.linalg (LU); the inertia correction uses the
-  curvature test of Chiang & Zavala (2016) instead of an inertia-revealing factorisation;
+* the primal-dual KKT system [W + Sigma + dw I, A^T; A, -dc I] is solved by structured
+  elimination (StructuredKKT: batched LU of the interval interiors on the awelu kernel, a dense
+  or block-tridiagonal Schur complement on the separators), assembled in a fixed summation order
+  (deterministic gather-sum tables); the inertia correction uses the curvature test of Chiang &
+  Zavala (2016) instead of an inertia-revealing factorisation;
 * fixed variables (lbx == ubx) are removed (IPOPT's fixed_variable_treatment=make_parameter);
   inequality rows get slacks; gradient-based NLP scaling, bound push, monotone Fiacco-McCormick
   barrier update, fraction-to-the-boundary rule and the filter line search follow IPOPT's
-  defaults (tol 1e-8, mu_init 0.1, kappa_mu 0.2, theta_mu 1.5, tau_min 0.99).
+  defaults (tol 1e-8, mu_init 0.1, kappa_mu 0.2, theta_mu 1.5, tau_min 0.99);
+* after a failed line search: a retry with stronger regularisation, then a reduced feasibility
+  restoration (Gauss-Newton steps on ||c|| inside the bounds until the filter accepts).
 
-What is left out: second-order corrections, the feasibility restoration phase (a failed line
-search ends the solve with status 'line_search_failure'), and quasi-Newton options.
+What is left out: second-order corrections, IPOPT's full restoration-phase NLP, and quasi-Newton
+options.
 """
 from __future__ import annotations
 
