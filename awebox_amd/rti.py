@@ -61,9 +61,12 @@ class BatchedRti:
     """B tracking-MPC closed loops advanced by one real-time iteration per call of ``step``."""
 
     def __init__(self, consts: k3.Kite3Constants, batch: int, device="cuda", delta_w=1e-8, delta_c=0.0,
-                 evaluator=None):
+                 evaluator=None, plant="collocation", n_fe=20):
         """``evaluator``: anything with MpcEvaluator's device interface (sparsity_jac, n_p, nnz,
-        eval_nlp_device); default = the HIP evaluator (awempc) for ``batch`` instances."""
+        eval_nlp_device); default = the HIP evaluator (awempc) for ``batch`` instances.
+        ``plant``: "collocation" (interval 0's Radau collocation) or "rk4root" (the reference's
+        sim integrator: ``n_fe`` RK4 steps per sampling time, the algebraic and derivative
+        variables by a Newton rootfinder at every stage; tools/integrator_routines.py:32-96)."""
         self.consts, self.B, self.dev = consts, batch, torch.device(device)
         cfg = consts.cfg
         self.lay = lay = k3.MpcLayout(cfg.n_k, cfg.d)
@@ -212,6 +215,23 @@ class BatchedRti:
         self.pl_keep = t(np.array(pk))
         self.pl_dst = t(np.array([rsel[int(jr_all[e])] * n_pl + csel[int(jc_all[e])] for e in pk]))
         self.x_idx = [t(lay.x(0))] + [t(lay.coll_x(0, j)) for j in range(cfg.d)]
+        if plant not in ("collocation", "rk4root"):
+            raise ValueError(f"unknown plant {plant!r}")
+        self.plant, self.n_fe = plant, n_fe
+        # rk4root: the shooting-node rows of interval 0 against (xdot[0], z[0])
+        self.rk_rows = t(lay.g_shooting(0))
+        self.rk_cols = t(np.concatenate([lay.xdot(0), lay.z(0)]))
+        rsel = {int(r): i for i, r in enumerate(lay.g_shooting(0))}
+        csel = {int(c): i for i, c in enumerate(np.concatenate([lay.xdot(0), lay.z(0)]))}
+        if len(rsel) != len(csel):
+            raise ValueError("shooting rows and (xdot, z) do not form a square system")
+        pk = [e for e in range(len(row)) if int(jr_all[e]) in rsel and int(jc_all[e]) in csel]
+        self.n_rk = len(rsel)
+        self.rk_keep = t(np.array(pk))
+        self.rk_dst = t(np.array([rsel[int(jr_all[e])] * self.n_rk + csel[int(jc_all[e])] for e in pk]))
+        self.xdot_idx = t(lay.xdot(0))
+        s_ = consts.scaling
+        self.rk_ratio = torch.tensor(s_[k3.NX:2 * k3.NX] / s_[:k3.NX], dtype=torch.float64, device=self.dev)
 
     # ------------------------------------------------------------------ set-up ----------
     def reference(self, t0: np.ndarray) -> np.ndarray:
@@ -383,7 +403,7 @@ class BatchedRti:
         horizon shifted.  Returns per-loop diagnostics."""
         kkt_res, path_max = self.iterate()
         self.u0 = self.V[:, self.u0_idx].clone()
-        x1, plant_res = self._plant()
+        x1, plant_res = self._plant() if self.plant == "collocation" else self._rk4root()
         self._shift(x1)
         self.step_count += 1
         x_ref = self.P[:, self.lay.p_ref + self.lay.x(0)[0]:self.lay.p_ref + self.lay.x(0)[0] + k3.NX]
@@ -409,6 +429,43 @@ class BatchedRti:
             Vp[:, self.pl_cols] -= self._solve(LU, piv, r.unsqueeze(-1).contiguous()).squeeze(-1)
         x1 = sum(float(self.D[r_]) * Vp[:, self.x_idx[r_]] for r_ in range(self.lay.d + 1))
         return x1, res
+
+    def _rk4root(self, max_newton=6, tol=1e-11):
+        """The reference's plant (sim.py:72-78 -> rk4root, integrator_routines.py:32-96): n_fe RK4
+        steps over one sampling time with the applied u[0]; at every stage the rootfinder solves
+        the shooting-node rows (dynamics, holonomic and trivial rows: 12 for the 3-DOF kite) for
+        (xdot, z) at the stage state -- here Newton on the HIP evaluator's rows and Jacobian
+        block, warm-started from the previous stage.  Returns (x1, the largest rootfinder
+        residual)."""
+        n, B = self.n_rk, self.B
+        h = self.consts.cfg.ts / self.n_fe
+        Vp = self.V.clone()
+        x = self.P[:, self.lay.p_x0:self.lay.p_x0 + k3.NX].clone()
+        worst = torch.zeros(B, dtype=torch.float64, device=self.dev)
+
+        def ode(xs):
+            nonlocal worst
+            Vp[:, self.x_idx[0]] = xs
+            for it in range(max_newton + 1):
+                self.ev.eval_nlp_device(Vp, self.P, self.f, self.g, self.grad, self.jac)
+                r = self.g[:, self.rk_rows]
+                res = r.abs().amax(dim=1)
+                if it == max_newton or (it >= 1 and float(res.max()) < tol):
+                    break
+                A = torch.zeros(B, n * n, dtype=torch.float64, device=self.dev)
+                A[:, self.rk_dst] = self.jac[:, self.rk_keep]
+                LU, piv = self._lu(A.view(B, n, n))
+                Vp[:, self.rk_cols] -= self._solve(LU, piv, r.unsqueeze(-1).contiguous()).squeeze(-1)
+            worst = torch.maximum(worst, res)
+            return Vp[:, self.xdot_idx] * self.rk_ratio
+
+        for _ in range(self.n_fe):
+            k1 = ode(x)
+            k2 = ode(x + 0.5 * h * k1)
+            k3_ = ode(x + 0.5 * h * k2)
+            k4 = ode(x + h * k3_)
+            x = x + h * (k1 + 2.0 * k2 + 2.0 * k3_ + k4) / 6.0
+        return x, worst
 
     def _shift(self, x1):
         """Move the horizon one interval: V[k] <- V[k+1], keep the last interval; new x0 and the

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--n-k", type=int, default=20)
     ap.add_argument("--d", type=int, default=4)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--plant", choices=["collocation", "rk4root"], default="collocation")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -27,7 +28,7 @@ def main():
     from awebox_amd.rti import BatchedRti
 
     c = k3.build_constants(k3.Kite3Config(n_k=a.n_k, d=a.d))
-    r = BatchedRti(c, a.batch, device="cuda")
+    r = BatchedRti(c, a.batch, device="cuda", plant=a.plant)
     r.start()
     sync = torch.cuda.synchronize
     phases = {"iterate": [], "plant": [], "shift": []}
@@ -39,7 +40,7 @@ def main():
         r.u0 = r.V[:, r.u0_idx].clone()
         sync()
         t1 = time.perf_counter()
-        x1, pres = r._plant()
+        x1, pres = r._plant() if a.plant == "collocation" else r._rk4root()
         sync()
         t2 = time.perf_counter()
         r._shift(x1)
@@ -64,7 +65,7 @@ def main():
     sync()
     el = (time.perf_counter() - t0) / n
     skip = min(2, a.steps - 1)
-    res = {"batch": a.batch, "n_k": a.n_k, "d": a.d, "ms_per_rti_step": el * 1e3,
+    res = {"batch": a.batch, "n_k": a.n_k, "d": a.d, "plant": a.plant, "ms_per_rti_step": el * 1e3,
            "loop_steps_per_s": a.batch / el,
            "phase_ms_median": {k: float(np.median(v[skip:])) for k, v in phases.items()},
            "kkt": {"interval_block": r.nI, "separator_block": r.nS, "coupling": r.L},
