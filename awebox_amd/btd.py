@@ -31,7 +31,7 @@ class BorderedBtd:
     within the block) for the n_S separators; the matrix entries arrive as value vectors aligned
     with the coordinate lists given at construction (duplicates are summed)."""
 
-    def __init__(self, stage_of, pos_of, nb, m, rows, cols, dev):
+    def __init__(self, stage_of, pos_of, nb, m, rows, cols, dev, deterministic=True):
         stage_of, pos_of = np.asarray(stage_of), np.asarray(pos_of)
         rows, cols = np.asarray(rows), np.asarray(cols)
         nS = len(stage_of)
@@ -67,6 +67,10 @@ class BorderedBtd:
         sep_t = np.where(stage_of >= 0)[0]
         self.sep_t, self.slot_t = t(sep_t), t(slot[sep_t])
         self.sep_g = t(border)
+        self.sc = None
+        if deterministic:                                  # fixed-order sums of duplicate entries
+            from .ipm import _ScatterSum
+            self.sc = [_ScatterSum(d.cpu().numpy(), dev) for d in (self.dst_tt, self.dst_tg, self.dst_gt, self.dst_gg)]
 
     # ---------------------------------------------------------------------------------------
     def factor(self, vals):
@@ -77,13 +81,16 @@ class BorderedBtd:
         n_t = nb * m
         f64 = dict(dtype=torch.float64, device=self.dev)
         T = self.T0.repeat(B, 1)
-        T.index_add_(1, self.dst_tt, v[:, self.src_tt])
         E = torch.zeros(B, n_t * nG, **f64)
-        E.index_add_(1, self.dst_tg, v[:, self.src_tg])
         Fm = torch.zeros(B, nG * n_t, **f64)
-        Fm.index_add_(1, self.dst_gt, v[:, self.src_gt])
         C = torch.zeros(B, nG * nG, **f64)
-        C.index_add_(1, self.dst_gg, v[:, self.src_gg])
+        parts = ((T, self.src_tt, self.dst_tt), (E, self.src_tg, self.dst_tg), (Fm, self.src_gt, self.dst_gt),
+                 (C, self.src_gg, self.dst_gg))
+        for i, (out, src, dst) in enumerate(parts):
+            if self.sc is not None:
+                self.sc[i].add_into(out, v[:, src])
+            else:
+                out.index_add_(1, dst, v[:, src])
         T = T.view(B, nb, 3, m, m)
         self.B = B
         self.squeeze = squeeze

@@ -163,7 +163,37 @@ def outputs(consts: pb.Ap2Constants, lay: pb.NlpLayout, V: np.ndarray) -> dict:
     for k in range(lay.n_k):
         for j in range(lay.d):
             cx = V[lay.coll_x(k, j)]
-            lam = V[lay.coll_z(k, j)] * s[o_lam]
+            lam = V[lay.coll_z(k, j)][0] * s[o_lam]
             p = lam * cx[o_l] * s[o_l] * cx[o_dl] * s[o_dl]
             energy += tf / lay.n_k * w[j] * float(p)
     return {"avg_power_W": energy / tf, "period_s": float(tf), "energy_J": energy}
+
+
+def power_integrand(consts: pb.Ap2Constants):
+    """The power integral output's integrand p = lambda10 l_t dl_t [W] (dynamics.py:318-330) from
+    scaled states x [B, 23] and algebraic variables z [B, 1] (torch tensors)."""
+    s = consts.scaling
+    o_l, _ = _node_offset("x", "l_t")
+    o_dl, _ = _node_offset("x", "dl_t")
+    o_lam, _ = _node_offset("z", "lambda10")
+    c = float(s[o_lam] * s[o_l] * s[o_dl])
+
+    def p(x, z):
+        return c * z[:, 0] * x[:, o_l] * x[:, o_dl]
+    return p
+
+
+def interval_energy(consts: pb.Ap2Constants, lay: pb.NlpLayout, V: np.ndarray, k: int) -> float:
+    """Energy [J] of interval k: the integral output's increment over the interval
+    (collocation.py:272-316), the reference integrators' ``qf``."""
+    s = consts.scaling
+    w = np.asarray(pb.collocation(lay.d)[3], dtype=float)
+    tf = V[lay.theta()[1]] * s[pb.W_TH0 + 1]
+    o_l, _ = _node_offset("x", "l_t")
+    o_dl, _ = _node_offset("x", "dl_t")
+    o_lam, _ = _node_offset("z", "lambda10")
+    e = 0.0
+    for j in range(lay.d):
+        cx = V[lay.coll_x(k, j)]
+        e += tf / lay.n_k * w[j] * V[lay.coll_z(k, j)][0] * s[o_lam] * cx[o_l] * s[o_l] * cx[o_dl] * s[o_dl]
+    return float(e)

@@ -202,14 +202,16 @@ class _Csr:
 
 
 class _ScatterSum:
-    """out[dst[i]] += vals[i] for a fixed index pattern, deterministically and without atomics:
-    the duplicates of every destination are pre-grouped on the host into gather tables (one per
-    power-of-two bucket of the multiplicity, padding -> a zero slot), so a few gathers, row sums
-    and plain indexed stores replace index_put_(accumulate=True), whose atomics add duplicates in
-    a run-dependent order (the homotopy path is sensitive to that roundoff)."""
+    """out[..., dst[i]] += vals[..., i] for a fixed index pattern, deterministically and without
+    atomics: the duplicates of every destination are pre-grouped on the host into gather tables
+    (one per power-of-two bucket of the multiplicity, padding -> a zero slot), so a few gathers,
+    row sums and plain indexed stores replace index_put_(accumulate=True) / index_add_, whose
+    atomics add duplicates in a run-dependent order (the homotopy path is
+    sensitive to that roundoff).  Leading (batch) dimensions of ``out`` and ``vals`` are kept."""
 
     def __init__(self, dst, dev):
-        dst = np.asarray(dst, dtype=np.int64)
+        dst = np.asarray(dst, dtype=np.int64).reshape(-1)
+        self.n_src = len(dst)
         order = np.argsort(dst, kind="stable")
         uniq, start, count = np.unique(dst[order], return_index=True, return_counts=True)
         self.buckets = []
@@ -225,10 +227,25 @@ class _ScatterSum:
             lo, width = width, 2 * width
 
     def add_into(self, out, vals):
-        ext = torch.cat([vals, vals.new_zeros(1)])
+        ext = torch.cat([vals, vals.new_zeros(vals.shape[:-1] + (1,))], dim=-1)
         for d, table in self.buckets:
-            out[d] += ext[table].sum(dim=1)
+            out[..., d] += ext[..., table].sum(dim=-1)
         return out
+
+
+class _GatherMv:
+    """y = A(vals) x for a fixed COO pattern: products vals * x[cols], summed per row by a
+    _ScatterSum (fixed order).  Replaces rocSPARSE's CSR SpMV, whose adaptive algorithm splits
+    long rows (the t_f column of J, i.e. a row of J^T) across workgroups with atomic adds."""
+
+    def __init__(self, rows, cols, shape, dev):
+        self.cols = torch.tensor(np.asarray(cols, dtype=np.int64), device=dev)
+        self.sum = _ScatterSum(rows, dev)
+        self.shape = shape
+
+    def mv(self, vals, x):
+        out = x.new_zeros(x.shape[:-1] + (self.shape[0],))
+        return self.sum.add_into(out, vals * x[..., self.cols])
 
 
 def _dense_A(nlp, jv, N0, K):
@@ -333,6 +350,8 @@ class StructuredKKT:
             self.sc = [_ScatterSum(t.cpu().numpy(), dev) for t in (self.dst_ii, self.dst_is, self.dst_ss,
                                                                     self.schur_flat)]
             self.sc_mv = _ScatterSum(P_, dev)
+            self.sc_dense = _ScatterSum(P_ * N + Q_, dev)
+            self.sc_rs = _ScatterSum(lsep_arr.reshape(-1), dev)
         # separators in stages [c[k-1], x[k]] (block tridiagonal, globals as border): pairing each
         # shooting state with the multipliers of the continuity row that defines it keeps the block
         # sweep's pivot blocks regular -- the finer order x[0], c[0], x[1], ... meets near-singular
@@ -362,7 +381,8 @@ class StructuredKKT:
             try:
                 self.btd = BorderedBtd(stage_of, pos_of, n_k + 1, 2 * nx,
                                        np.concatenate([ss_r, sch_r.reshape(-1)]),
-                                       np.concatenate([ss_c, sch_c.reshape(-1)]), dev)
+                                       np.concatenate([ss_c, sch_c.reshape(-1)]), dev,
+                                       deterministic=deterministic)
             except ValueError:
                 self.btd = None                                 # not stage-structured: dense S
         self.int_flat = torch.tensor(owner[int_p] * nI + loc[int_p], device=dev)
@@ -448,7 +468,10 @@ class StructuredKKT:
         # ill-conditioned interior pivots: one dense LU of the assembled K for this system
         self.n_dense += 1
         K = torch.zeros(self.N * self.N, dtype=torch.float64, device=self.dev)
-        K.index_put_((self.P_ * self.N + self.Q_,), self.vals, accumulate=True)
+        if self.sc:
+            self.sc_dense.add_into(K, self.vals)
+        else:
+            K.index_put_((self.P_ * self.N + self.Q_,), self.vals, accumulate=True)
         return torch.linalg.solve(K.view(self.N, self.N), rhs)
 
     def _block_solve(self, B):
@@ -469,7 +492,10 @@ class StructuredKKT:
         rS[:nS] = rhs[self.sep_p]
         z = self._block_solve(rI)                                              # [n_k, nI, 1]
         upd = (self.KIS.transpose(1, 2) @ z).reshape(-1)                      # [n_k * L]
-        rS = rS.index_add(0, self.lsep.reshape(-1), -upd)
+        if self.sc:
+            self.sc_rs.add_into(rS, -upd)
+        else:
+            rS = rS.index_add(0, self.lsep.reshape(-1), -upd)
         rS[nS] = 0.0
         if self.use_btd:
             xS = torch.zeros(nS + 1, **f64)
@@ -600,10 +626,11 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
     def grad_y(gradv):
         return torch.cat([gradv, torch.zeros(mI, **f64)])
 
-    jt_op = _Csr(nlp.j_col.cpu().numpy(), nlp.j_row.cpu().numpy(), (ny, m), dev)
+    Op = _GatherMv if opts.deterministic else _Csr
+    jt_op = Op(nlp.j_col.cpu().numpy(), nlp.j_row.cpu().numpy(), (ny, m), dev)
     hr_np, hc_np = nlp.h_r.cpu().numpy(), nlp.h_c.cpu().numpy()
     off_np = hr_np != hc_np
-    h_op = _Csr(np.concatenate([hr_np, hc_np[off_np]]), np.concatenate([hc_np, hr_np[off_np]]), (ny, ny), dev)
+    h_op = Op(np.concatenate([hr_np, hc_np[off_np]]), np.concatenate([hc_np, hr_np[off_np]]), (ny, ny), dev)
 
     def A_T_lam(jvv, lamv):
         r = jt_op.mv(jvv, lamv)

@@ -82,6 +82,24 @@ def test_structured_kkt_btd_on_gpu():
     assert fwd <= 1e-6
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("separators", ["dense", "btd"])
+def test_structured_kkt_bitwise_repeatable_on_gpu(separators):
+    """Two factor + solve calls on identical inputs give bitwise-identical solutions (fixed-order
+    assembly, Schur update and residual products: no atomics anywhere in the KKT solve)."""
+    import torch
+    from awebox_amd.evaluator import Ap2Evaluator
+    from awebox_amd.ipm import StructuredKKT
+    nlp, sk, hv, jv, diag, K, rhs = _kkt_case("cuda", lambda c: Ap2Evaluator(c, batch=1))
+    lay = pb.NlpLayout(5, 3)
+    xs = []
+    for _ in range(2):
+        sk = StructuredKKT(nlp, lay, "cuda", separators=separators, deterministic=True)
+        sk.factor(hv, diag, jv, 1e-9, nlp.mI)
+        xs.append(sk.solve(rhs.clone()))
+    assert torch.equal(xs[0], xs[1])
+
+
 @pytest.mark.parametrize("delta_c,btd", [(0.0, False), (1e-6, False), (0.0, True), (1e-6, True)])
 def test_structured_kkt_matches_dense(delta_c, btd):
     """Interval elimination + Schur complement solves the same KKT system as a dense LU; with
