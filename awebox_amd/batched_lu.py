@@ -24,6 +24,8 @@ def load_library(path: str = _PATH):
                                             ctypes.c_void_p, ctypes.c_void_p]
         lib.awelu_btd_factor_batched.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3
         lib.awelu_btd_solve_batched.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 4
+        lib.awelu_sym_inertia_batched.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_double,
+                                                  ctypes.c_void_p, ctypes.c_void_p]
         lib.awelu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
@@ -117,3 +119,31 @@ def btd_dense(T):
             if 0 <= k + dk < nb:
                 A[:, k * m:(k + 1) * m, (k + dk) * m:(k + dk + 1) * m] = T[:, k, s_]
     return A
+
+
+def sym_inertia(A, ztol=1e-13):
+    """(positive, negative, zero) eigenvalue counts [batch, 3] (int32, on the device) of symmetric
+    float64 CUDA matrices A [batch, n, n] (lower triangle read; A is not modified)."""
+    import torch
+    if A.dtype != torch.float64 or not A.is_cuda or A.dim() != 3 or A.shape[1] != A.shape[2]:
+        raise ValueError(f"sym_inertia needs a float64 CUDA tensor [batch, n, n], got {tuple(A.shape)}")
+    b, n, _ = A.shape
+    W = A.contiguous().clone()
+    counts = torch.empty(b, 3, dtype=torch.int32, device=A.device)
+    lib = load_library()
+    s = torch.cuda.current_stream(A.device).cuda_stream
+    rc = lib.awelu_sym_inertia_batched(n, b, ctypes.c_void_p(W.data_ptr()), ctypes.c_double(ztol),
+                                       ctypes.c_void_p(counts.data_ptr()), ctypes.c_void_p(s))
+    if rc != 0:
+        raise RuntimeError(f"awelu_sym_inertia_batched: {lib.awelu_last_error().decode()}")
+    return counts
+
+
+def sym_inertia_host(A, ztol=1e-13):
+    """The same counts from symmetric eigenvalues (host tensors: the CPU test harness)."""
+    import torch
+    ev = torch.linalg.eigvalsh(0.5 * (A + A.transpose(-1, -2)))
+    scale = A.abs().amax(dim=(-1, -2), keepdim=False).clamp(min=1e-300).unsqueeze(-1)
+    pos = (ev > ztol * scale).sum(-1)
+    neg = (ev < -ztol * scale).sum(-1)
+    return torch.stack([pos, neg, ev.shape[-1] - pos - neg], dim=-1).to(torch.int32)

@@ -63,6 +63,7 @@ class BorderedBtd:
         T0 = np.zeros((nb, 3, m, m))
         a_, i_ = np.where(~used)
         T0[a_, 1, i_, i_] = 1.0                           # unused block positions (fixed variables)
+        self.n_unused = len(a_)
         self.T0 = torch.tensor(T0.reshape(-1), dtype=torch.float64, device=dev)
         sep_t = np.where(stage_of >= 0)[0]
         self.sep_t, self.slot_t = t(sep_t), t(slot[sep_t])
@@ -99,12 +100,39 @@ class BorderedBtd:
             self.Tf = btd_factor(T)
         else:
             from .batched_lu import btd_dense
+            self.T_blocks = T
             self.Tf = torch.linalg.lu_factor(btd_dense(T))
         self.Fm = Fm.view(B, nG, n_t)
         if nG:
             self.Z = self._t_solve(E.view(B, n_t, nG))                     # T^-1 E
             Cp = C.view(B, nG, nG) - self.Fm @ self.Z
+            self.Cp = Cp
             self.Cf = self._lu(Cp)
+
+    def inertia(self):
+        """[B, 3] (positive, negative, zero) eigenvalue counts of the separator matrix S: the pivot
+        blocks D'_k of the block sweep (their inverses Dinv_k have the same signs) plus the border's
+        Schur complement C' (Haynsworth additivity); the identity rows of unused block positions
+        are taken out."""
+        from .batched_lu import sym_inertia, sym_inertia_host
+        B, nb, m = self.B, self.nb, self.m
+        if self.Tf[0].is_cuda:
+            F, Dinv = self.Tf
+            c = sym_inertia(Dinv.reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
+        else:                                              # host: the pivot blocks by the block recursion
+            T = self.T_blocks
+            D = T[:, 0, 1]
+            blocks = [D]
+            for k in range(1, nb):
+                D = T[:, k, 1] - T[:, k, 0] @ torch.linalg.solve(D, T[:, k - 1, 2])
+                blocks.append(D)
+            c = sym_inertia_host(torch.stack(blocks, 1).reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
+        c = c.to(torch.int64)
+        c[:, 0] -= self.n_unused
+        if self.nG:
+            cc = (sym_inertia if self.Cp.is_cuda else sym_inertia_host)(self.Cp.contiguous(), ztol=1e-30)
+            c = c + cc.to(torch.int64)
+        return c
 
     def _t_solve(self, X):
         B, nb, m = self.B, self.nb, self.m

@@ -414,6 +414,156 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
     }
 }
 
+
+// Inertia (numbers of positive, negative and zero eigenvalues) of `batch` symmetric n x n matrices
+// by Bunch-Kaufman symmetric indefinite elimination (LAPACK dsytf2, lower triangle, alpha =
+// (1 + sqrt 17) / 8), Sylvester's law on the block-diagonal factor: a 1 x 1 pivot counts its sign,
+// a 2 x 2 pivot by the signs of its determinant and trace.  IPOPT's inertia correction needs
+// exactly these counts of the KKT matrix (MA27/MA57 report them); ipm.StructuredKKT adds them over
+// the interval blocks and the separator pivot blocks (Haynsworth additivity).
+// One workgroup per matrix, working in place on the lower triangle of A[b] (row-major, the upper
+// triangle is ignored; the matrix is destroyed).  Per elimination step: column max by wave
+// shuffles (+ the row max of the candidate when the diagonal is small), a symmetric interchange,
+// the pivot column(s) staged in LDS, then the trailing lower triangle updated one row per wave
+// (lanes over the row's columns: coalesced row-major accesses).  A pivot with max(|a_kk|, colmax) <=
+// ztol * max|A| counts as a zero eigenvalue and is skipped.
+__device__ __forceinline__ void block_argmax(double& v, int& i, double* rv, int* ri, int tid) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(v, off);
+        const int oi = __shfl_xor(i, off);
+        if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+    }
+    if ((tid & 63) == 0) { rv[tid >> 6] = v; ri[tid >> 6] = i; }
+    __syncthreads();
+    v = rv[0];
+    i = ri[0];
+    for (int w = 1; w < kThreads / 64; ++w)
+        if (rv[w] > v || (rv[w] == v && ri[w] < i)) { v = rv[w]; i = ri[w]; }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kThreads) void sym_inertia_kernel(int n, double* __restrict__ As, double ztol,
+                                                               int* __restrict__ counts) {
+    extern __shared__ double pc[];                      // pivot columns: [2][n]
+    __shared__ double rv[kThreads / 64];
+    __shared__ int ri[kThreads / 64];
+    double* A = As + (size_t)blockIdx.x * n * n;
+    const int tid = threadIdx.x;
+    const int wv = tid >> 6, ln = tid & 63;
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    auto L = [&](int i, int j) -> double& { return i >= j ? A[(size_t)i * n + j] : A[(size_t)j * n + i]; };
+    // scale for the zero-pivot test
+    double amax = 0.0;
+    int dummy = 0;
+    for (int t = tid; t < n * n; t += kThreads) {
+        const int i = t / n, j = t - i * n;
+        if (j <= i) amax = fmax(amax, fabs(A[t]));
+    }
+    block_argmax(amax, dummy, rv, ri, tid);
+    const double zlim = ztol * amax;
+    int pos = 0, neg = 0, zero = 0;                     // uniform across the workgroup
+    int k = 0;
+    while (k < n) {
+        const double absakk = fabs(L(k, k));
+        double colmax = 0.0;
+        int imax = k;
+        for (int i = k + 1 + tid; i < n; i += kThreads) {
+            const double v = fabs(L(i, k));
+            if (v > colmax) { colmax = v; imax = i; }
+        }
+        block_argmax(colmax, imax, rv, ri, tid);
+        if (fmax(absakk, colmax) <= zlim) {             // zero column: a zero eigenvalue
+            ++zero;
+            ++k;
+            continue;
+        }
+        int kp = k, kstep = 1;
+        if (absakk < alpha * colmax) {
+            double rowmax = 0.0;
+            int jm = 0;
+            for (int j = k + tid; j < n; j += kThreads)
+                if (j != imax) {
+                    const double v = fabs(L(imax, j));
+                    if (v > rowmax) { rowmax = v; jm = j; }
+                }
+            block_argmax(rowmax, jm, rv, ri, tid);
+            if (absakk >= alpha * colmax * (colmax / rowmax)) {
+                kp = k;
+            } else if (fabs(L(imax, imax)) >= alpha * rowmax) {
+                kp = imax;
+            } else {
+                kp = imax;
+                kstep = 2;
+            }
+        }
+        const int kk = k + kstep - 1;
+        if (kp != kk) {                                  // symmetric interchange of kk and kp
+            for (int i = kp + 1 + tid; i < n; i += kThreads) {
+                const double a = A[(size_t)i * n + kk];
+                A[(size_t)i * n + kk] = A[(size_t)i * n + kp];
+                A[(size_t)i * n + kp] = a;
+            }
+            for (int j = kk + 1 + tid; j < kp; j += kThreads) {
+                const double a = A[(size_t)j * n + kk];
+                A[(size_t)j * n + kk] = A[(size_t)kp * n + j];
+                A[(size_t)kp * n + j] = a;
+            }
+            if (tid == 0) {
+                const double a = A[(size_t)kk * n + kk];
+                A[(size_t)kk * n + kk] = A[(size_t)kp * n + kp];
+                A[(size_t)kp * n + kp] = a;
+                if (kstep == 2) {
+                    const double b = A[(size_t)(k + 1) * n + k];
+                    A[(size_t)(k + 1) * n + k] = A[(size_t)kp * n + k];
+                    A[(size_t)kp * n + k] = b;
+                }
+            }
+            __syncthreads();
+        }
+        // stage the pivot column(s) below the pivot block
+        const int r0 = k + kstep;
+        for (int i = r0 + tid; i < n; i += kThreads) {
+            pc[i] = A[(size_t)i * n + k];
+            if (kstep == 2) pc[n + i] = A[(size_t)i * n + k + 1];
+        }
+        const double d11 = A[(size_t)k * n + k];
+        double d21 = 0.0, d22 = 0.0;
+        if (kstep == 2) {
+            d21 = A[(size_t)(k + 1) * n + k];
+            d22 = A[(size_t)(k + 1) * n + k + 1];
+        }
+        __syncthreads();
+        if (kstep == 1) {
+            if (d11 > 0.0) ++pos; else if (d11 < 0.0) ++neg; else ++zero;
+            const double rd = 1.0 / d11;
+            for (int i = r0 + wv; i < n; i += kThreads / 64) {     // one row per wave, lanes over j <= i
+                const double ci = pc[i] * rd;
+                double* row = A + (size_t)i * n;
+                for (int j = r0 + ln; j <= i; j += 64) row[j] -= ci * pc[j];
+            }
+        } else {
+            const double det = d11 * d22 - d21 * d21;
+            if (det < 0.0) { ++pos; ++neg; }
+            else if (det > 0.0) { if (d11 + d22 > 0.0) pos += 2; else neg += 2; }
+            else { ++zero; if (d11 + d22 > 0.0) ++pos; else if (d11 + d22 < 0.0) ++neg; else ++zero; }
+            const double i11 = d22 / det, i22 = d11 / det, i21 = -d21 / det;   // D^-1
+            for (int i = r0 + wv; i < n; i += kThreads / 64) {
+                const double ai = pc[i], bi = pc[n + i];
+                const double wi1 = i11 * ai + i21 * bi, wi2 = i21 * ai + i22 * bi;
+                double* row = A + (size_t)i * n;
+                for (int j = r0 + ln; j <= i; j += 64) row[j] -= wi1 * pc[j] + wi2 * pc[n + j];
+            }
+        }
+        __syncthreads();
+        k += kstep;
+    }
+    if (tid == 0) {
+        counts[3 * blockIdx.x + 0] = pos;
+        counts[3 * blockIdx.x + 1] = neg;
+        counts[3 * blockIdx.x + 2] = zero;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -497,6 +647,25 @@ int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, const double* T,
         const int w = std::min(kBtdMaxRhs, nrhs - j0);
         btd_apply_kernel<<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, nrhs, j0, w, T, Dinv, X);
     }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// Inertia of `batch` symmetric n x n matrices A[b][n][n] (lower triangle read, A destroyed):
+// counts[b][3] = (positive, negative, zero) eigenvalue counts.  Asynchronous on `stream`.
+int awelu_sym_inertia_batched(int n, int batch, double* A, double ztol, int* counts, void* stream) {
+    if (n < 1 || n > 4000 || batch < 1 || !A || !counts) {
+        g_err = "need 1 <= n <= 4000 (pivot columns in LDS), batch >= 1 and device pointers";
+        return 1;
+    }
+    const size_t lds = sizeof(double) * 2 * (size_t)n;
+    if (lds > 64 * 1024)
+        hipFuncSetAttribute((const void*)sym_inertia_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    sym_inertia_kernel<<<dim3((unsigned)batch), kThreads, lds, (hipStream_t)stream>>>(n, A, ztol, counts);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

@@ -66,10 +66,14 @@ class IpmOptions:
     eta_phi: float = 1e-8
     alpha_min_frac: float = 0.05
     max_backtracks: int = 40
+    max_soc: int = 4                 # second-order corrections per line search (IPOPT max_soc)
+    kappa_soc: float = 0.99
     kkt: str = "structured"          # "structured" (interval elimination + Schur) or "dense"
     lu_backend: str = "awelu"        # interval-block LU: "awelu" (batched_lu.hip) or "torch" (rocSOLVER)
-    separators: str = "dense"        # separator system: "dense" LU or "btd" (awebox_amd/btd.py block sweep)
+    separators: str = "btd"          # separator system: "dense" LU or "btd" (awebox_amd/btd.py block sweep)
     deterministic: bool = True       # KKT assembly by gather-sum tables instead of atomic scatter-adds
+    inertia: str = "exact"           # inertia correction: "curvature" test (Chiang & Zavala) or "exact" (IPOPT:
+                                     # In(K) = In(K_II) + In(S) from symmetric eigenvalues of the blocks)
     profile: bool = False            # synchronise and time the solver's phases (IpmResult.timing)
     verbose: bool = False
 
@@ -260,6 +264,10 @@ def _dense_A(nlp, jv, N0, K):
     K[scol, srow] = -1.0
 
 
+ZERO_PIVOT = 1e-30   # relative zero-pivot threshold of the inertia count: KKT pivots legitimately span
+                     # 1e-10 .. 1e10 at small mu, so only exactly singular columns count as zero
+
+
 class StructuredKKT:
     """KKT solve by elimination of every interval's interior unknowns (batched dense LU on the
     GPU) and a dense Schur complement on the separators.
@@ -359,6 +367,7 @@ class StructuredKKT:
         # with |W_k| <= 60, a backward error of 2e-21 (emulated on the CPU)
         self.btd = None
         self.force_btd = False                                  # CPU tests: the BTD path on host
+        self.btd_off = False                                    # the dense separator LU even when btd exists
         from .batched_lu import BTD_MAX_M
         if lu_backend == "awelu" and separators == "btd" and 2 * nx <= BTD_MAX_M:
             stage_of = np.full(self.nS, -1, dtype=np.int64)
@@ -403,6 +412,7 @@ class StructuredKKT:
             KII.index_put_((self.dst_ii,), vals[self.sel_ii], accumulate=True)
         KII[self.pad_flat] = 1.0
         KII = KII.view(n_k, nI, nI)
+        self.KII = KII
         KIS = torch.zeros(n_k * nI * L, **f64)
         if self.sc:
             self.sc[1].add_into(KIS, vals[self.sel_is])
@@ -418,7 +428,7 @@ class StructuredKKT:
         self.X = self._block_solve(KIS)                                        # K_II^-1 K_IS
         T = KIS.transpose(1, 2) @ self.X                                       # [n_k, L, L]
         self.KIS = KIS
-        if self.btd is not None and (KII.is_cuda or self.force_btd):
+        if self.btd is not None and not self.btd_off and (KII.is_cuda or self.force_btd):
             self.btd.factor(torch.cat([vals[self.sel_ss], -T.reshape(-1)]))
             self.use_btd = True
             return
@@ -434,7 +444,26 @@ class StructuredKKT:
         S[nS, :] = 0.0
         S[:, nS] = 0.0
         S[nS, nS] = 1.0
+        self.S = S
         self.LU_S, self.piv_S = torch.linalg.lu_factor(S)
+
+    def inertia(self):
+        """(positive, negative, zero) eigenvalue counts of K by Haynsworth's additivity,
+        In(K) = sum_k In(K_II^k) + In(S): Bunch-Kaufman inertia of the interval blocks (padding
+        rows excluded) and of the separator system -- the dense Schur complement S, or with the
+        block-tridiagonal separators the sweep's pivot blocks and the border (btd.BorderedBtd)."""
+        from .batched_lu import sym_inertia, sym_inertia_host
+        f = sym_inertia if self.KII.is_cuda else sym_inertia_host
+        c = f(self.KII, ztol=ZERO_PIVOT).to(torch.int64).sum(0)
+        c[0] -= len(self.pad_flat)
+        if self.use_btd:
+            c = c + self.btd.inertia()[0]
+        else:
+            cs = f(self.S.unsqueeze(0), ztol=ZERO_PIVOT).to(torch.int64)[0]
+            cs[0] -= 1                                          # the dummy separator's 1.0
+            c = c + cs
+        pos, neg, zero = (int(v) for v in c.cpu().tolist())
+        return pos, neg, zero
 
     def _mv(self, vals, x):
         """K(vals) x: a fixed-order gather-sum when deterministic, rocSPARSE CSR otherwise."""
@@ -589,9 +618,13 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
         try:
             skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators,
                                  deterministic=opts.deterministic)
+            skkt.force_btd = opts.separators == "btd"           # the block sweep on host tensors too
         except ValueError:
             skkt = None
     K = torch.zeros(N, N, **f64) if skkt is None else None
+    # exact inertia needs the separator pivot blocks of the block sweep on the device (a dense
+    # Bunch-Kaufman pass over the whole Schur complement is ~1 s); otherwise the curvature test
+    exact_inertia = opts.inertia == "exact" and skkt is not None and (skkt.btd is not None or not dev.type == "cuda")
     timing = {}
 
     class _Phase:
@@ -750,20 +783,41 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
                             skkt.factor(hv, sigma + delta_w, jv, delta_c, mI)
                         else:
                             assemble(K, hv, sigma, delta_w, delta_c)
-                    with _Phase("kkt_solve"):
-                        sol = skkt.solve(rhs) if skkt is not None else torch.linalg.solve(K, rhs)
-                    ok = bool(torch.isfinite(sol).all().item())
+                    if exact_inertia:
+                        # IPOPT's inertia correction (Waechter & Biegler 2006, Alg. IC): a singular
+                        # matrix gets delta_c once, a wrong inertia a larger delta_w
+                        with _Phase("inertia"):
+                            pos, neg, zero = skkt.inertia()
+                        # zero or missing negative eigenvalues: a (numerically) rank-deficient
+                        # constraint Jacobian -> delta_c; too few positive ones -> delta_w
+                        if (zero > 0 or neg < m) and delta_c == 0.0:
+                            delta_c = opts.delta_c * mu ** 0.25
+                            continue
+                        ok = pos == ny and neg == m
+                        if ok:
+                            with _Phase("kkt_solve"):
+                                sol = skkt.solve(rhs)
+                            if not bool(torch.isfinite(sol).all().item()):
+                                ok = False
+                        if ok:
+                            if delta_w > 0:
+                                delta_w_last = delta_w
+                            return sol[:ny], sol[ny:], delta_w
+                    else:
+                        with _Phase("kkt_solve"):
+                            sol = skkt.solve(rhs) if skkt is not None else torch.linalg.solve(K, rhs)
+                        ok = bool(torch.isfinite(sol).all().item())
+                        if ok:
+                            dy = sol[:ny]
+                            Wd = h_op.mv(torch.cat([hv, hv[nlp.h_offdiag]]), dy)
+                            curv = float((dy * (Wd + (sigma + delta_w) * dy)).sum().item())
+                            if curv >= opts.curvature_kappa * float((dy * dy).sum().item()):
+                                if delta_w > 0:
+                                    delta_w_last = delta_w
+                                return sol[:ny], sol[ny:], delta_w
+                        else:
+                            delta_c = opts.delta_c * mu ** 0.25
                 except RuntimeError:
-                    ok = False
-                if ok:
-                    dy = sol[:ny]
-                    Wd = h_op.mv(torch.cat([hv, hv[nlp.h_offdiag]]), dy)
-                    curv = float((dy * (Wd + (sigma + delta_w) * dy)).sum().item())
-                    if curv >= opts.curvature_kappa * float((dy * dy).sum().item()):
-                        if delta_w > 0:
-                            delta_w_last = delta_w
-                        return sol[:ny], sol[ny:], delta_w
-                else:
                     delta_c = opts.delta_c * mu ** 0.25
                 if delta_w == 0.0:
                     delta_w = opts.delta_w0 if delta_w_last == 0.0 else max(opts.delta_w_min, delta_w_last / 3.0)
@@ -773,43 +827,96 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
                     return None
             return None
 
-        def line_search(dy):
-            """Filter line search from the fraction-to-the-boundary step; (alpha, y_trial) or None."""
+        def acceptable(alpha, theta_t, phi_t, gphi_d):
+            """IPOPT's filter acceptance of a trial point (switching condition + Armijo, or
+            sufficient decrease of theta or phi, and acceptability to the filter)."""
+            if not (math.isfinite(theta_t) and math.isfinite(phi_t)):
+                return False, False
+            switching = gphi_d < 0 and alpha * (-gphi_d) ** opts.s_phi > opts.delta_switch * theta ** opts.s_theta
+            if theta <= theta_min and switching:
+                ok = phi_t <= phi + opts.eta_phi * alpha * gphi_d
+                f_type = True
+            else:
+                ok = theta_t <= theta_max and (theta_t <= (1 - opts.gamma_theta) * theta or
+                                               phi_t <= phi - opts.gamma_phi * theta)
+                f_type = False
+            ok = ok and all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt)
+            return ok, f_type
+
+        def trial(yt):
+            with _Phase("eval_fg"):
+                ft, gt = nlp.eval_fg(yt[:n])
+            ct = nlp.constraints(gt, yt[n:])
+            return ct, float(ct.abs().sum().item()), float(barrier_phi(ft, yt).item())
+
+        def line_search(dy, dlam, rhs_top):
+            """Filter line search from the fraction-to-the-boundary step, with IPOPT's second-order
+            corrections when the first trial is rejected with theta_trial >= theta.  Returns
+            (alpha, y_trial, dy, dlam) -- dy/dlam replaced by the corrected step when a
+            correction was accepted -- or None."""
             nonlocal filt
             alpha = min(max_step(dl, dy, hl), max_step(du, -dy, hu))
+            ls_info["alpha_max"] = alpha
+            if opts.verbose and alpha < 1.0:
+                rl = torch.where(hl & (dy < 0), -tau * dl / dy, torch.full_like(dy, math.inf))
+                ru = torch.where(hu & (dy > 0), tau * du / dy, torch.full_like(dy, math.inf))
+                r2 = torch.minimum(rl, ru)
+                ls_info["ftb_index"] = int(r2.argmin().item())
+            ls_info["backtracks"] = 0
+            ls_info["soc"] = 0
             gphi_d = float((grad_phi * dy).sum().item())
             alpha_min = opts.alpha_min_frac * min(opts.gamma_theta, opts.gamma_phi * theta / max(-gphi_d, 1e-300)
                                                    if gphi_d < 0 else opts.gamma_theta)
-            for _ in range(opts.max_backtracks):
+            for bt in range(opts.max_backtracks):
                 yt = y + alpha * dy
-                with _Phase("eval_fg"):
-                    ft, gt = nlp.eval_fg(yt[:n])
-                ct = nlp.constraints(gt, yt[n:])
-                theta_t = float(ct.abs().sum().item())
-                phi_t = float(barrier_phi(ft, yt).item())
-                if math.isfinite(theta_t) and math.isfinite(phi_t):
-                    switching = gphi_d < 0 and alpha * (-gphi_d) ** opts.s_phi > opts.delta_switch * theta ** opts.s_theta
-                    if theta <= theta_min and switching:
-                        if phi_t <= phi + opts.eta_phi * alpha * gphi_d:
-                            return alpha, yt
-                    elif theta_t <= theta_max and (theta_t <= (1 - opts.gamma_theta) * theta or
-                                                   phi_t <= phi - opts.gamma_phi * theta):
-                        if all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt):
-                            filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
-                            return alpha, yt
+                ct, theta_t, phi_t = trial(yt)
+                ok, f_type = acceptable(alpha, theta_t, phi_t, gphi_d)
+                if ok:
+                    if not f_type:
+                        filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
+                    return alpha, yt, dy, dlam
+                if bt == 0 and opts.max_soc > 0 and skkt is not None and math.isfinite(theta_t) and theta_t >= theta:
+                    # second-order correction (Waechter & Biegler 2006, section 2.4): same matrix,
+                    # constraint part of the right-hand side c_soc = alpha c(y) + c(y_trial)
+                    c_soc = alpha * c + ct
+                    theta_old = theta_t
+                    for _p in range(opts.max_soc):
+                        with _Phase("kkt_solve"):
+                            sol = skkt.solve(torch.cat([rhs_top, -c_soc]))
+                        if not bool(torch.isfinite(sol).all().item()):
+                            break
+                        dys = sol[:ny]
+                        a_s = min(max_step(dl, dys, hl), max_step(du, -dys, hu))
+                        ys = y + a_s * dys
+                        cs_, theta_s, phi_s = trial(ys)
+                        ls_info["soc"] += 1
+                        ok, f_type = acceptable(alpha, theta_s, phi_s, gphi_d)
+                        if ok:
+                            if not f_type:
+                                filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
+                            return a_s, ys, dys, sol[ny:]
+                        if not math.isfinite(theta_s) or theta_s > opts.kappa_soc * theta_old:
+                            break
+                        theta_old = theta_s
+                        c_soc = a_s * c_soc + cs_
+                if opts.verbose and bt < 8:
+                    print(f"     ls bt={bt} alpha={alpha:.3e} theta {theta:.6e}->{theta_t:.6e} phi {phi:.10e}->{phi_t:.10e} "
+                          f"gphi_d={gphi_d:.3e} theta_min={theta_min:.2e} filt={len(filt)}", flush=True)
                 alpha *= 0.5
+                ls_info["backtracks"] += 1
                 if alpha < alpha_min:
                     break
             return None
 
         accepted = None
         delta_w = 0.0
+        ls_info = {}
         for dw_floor in (0.0, 1e-2, 1.0, 1e2):
             nd = newton_direction(dw_floor)
             if nd is None:
                 continue
             dy, dlam, delta_w = nd
-            accepted = line_search(dy)
+            accepted = line_search(dy, dlam, -(grad_phi + A_T_lam(jv, lam)))
             if accepted is not None:
                 break
         if accepted is None:
@@ -822,9 +929,23 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
             y, lam = rest
             filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
             dl, du = gaps(y)
-            zl = torch.where(hl, torch.clamp(mu / dl, max=1e3), zl)
-            zu = torch.where(hu, torch.clamp(mu / du, max=1e3), zu)
             f, grad, g, jv = nlp.eval_all(y[:n])
+            if skkt is not None and exact_inertia:
+                # IPOPT after restoration: bound multipliers kept within the kappa_sigma band of the
+                # new point, constraint multipliers by least squares on the dual infeasibility,
+                # [I A^T; A 0] (w, lam) = (-(grad f - z_L + z_U), 0)
+                zl = torch.where(hl, torch.clamp(zl, min=mu / (opts.kappa_sigma * dl), max=opts.kappa_sigma * mu / dl), zl)
+                zu = torch.where(hu, torch.clamp(zu, min=mu / (opts.kappa_sigma * du), max=opts.kappa_sigma * mu / du), zu)
+                try:
+                    skkt.factor(hv_zero, torch.ones(ny, **f64), jv, 0.0, mI)
+                    sol = skkt.solve(torch.cat([-(grad_y(grad) - zl + zu), torch.zeros(m, **f64)]))
+                    if bool(torch.isfinite(sol).all().item()):
+                        lam = sol[ny:]
+                except RuntimeError:
+                    pass
+            else:
+                zl = torch.where(hl, torch.clamp(mu / dl, max=1e3), zl)
+                zu = torch.where(hu, torch.clamp(mu / du, max=1e3), zu)
             it += 1
             log.append(dict(it=it, f=float(f.item()) / nlp.obj_scale, inf_pr=e_p, inf_du=e_d, mu=mu,
                             alpha=0.0, alpha_z=0.0, delta_w=-1.0))
@@ -832,7 +953,7 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
                 print(f"{it:4d} restoration theta {theta:.3e} -> {float(nlp.constraints(g, y[n:]).abs().sum().item()):.3e}",
                       flush=True)
             continue
-        alpha, yt = accepted
+        alpha, yt, dy, dlam = accepted
         dzl = torch.where(hl, mu / dl - zl - zl / dl * dy, torch.zeros_like(y))
         dzu = torch.where(hu, mu / du - zu + zu / du * dy, torch.zeros_like(y))
         alpha_z = min(max_step(zl, dzl, hl), max_step(zu, dzu, hu))
@@ -848,7 +969,7 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
             f, grad, g, jv = nlp.eval_all(y[:n])
         it += 1
         rec = dict(it=it, f=float(f.item()) / nlp.obj_scale, inf_pr=e_p, inf_du=e_d, mu=mu, alpha=alpha,
-                   alpha_z=alpha_z, delta_w=delta_w)
+                   alpha_z=alpha_z, delta_w=delta_w, **ls_info)
         log.append(rec)
         if opts.verbose:
             print(f"{it:4d} f={rec['f']: .8e} pr={e_p:.2e} du={e_d:.2e} mu={mu:.1e} a={alpha:.2e} dw={delta_w:.1e}",

@@ -32,7 +32,7 @@ def hippo_options(label: str, base: IpmOptions | None = None) -> IpmOptions:
 
 def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device="cuda",
              v_init: np.ndarray | None = None, final_step: str | None = None, verbose=False,
-             u_ref: float | None = None):
+             u_ref: float | None = None, keep_logs=False):
     """Run the homotopy; returns (V_opt, per-step summaries, outputs, last IpmResult).
     ``u_ref`` overrides the wind reference speed in P (the sweep parameter)."""
     lay = pb.NlpLayout(consts.cfg.n_k, consts.cfg.d)
@@ -50,6 +50,8 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
         rec = dict(step=st.label, status=res.status, iterations=res.iterations, f=res.f,
                    kkt_error=res.kkt_error, constr_viol=res.constr_viol, seconds=time.perf_counter() - t0,
                    **out)
+        if keep_logs:
+            rec["log"] = res.log
         summary.append(rec)
         if verbose:
             print(rec, flush=True)

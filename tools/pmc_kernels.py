@@ -9,9 +9,34 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def ap2(B=2048):
+    """5 batched AP2 N=40 d=4 evaluations at the bench's batch (the headline kernel)."""
+    import numpy as np
+    import torch
+
+    from awebox_amd import problem as pb
+    from awebox_amd.evaluator import Ap2Evaluator
+    from awebox_amd.initial_guess import batch_member, initial_guess
+    dev = torch.device("cuda:0")
+    consts = pb.build_constants()
+    lay = pb.NlpLayout(40, 4)
+    v0 = initial_guess(consts, lay)
+    V = torch.tensor(np.stack([batch_member(v0, lay, b) for b in range(B)]), device=dev)
+    P = torch.tensor(np.stack([pb.pack_p(lay, consts, v0)] * B), device=dev)
+    ev = Ap2Evaluator(consts, batch=B)
+    out = [torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, ev.n_g, dtype=torch.float64, device=dev),
+           torch.empty(B, ev.n_v, dtype=torch.float64, device=dev), torch.empty(B, ev.nnz, dtype=torch.float64, device=dev)]
+    for _ in range(5):
+        ev.eval_nlp_device(V, P, *out)
+    torch.cuda.synchronize()
+    print("pmc ap2 done", flush=True)
+
+
 def main():
     import numpy as np
     import torch
+    if "--ap2" in sys.argv:
+        return ap2()
 
     from awebox_amd import dual as du
     from awebox_amd import kite3 as k3

@@ -30,7 +30,7 @@ if __name__ == "__main__":
         batch = int(args[1])
         args = args[2:]
     pats = args or ["gpurun_out/*/run_counter_collection.csv"]
-    paths = [p for pat in pats for p in glob.glob(pat)]
+    paths = [p for pat in pats for p in glob.glob(pat, recursive=True)]
     summ = summarise(paths)
     for k, v in sorted(summ.items()):
         print(f"{k:28s} {v:16.1f}")
