@@ -11,7 +11,7 @@
   assembly, Schur updates and sparse products are fixed-order sums, ipm._ScatterSum).
 * The NLP has several local optima near the reference's (35.9 s / 4.79 kW, f = -0.9191;
   51.7 s / 4.88 kW, f = -0.9379; ...): the anchor and the integrator checks run on the 35.9 s
-  orbit (a KKT point of this NLP, fixture tests/golden/ap2_n40_orbit_35s.npz), the full homotopy
+  orbit (a KKT point of this NLP, fixture tests/fixtures/ap2_n40_orbit_35s.npz), the full homotopy
   test on whichever optimum the path reaches.
 
 CPU: the same checks on the CPU port (test infrastructure, oracle/cpu_device.py) at N=6 d=3.
@@ -125,7 +125,7 @@ def test_ap2_n40_reference_orbit_anchor_and_integrators():
     from awebox_amd.evaluator import Ap2Evaluator
     from awebox_amd.ipm import solve
     from awebox_amd.trajectory import hippo_options
-    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "ap2_n40_orbit_35s.npz"))
+    fx = np.load(os.path.join(os.path.dirname(__file__), "fixtures", "ap2_n40_orbit_35s.npz"))
     consts = pb.build_constants()
     lay = pb.NlpLayout(40, 4)
     ev = Ap2Evaluator(consts, batch=1)
