@@ -111,14 +111,15 @@ class BorderedBtd:
 
     def inertia(self):
         """[B, 3] (positive, negative, zero) eigenvalue counts of the separator matrix S: the pivot
-        blocks D'_k of the block sweep (their inverses Dinv_k have the same signs) plus the border's
+        blocks D'_k of the block sweep (Bunch-Kaufman on the blocks themselves, not on their
+        explicit inverses, whose signs are unreliable when a block is nearly singular) plus the border's
         Schur complement C' (Haynsworth additivity); the identity rows of unused block positions
         are taken out."""
         from .batched_lu import sym_inertia, sym_inertia_host
         B, nb, m = self.B, self.nb, self.m
         if self.Tf[0].is_cuda:
-            F, Dinv = self.Tf
-            c = sym_inertia(Dinv.reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
+            F, Dinv = self.Tf                              # F's diagonal slots hold the pivot blocks D'_k
+            c = sym_inertia(F[:, :, 1].reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
         else:                                              # host: the pivot blocks by the block recursion
             T = self.T_blocks
             D = T[:, 0, 1]

@@ -50,6 +50,8 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
         rec = dict(step=st.label, status=res.status, iterations=res.iterations, f=res.f,
                    kkt_error=res.kkt_error, constr_viol=res.constr_viol, seconds=time.perf_counter() - t0,
                    **out)
+        if res.timing:
+            rec["timing"] = {k: round(v, 3) for k, v in res.timing.items()}
         if keep_logs:
             rec["log"] = res.log
         summary.append(rec)
