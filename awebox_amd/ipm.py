@@ -7,26 +7,30 @@ available here, so this module restates the IPOPT algorithm (Waechter & Biegler,
 
 * NLP functions, gradient, Jacobian and the exact Hessian of the Lagrangian come from the HIP
   evaluator (awebox_amd.evaluator) on device tensors;
+* B instances of one NLP structure (sweep points, homotopy runs) are solved side by side
+  (solve_batch): each keeps its own IPOPT iteration, while evaluations, Hessians and KKT
+  factorisations are batched;
 * the primal-dual KKT system [W + Sigma + dw I, A^T; A, -dc I] is solved by structured
   elimination (StructuredKKT: batched LU of the interval interiors on the awelu kernel, a dense
   or block-tridiagonal Schur complement on the separators), assembled in a fixed summation order
-  (deterministic gather-sum tables); the inertia correction uses the curvature test of Chiang &
-  Zavala (2016) instead of an inertia-revealing factorisation;
+  (deterministic gather-sum tables); IPOPT's inertia correction gets the exact inertia of K from
+  Bunch-Kaufman counts of the interval blocks and the separator pivot blocks (Haynsworth
+  additivity); the curvature test of Chiang & Zavala (2016) remains as an option;
 * fixed variables (lbx == ubx) are removed (IPOPT's fixed_variable_treatment=make_parameter);
   inequality rows get slacks; gradient-based NLP scaling, bound push, monotone Fiacco-McCormick
   barrier update, fraction-to-the-boundary rule and the filter line search follow IPOPT's
   defaults (tol 1e-8, mu_init 0.1, kappa_mu 0.2, theta_mu 1.5, tau_min 0.99);
+* second-order corrections in the line search (max_soc 4, kappa_soc 0.99);
 * after a failed line search: a retry with stronger regularisation, then a reduced feasibility
-  restoration (Gauss-Newton steps on ||c|| inside the bounds until the filter accepts).
+  restoration (Gauss-Newton steps on ||c|| inside the bounds until the filter accepts) followed
+  by least-squares constraint multipliers.
 
-What is left out: second-order corrections, IPOPT's full restoration-phase NLP, and quasi-Newton
-options.
+What is left out: IPOPT's full restoration-phase NLP, the watchdog, and quasi-Newton options.
 """
 from __future__ import annotations
 
 import math
 import time
-import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -71,7 +75,6 @@ class IpmOptions:
     kkt: str = "structured"          # "structured" (interval elimination + Schur) or "dense"
     lu_backend: str = "awelu"        # interval-block LU: "awelu" (batched_lu.hip) or "torch" (rocSOLVER)
     separators: str = "btd"          # separator system: "dense" LU or "btd" (awebox_amd/btd.py block sweep)
-    deterministic: bool = True       # KKT assembly by gather-sum tables instead of atomic scatter-adds
     inertia: str = "exact"           # inertia correction: "curvature" test (Chiang & Zavala) or "exact" (IPOPT:
                                      # In(K) = In(K_II) + In(S) from symmetric eigenvalues of the blocks)
     profile: bool = False            # synchronise and time the solver's phases (IpmResult.timing)
@@ -97,12 +100,16 @@ class IpmResult:
 
 
 class DeviceNlp:
-    """Evaluator-backed NLP restricted to the free variables, with slacks for inequality rows."""
+    """Evaluator-backed NLP restricted to the free variables, with slacks for inequality rows, for
+    B instances at once (the evaluator's batch): same structure (free set, inequality rows,
+    bounds), per-instance P and scaling."""
 
     def __init__(self, ev, P, lbx, ubx, lbg, ubg, device):
         self.ev, self.dev = ev, device
         n_v, n_g = ev.n_v, ev.n_g
-        self.P = torch.tensor(np.asarray(P, dtype=np.float64).reshape(1, -1), device=device)
+        P = np.atleast_2d(np.asarray(P, dtype=np.float64))
+        self.B = B = P.shape[0]
+        self.P = torch.tensor(P, device=device)
         lbx, ubx = np.asarray(lbx, dtype=np.float64), np.asarray(ubx, dtype=np.float64)
         self.fixed = lbx >= ubx
         self.free = np.where(~self.fixed)[0]
@@ -113,11 +120,11 @@ class DeviceNlp:
         self.eq = np.where(lbg >= ubg)[0]
         self.m, self.mI = n_g, len(self.ineq)
         self.g_target = torch.tensor(np.where(lbg >= ubg, lbg, 0.0), device=device)
-        # bounds of y = [x_free; s]
+        # bounds of y = [x_free; s] (slack bounds are scaled per instance once c_scale is known)
         yl = np.concatenate([lbx[self.free], lbg[self.ineq]])
         yu = np.concatenate([ubx[self.free], ubg[self.ineq]])
-        self.yl = torch.tensor(yl, device=device)
-        self.yu = torch.tensor(yu, device=device)
+        self.yl = torch.tensor(np.tile(yl, (B, 1)), device=device)
+        self.yu = torch.tensor(np.tile(yu, (B, 1)), device=device)
         self.has_l = torch.isfinite(self.yl)
         self.has_u = torch.isfinite(self.yu)
         self.ny = self.n + self.mI
@@ -139,70 +146,48 @@ class DeviceNlp:
         self.h_offdiag = self.h_r != self.h_c
         self.s_row = torch.tensor(self.ineq.astype(np.int64), device=device)
         # device buffers of the evaluator
-        B = 1
-        self.V = torch.tensor(self.x_fix.reshape(1, -1), device=device)
-        self.f = torch.zeros(B, dtype=torch.float64, device=device)
-        self.g = torch.zeros(B, n_g, dtype=torch.float64, device=device)
-        self.grad = torch.zeros(B, n_v, dtype=torch.float64, device=device)
-        self.jac = torch.zeros(B, ev.nnz, dtype=torch.float64, device=device)
-        self.H = torch.zeros(B, ev.nnz_h, dtype=torch.float64, device=device)
-        self.sig = torch.ones(B, dtype=torch.float64, device=device)
+        f64 = dict(dtype=torch.float64, device=device)
+        self.V = torch.tensor(np.tile(self.x_fix, (B, 1)), device=device)
+        self.f = torch.zeros(B, **f64)
+        self.g = torch.zeros(B, n_g, **f64)
+        self.grad = torch.zeros(B, n_v, **f64)
+        self.jac = torch.zeros(B, ev.nnz, **f64)
+        self.H = torch.zeros(B, ev.nnz_h, **f64)
+        self.sig = torch.ones(B, **f64)
         self.free_t = torch.tensor(self.free, device=device)
         self.ineq_t = torch.tensor(self.ineq, device=device)
-        self.obj_scale = 1.0
-        self.c_scale = torch.ones(n_g, dtype=torch.float64, device=device)
+        self.obj_scale = torch.ones(B, **f64)
+        self.c_scale = torch.ones(B, n_g, **f64)
 
     def full_x(self, x):
-        self.V[0, self.free_t] = x
+        self.V[:, self.free_t] = x
         return self.V
 
     def eval_all(self, x):
-        """f, grad_f (reduced), c(y) pieces: g(x) and the Jacobian values (reduced, scaled)."""
+        """f [B], grad_f (reduced) [B, n], g [B, m] and the Jacobian values (reduced, scaled)."""
         self.ev.eval_nlp_device(self.full_x(x), self.P, self.f, self.g, self.grad, self.jac)
-        f = self.f[0] * self.obj_scale
-        grad = self.grad[0, self.free_t] * self.obj_scale
-        g = self.g[0] * self.c_scale
-        jv = self.jac[0, self.j_keep] * self.c_scale[self.j_row]
+        f = self.f * self.obj_scale
+        grad = self.grad[:, self.free_t] * self.obj_scale[:, None]
+        g = self.g * self.c_scale
+        jv = self.jac[:, self.j_keep] * self.c_scale[:, self.j_row]
         return f, grad, g, jv
 
     def eval_fg(self, x):
         self.ev.eval_nlp_device(self.full_x(x), self.P, self.f, self.g, self.grad, self.jac)
-        return self.f[0] * self.obj_scale, self.g[0] * self.c_scale
+        return self.f * self.obj_scale, self.g * self.c_scale
 
     def hess(self, x, lam):
-        """Hessian of obj_scale f + (c_scale lam)^T g, reduced upper values."""
-        lam_unscaled = (lam * self.c_scale).reshape(1, -1).contiguous()
-        self.sig[0] = self.obj_scale
+        """Hessian of obj_scale f + (c_scale lam)^T g, reduced upper values [B, nH]."""
+        lam_unscaled = (lam * self.c_scale).contiguous()
+        self.sig.copy_(self.obj_scale)
         self.ev.eval_hess_device(self.full_x(x), self.P, self.sig, lam_unscaled, self.H)
-        return self.H[0, self.h_keep]
+        return self.H[:, self.h_keep]
 
     def constraints(self, g, s):
-        """c(y) = [g_E - target; g_I - s] (scaled rows)."""
+        """c(y) = [g_E - target; g_I - s] (scaled rows), [B, m]."""
         c = g - self.g_target * self.c_scale
-        c = c.clone()
-        c[self.ineq_t] = c[self.ineq_t] - s
+        c[:, self.ineq_t] = c[:, self.ineq_t] - s
         return c
-
-
-class _Csr:
-    """Fixed COO pattern as a CSR operator: y = A(vals) x through a sparse matrix-vector product
-    (no atomics; fp64 scatter-adds with many duplicates are slow on the GPU)."""
-
-    def __init__(self, rows, cols, shape, dev):
-        rows = np.asarray(rows, dtype=np.int64)
-        cols = np.asarray(cols, dtype=np.int64)
-        order = np.lexsort((cols, rows))
-        self.perm = torch.tensor(order, device=dev)
-        self.col = torch.tensor(cols[order], device=dev)
-        self.crow = torch.tensor(np.concatenate([[0], np.cumsum(np.bincount(rows, minlength=shape[0]))]),
-                                 dtype=torch.int64, device=dev)
-        self.shape = shape
-
-    def mv(self, vals, x):
-        with warnings.catch_warnings():
-            warnings.filterwarnings("ignore", message="Sparse CSR tensor support is in beta state")
-            A = torch.sparse_csr_tensor(self.crow, self.col, vals[self.perm], size=self.shape)
-        return (A @ x.unsqueeze(1)).squeeze(1)
 
 
 class _ScatterSum:
@@ -268,9 +253,13 @@ ZERO_PIVOT = 1e-30   # relative zero-pivot threshold of the inertia count: KKT p
                      # 1e-10 .. 1e10 at small mu, so only exactly singular columns count as zero
 
 
+ZERO_PIVOT = 1e-30   # relative zero-pivot threshold of the inertia count: KKT pivots legitimately span
+                     # 1e-10 .. 1e10 at small mu, so only exactly singular columns count as zero
+
+
 class StructuredKKT:
     """KKT solve by elimination of every interval's interior unknowns (batched dense LU on the
-    GPU) and a dense Schur complement on the separators.
+    GPU) and a Schur complement on the separators, for B instances of one KKT pattern at once.
 
     Intervals of the collocation NLP couple only through the shooting states x[k] (shared by
     interval k and the continuity rows of interval k-1), the free global variables (t_f and
@@ -279,13 +268,16 @@ class StructuredKKT:
     collocation variables, the path slacks and the multipliers of interval k's node, path and
     collocation rows -- is interior to interval k.  With K = [K_II, K_IS; K_SI, K_SS]:
         S = K_SS - sum_k K_SI^k (K_II^k)^-1 K_IS^k,
-    about 5 GFLOP at N=40 instead of the 1.3 TFLOP of a dense LU of the whole system."""
+    about 5 GFLOP at N=40 instead of the 1.3 TFLOP of a dense LU of the whole system.  The
+    B x n_k interval blocks are one batch of the awelu LU kernel; the separators are either B
+    block-tridiagonal chains (awebox_amd/btd.py) or B dense Schur complements.  Every assembly is
+    a fixed-order gather-sum (_ScatterSum): the results do not depend on the run."""
 
-    def __init__(self, nlp, lay, dev, lu_backend="awelu", separators="btd", deterministic=False):
+    def __init__(self, nlp, lay, dev, lu_backend="awelu", separators="btd", deterministic=True):
         n, ny, m = nlp.n, nlp.ny, nlp.m
         self.lu_backend = lu_backend
         N = ny + m
-        self.N, self.dev = N, dev
+        self.N, self.dev, self.ny = N, dev, ny
         n_k, stride, v0, rows = lay.n_k, lay.interval_stride, lay.v_intervals, lay.rows_per_interval
         nx = getattr(lay, "nx", pb.NX)                          # states per shooting node
         owner = np.full(N, -1, dtype=np.int64)                  # interval of an interior unknown
@@ -322,7 +314,6 @@ class StructuredKKT:
         Q_ = np.concatenate([hc, hr[off], np.arange(ny), jc, ny + jr, sc, ny + sr, ny + np.arange(m)])
         self.off_mask = torch.tensor(off, device=dev)
         self.P_, self.Q_ = torch.tensor(P_, device=dev), torch.tensor(Q_, device=dev)
-        self.csr = _Csr(P_, Q_, (N, N), dev)
         self.n_solve = self.n_dense = 0
         oP, oQ = owner[P_], owner[Q_]
         ii = (oP >= 0) & (oP == oQ)
@@ -340,26 +331,22 @@ class StructuredKKT:
         self.lsep = torch.tensor(lsep_arr, device=dev)
         nI, L, nS = self.nI, self.L, self.nS
         self.sel_ii = torch.tensor(np.where(ii)[0], device=dev)
-        self.dst_ii = torch.tensor(oP[ii] * nI * nI + loc[P_[ii]] * nI + loc[Q_[ii]], device=dev)
+        dst_ii = oP[ii] * nI * nI + loc[P_[ii]] * nI + loc[Q_[ii]]
         isi = np.where(is_)[0]
         self.sel_is = torch.tensor(isi, device=dev)
-        self.dst_is = torch.tensor(oP[isi] * nI * L + loc[P_[isi]] * L + lpos[oP[isi], sep_id[Q_[isi]]], device=dev)
+        dst_is = oP[isi] * nI * L + loc[P_[isi]] * L + lpos[oP[isi], sep_id[Q_[isi]]]
         self.sel_ss = torch.tensor(np.where(ss)[0], device=dev)
-        self.dst_ss = torch.tensor(sep_id[P_[ss]] * (nS + 1) + sep_id[Q_[ss]], device=dev)
+        dst_ss = sep_id[P_[ss]] * (nS + 1) + sep_id[Q_[ss]]
         pad = [(k, j) for k in range(n_k) for j in range(int(counts[k]), nI)]
+        self.n_pad = len(pad)
         self.pad_flat = torch.tensor([k * nI * nI + j * nI + j for k, j in pad], dtype=torch.int64, device=dev)
-        r_idx = self.lsep[:, :, None].expand(n_k, L, L)
-        c_idx = self.lsep[:, None, :].expand(n_k, L, L)
-        self.schur_flat = (r_idx * (nS + 1) + c_idx).reshape(-1)
+        schur_flat = (lsep_arr[:, :, None] * (nS + 1) + lsep_arr[:, None, :]).reshape(-1)
         int_p = np.where(owner >= 0)[0]
         self.int_p = torch.tensor(int_p, device=dev)
-        self.sc = None
-        if deterministic:
-            self.sc = [_ScatterSum(t.cpu().numpy(), dev) for t in (self.dst_ii, self.dst_is, self.dst_ss,
-                                                                    self.schur_flat)]
-            self.sc_mv = _ScatterSum(P_, dev)
-            self.sc_dense = _ScatterSum(P_ * N + Q_, dev)
-            self.sc_rs = _ScatterSum(lsep_arr.reshape(-1), dev)
+        self.sc = [_ScatterSum(t, dev) for t in (dst_ii, dst_is, dst_ss, schur_flat)]
+        self.sc_mv = _ScatterSum(P_, dev)
+        self.sc_dense = _ScatterSum(P_ * N + Q_, dev)
+        self.sc_rs = _ScatterSum(lsep_arr.reshape(-1), dev)
         # separators in stages [c[k-1], x[k]] (block tridiagonal, globals as border): pairing each
         # shooting state with the multipliers of the continuity row that defines it keeps the block
         # sweep's pivot blocks regular -- the finer order x[0], c[0], x[1], ... meets near-singular
@@ -390,35 +377,33 @@ class StructuredKKT:
             try:
                 self.btd = BorderedBtd(stage_of, pos_of, n_k + 1, 2 * nx,
                                        np.concatenate([ss_r, sch_r.reshape(-1)]),
-                                       np.concatenate([ss_c, sch_c.reshape(-1)]), dev,
-                                       deterministic=deterministic)
+                                       np.concatenate([ss_c, sch_c.reshape(-1)]), dev)
             except ValueError:
                 self.btd = None                                 # not stage-structured: dense S
         self.int_flat = torch.tensor(owner[int_p] * nI + loc[int_p], device=dev)
         self.sep_p = torch.tensor(sep, device=dev)
 
+    # ---------------------------------------------------------------------------------------
     def factor(self, hv, diag, jv, delta_c, mI):
+        """Factorise K for every instance: hv [B, nH] Hessian values, diag [B, ny] (Sigma +
+        delta_w), jv [B, nJ] Jacobian values, delta_c float or [B] (1-D inputs: one instance)."""
         f64 = dict(dtype=torch.float64, device=self.dev)
-        m = self.N - diag.numel()
-        vals = torch.cat([hv, hv[self.off_mask], diag, jv, jv, -torch.ones(2 * mI, **f64),
-                          torch.full((m,), -float(delta_c), **f64)])
+        self.squeeze = hv.dim() == 1
+        hv, diag, jv = (t.unsqueeze(0) if t.dim() == 1 else t for t in (hv, diag, jv))
+        B = hv.shape[0]
+        self.B = B
+        m = self.N - diag.shape[1]
+        dc = torch.as_tensor(delta_c, dtype=torch.float64, device=self.dev).reshape(-1).expand(B)
+        vals = torch.cat([hv, hv[:, self.off_mask], diag, jv, jv, -torch.ones(B, 2 * mI, **f64),
+                          -dc[:, None].expand(B, m)], dim=1)
         self.vals = vals
-        self.k_norm = float(self._mv(vals.abs(), torch.ones(self.N, **f64)).max().item())
+        self.k_norm = self._mv(vals.abs(), torch.ones(B, self.N, **f64)).amax(dim=1)     # [B]
         nI, L, nS, n_k = self.nI, self.L, self.nS, self.n_k
-        KII = torch.zeros(n_k * nI * nI, **f64)
-        if self.sc:
-            self.sc[0].add_into(KII, vals[self.sel_ii])
-        else:
-            KII.index_put_((self.dst_ii,), vals[self.sel_ii], accumulate=True)
-        KII[self.pad_flat] = 1.0
-        KII = KII.view(n_k, nI, nI)
+        KII = self.sc[0].add_into(torch.zeros(B, n_k * nI * nI, **f64), vals[:, self.sel_ii])
+        KII[:, self.pad_flat] = 1.0
+        KII = KII.view(B * n_k, nI, nI)
         self.KII = KII
-        KIS = torch.zeros(n_k * nI * L, **f64)
-        if self.sc:
-            self.sc[1].add_into(KIS, vals[self.sel_is])
-        else:
-            KIS.index_put_((self.dst_is,), vals[self.sel_is], accumulate=True)
-        KIS = KIS.view(n_k, nI, L)
+        KIS = self.sc[1].add_into(torch.zeros(B, n_k * nI * L, **f64), vals[:, self.sel_is]).view(B * n_k, nI, L)
         self.awelu = self.lu_backend == "awelu" and KII.is_cuda   # the CPU test harness uses LAPACK
         if self.awelu:
             from .batched_lu import lu_factor
@@ -426,138 +411,154 @@ class StructuredKKT:
         else:
             self.LU_I, self.piv_I = torch.linalg.lu_factor(KII)
         self.X = self._block_solve(KIS)                                        # K_II^-1 K_IS
-        T = KIS.transpose(1, 2) @ self.X                                       # [n_k, L, L]
+        T = (KIS.transpose(1, 2) @ self.X).reshape(B, n_k * L * L)             # [B, n_k L L]
         self.KIS = KIS
         if self.btd is not None and not self.btd_off and (KII.is_cuda or self.force_btd):
-            self.btd.factor(torch.cat([vals[self.sel_ss], -T.reshape(-1)]))
+            self.btd.factor(torch.cat([vals[:, self.sel_ss], -T], dim=1))
             self.use_btd = True
             return
         self.use_btd = False
-        S = torch.zeros((nS + 1) * (nS + 1), **f64)
-        if self.sc:
-            self.sc[2].add_into(S, vals[self.sel_ss])
-            self.sc[3].add_into(S, -T.reshape(-1))
-        else:
-            S.index_put_((self.dst_ss,), vals[self.sel_ss], accumulate=True)
-            S.index_put_((self.schur_flat,), -T.reshape(-1), accumulate=True)
-        S = S.view(nS + 1, nS + 1)
-        S[nS, :] = 0.0
-        S[:, nS] = 0.0
-        S[nS, nS] = 1.0
+        S = torch.zeros(B, (nS + 1) * (nS + 1), **f64)
+        self.sc[2].add_into(S, vals[:, self.sel_ss])
+        self.sc[3].add_into(S, -T)
+        S = S.view(B, nS + 1, nS + 1)
+        S[:, nS, :] = 0.0
+        S[:, :, nS] = 0.0
+        S[:, nS, nS] = 1.0
         self.S = S
         self.LU_S, self.piv_S = torch.linalg.lu_factor(S)
 
     def inertia(self):
-        """(positive, negative, zero) eigenvalue counts of K by Haynsworth's additivity,
-        In(K) = sum_k In(K_II^k) + In(S): Bunch-Kaufman inertia of the interval blocks (padding
-        rows excluded) and of the separator system -- the dense Schur complement S, or with the
-        block-tridiagonal separators the sweep's pivot blocks and the border (btd.BorderedBtd)."""
+        """(positive, negative, zero) eigenvalue counts of K per instance, int64 [B, 3] (a tuple for
+        a one-instance factor()), by Haynsworth's additivity In(K) = sum_k In(K_II^k) + In(S):
+        Bunch-Kaufman inertia of the interval blocks (padding rows excluded) and of the separator
+        system -- the dense Schur complement, or with the block-tridiagonal separators the sweep's
+        pivot blocks and the border (btd.BorderedBtd)."""
         from .batched_lu import sym_inertia, sym_inertia_host
         f = sym_inertia if self.KII.is_cuda else sym_inertia_host
-        c = f(self.KII, ztol=ZERO_PIVOT).to(torch.int64).sum(0)
-        c[0] -= len(self.pad_flat)
+        B = self.B
+        c = f(self.KII, ztol=ZERO_PIVOT).to(torch.int64).view(B, self.n_k, 3).sum(1)
+        c[:, 0] -= self.n_pad
         if self.use_btd:
-            c = c + self.btd.inertia()[0]
+            c = c + self.btd.inertia()
         else:
-            cs = f(self.S.unsqueeze(0), ztol=ZERO_PIVOT).to(torch.int64)[0]
-            cs[0] -= 1                                          # the dummy separator's 1.0
+            cs = f(self.S, ztol=ZERO_PIVOT).to(torch.int64)
+            cs[:, 0] -= 1                                       # the dummy separator's 1.0
             c = c + cs
-        pos, neg, zero = (int(v) for v in c.cpu().tolist())
-        return pos, neg, zero
+        if self.squeeze:
+            return tuple(int(v) for v in c[0].cpu().tolist())
+        return c
 
     def _mv(self, vals, x):
-        """K(vals) x: a fixed-order gather-sum when deterministic, rocSPARSE CSR otherwise."""
-        if self.sc:
-            return self.sc_mv.add_into(torch.zeros(self.N, dtype=torch.float64, device=self.dev), vals * x[self.Q_])
-        return self.csr.mv(vals, x)
+        """K(vals) x for every instance: a fixed-order gather-sum."""
+        return self.sc_mv.add_into(torch.zeros(x.shape[0], self.N, dtype=torch.float64, device=self.dev),
+                                   vals * x[:, self.Q_])
 
     def matvec(self, x):
         return self._mv(self.vals, x)
 
     def solve(self, rhs, refine=3, rtol=1e-12):
-        """Elimination solve with iterative refinement on the sparse residual.  The interior
-        pivots come from blocks that may be ill-conditioned even when K is not (an indefinite
-        interior Hessian), so the result is accepted once its backward error is small,
-        ||K x - rhs|| <= rtol (||K|| ||x|| + ||rhs||) in the max norm; otherwise the system is
-        solved once by a dense LU of the assembled K."""
+        """Elimination solve with iterative refinement on the sparse residual, rhs [B, N] (or [N]).
+        The interior pivots come from blocks that may be ill-conditioned even when K is not (an
+        indefinite interior Hessian), so an instance's result is accepted once its backward error
+        is small, ||K x - rhs|| <= rtol (||K|| ||x|| + ||rhs||) in the max norm; an instance that
+        does not get there is solved once by a dense LU of its assembled K."""
+        one = rhs.dim() == 1
+        rhs = rhs.unsqueeze(0) if one else rhs
         self.n_solve += 1
         x = self._solve(rhs)
-        b_norm = float(rhs.abs().max().item())
-        self.backward = []
-        for _ in range(refine + 1):
+        b_norm = rhs.abs().amax(dim=1)
+        done = torch.zeros(rhs.shape[0], dtype=torch.bool, device=self.dev)
+        for it in range(refine + 1):
             r = rhs - self.matvec(x)
-            err = float(r.abs().max().item())
-            if not math.isfinite(err):
+            err = r.abs().amax(dim=1)
+            scale = self.k_norm * x.abs().amax(dim=1) + b_norm
+            done = done | (err <= rtol * scale)
+            bad = ~torch.isfinite(err)
+            if bool((done | bad).all().item()) or it == refine:
                 break
-            scale = self.k_norm * float(x.abs().max().item()) + b_norm
-            self.backward.append(err / scale)
-            if err <= rtol * scale:
-                return x
-            x = x + self._solve(r)
-        # ill-conditioned interior pivots: one dense LU of the assembled K for this system
-        self.n_dense += 1
-        K = torch.zeros(self.N * self.N, dtype=torch.float64, device=self.dev)
-        if self.sc:
-            self.sc_dense.add_into(K, self.vals)
-        else:
-            K.index_put_((self.P_ * self.N + self.Q_,), self.vals, accumulate=True)
-        return torch.linalg.solve(K.view(self.N, self.N), rhs)
+            x = torch.where(done[:, None], x, x + self._solve(r))
+        todo = (~done).nonzero().flatten().cpu().tolist()
+        for b in todo:                      # ill-conditioned interior pivots: dense LU of that K
+            self.n_dense += 1
+            K = self.sc_dense.add_into(torch.zeros(self.N * self.N, dtype=torch.float64, device=self.dev),
+                                       self.vals[b])
+            x[b] = torch.linalg.solve(K.view(self.N, self.N), rhs[b])
+        return x[0] if one else x
 
     def _block_solve(self, B):
         """K_II^-1 B for all interval blocks: triangular solves on the LU factors (rocBLAS on the
-        device, LAPACK in the CPU harness).  The awelu solve kernel (RTI's choice) is not used
-        here: it did not change the per-iteration time, and its roundoff moved the bench's 2-point
-        AP2 sweep to another local solution at 8 m/s (3,874 W over 60 s instead of 3,799 W over
-        29 s)."""
+        device, LAPACK in the CPU harness)."""
         return torch.linalg.lu_solve(self.LU_I, self.piv_I, B)
 
     def _solve(self, rhs):
         f64 = dict(dtype=torch.float64, device=self.dev)
         nI, L, nS, n_k = self.nI, self.L, self.nS, self.n_k
-        rI = torch.zeros(n_k * nI, **f64)
-        rI[self.int_flat] = rhs[self.int_p]
-        rI = rI.view(n_k, nI, 1)
-        rS = torch.zeros(nS + 1, **f64)
-        rS[:nS] = rhs[self.sep_p]
-        z = self._block_solve(rI)                                              # [n_k, nI, 1]
-        upd = (self.KIS.transpose(1, 2) @ z).reshape(-1)                      # [n_k * L]
-        if self.sc:
-            self.sc_rs.add_into(rS, -upd)
-        else:
-            rS = rS.index_add(0, self.lsep.reshape(-1), -upd)
-        rS[nS] = 0.0
+        B = rhs.shape[0]
+        rI = torch.zeros(B, n_k * nI, **f64)
+        rI[:, self.int_flat] = rhs[:, self.int_p]
+        rS = torch.zeros(B, nS + 1, **f64)
+        rS[:, :nS] = rhs[:, self.sep_p]
+        z = self._block_solve(rI.view(B * n_k, nI, 1))                         # [B n_k, nI, 1]
+        upd = (self.KIS.transpose(1, 2) @ z).reshape(B, n_k * L)
+        self.sc_rs.add_into(rS, -upd)
+        rS[:, nS] = 0.0
+        xS = torch.zeros(B, nS + 1, **f64)
         if self.use_btd:
-            xS = torch.zeros(nS + 1, **f64)
-            xS[:nS] = self.btd.solve(rS[:nS])
+            xS[:, :nS] = self.btd.solve(rS[:, :nS])
         else:
-            xS = torch.linalg.lu_solve(self.LU_S, self.piv_S, rS.view(-1, 1)).view(-1)
-        xI = z.view(n_k, nI) - (self.X @ xS[self.lsep].unsqueeze(-1)).view(n_k, nI)
-        sol = torch.empty(self.N, **f64)
-        sol[self.int_p] = xI.reshape(-1)[self.int_flat]
-        sol[self.sep_p] = xS[:nS]
+            xS = torch.linalg.lu_solve(self.LU_S, self.piv_S, rS.unsqueeze(-1)).squeeze(-1)
+        xI = z.view(B * n_k, nI) - (self.X @ xS[:, self.lsep].reshape(B * n_k, L, 1)).view(B * n_k, nI)
+        sol = torch.empty(B, self.N, **f64)
+        sol[:, self.int_p] = xI.view(B, n_k * nI)[:, self.int_flat]
+        sol[:, self.sep_p] = xS[:, :nS]
         return sol
+
+
+def _as_batch(a, B, n, fill=None):
+    """[B, n] float64 numpy array from None / [n] / [B, n]."""
+    if a is None:
+        return None if fill is None else np.full((B, n), fill)
+    a = np.asarray(a, dtype=np.float64)
+    return np.tile(a, (B, 1)) if a.ndim == 1 else a
 
 
 def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: IpmOptions | None = None,
           device="cuda") -> IpmResult:
-    """Solve min f s.t. lbg <= g <= ubg, lbx <= x <= ubx with the GPU interior-point method.
+    """Solve min f s.t. lbg <= g <= ubg, lbx <= x <= ubx for one instance with the GPU
+    interior-point method (solve_batch with B = 1)."""
+    return solve_batch(ev, np.atleast_2d(P), np.atleast_2d(x0), lbx, ubx, lbg, ubg,
+                       None if lam0 is None else np.atleast_2d(lam0),
+                       None if zl0 is None else np.atleast_2d(zl0),
+                       None if zu0 is None else np.atleast_2d(zu0), opts=opts, device=device)[0]
 
+
+def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: IpmOptions | None = None,
+                device="cuda") -> list[IpmResult]:
+    """Solve B instances of one NLP structure (P [B, n_p], x0 [B, n_v], shared bounds) side by side
+    with the GPU interior-point method; returns one IpmResult per instance.
+
+    Every instance runs its own IPOPT iteration (barrier parameter, filter, inertia correction,
+    line search, restoration, termination); their evaluations (ev.batch == B), Hessians and KKT
+    factorisations/solves are batched, so B instances cost little more per iteration than one.
     lam0 / zl0 / zu0 (constraint and V-bound multipliers of a previous solve) select IPOPT's
     warm_start_init_point: the multipliers are kept (pushed away from zero) and the primal point
     is pushed into the bounds with the smaller warm-start push."""
     opts = opts or IpmOptions()
     t_start = time.perf_counter()
     dev = torch.device(device)
+    P = np.atleast_2d(np.asarray(P, dtype=np.float64))
+    B = P.shape[0]
     nlp = DeviceNlp(ev, P, lbx, ubx, lbg, ubg, dev)
     n, mI, m, ny = nlp.n, nlp.mI, nlp.m, nlp.ny
     N = ny + m
     f64 = dict(dtype=torch.float64, device=dev)
-    log = []
+    logs = [[] for _ in range(B)]
+    x0 = _as_batch(x0, B, ev.n_v)
 
     # ---- initial point: bound push (IPOPT 3.6) -----------------------------------------------
-    x = torch.tensor(np.asarray(x0, dtype=np.float64)[nlp.free], **f64)
+    x = torch.tensor(x0[:, nlp.free], **f64)
     yl, yu, hl, hu = nlp.yl, nlp.yu, nlp.has_l, nlp.has_u
-
     warm = lam0 is not None
     bpush = opts.warm_start_bound_push if warm else opts.bound_push
     bfrac = opts.warm_start_bound_push if warm else opts.bound_frac
@@ -572,59 +573,59 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
         y = torch.where(hu, torch.minimum(y, hi - pu), y)
         return y
 
-    # gradient-based NLP scaling at the starting point (IPOPT nlp_scaling_method)
-    f0, grad0, g0, jv0 = nlp.eval_all(push(torch.cat([x, torch.zeros(mI, **f64)]))[:n])
-    gmax = float(grad0.abs().max().item()) if n else 0.0
-    nlp.obj_scale = min(1.0, opts.nlp_scaling_max_gradient / gmax) if gmax > 0 else 1.0
-    rowmax = torch.zeros(m, **f64).scatter_reduce_(0, nlp.j_row, jv0.abs(), "amax", include_self=True)
+    # gradient-based NLP scaling at the starting point (IPOPT nlp_scaling_method), per instance
+    f0, grad0, g0, jv0 = nlp.eval_all(push(torch.cat([x, torch.zeros(B, mI, **f64)], 1))[:, :n])
+    gmax = grad0.abs().amax(dim=1) if n else torch.zeros(B, **f64)
+    nlp.obj_scale = torch.where(gmax > 0, torch.clamp(opts.nlp_scaling_max_gradient / gmax, max=1.0),
+                                torch.ones_like(gmax))
+    rowmax = torch.zeros(B, m, **f64).scatter_reduce_(1, nlp.j_row.expand(B, -1), jv0.abs(), "amax",
+                                                      include_self=True)
     nlp.c_scale = torch.clamp(opts.nlp_scaling_max_gradient / torch.clamp(rowmax, min=1e-300), max=1.0)
-    # slack bounds live in the scaled constraint space
-    cs_I = nlp.c_scale[nlp.ineq_t]
-    nlp.yl[n:] = torch.where(nlp.has_l[n:], nlp.yl[n:] * cs_I, nlp.yl[n:])
-    nlp.yu[n:] = torch.where(nlp.has_u[n:], nlp.yu[n:] * cs_I, nlp.yu[n:])
+    cs_I = nlp.c_scale[:, nlp.ineq_t]
+    nlp.yl[:, n:] = torch.where(hl[:, n:], nlp.yl[:, n:] * cs_I, nlp.yl[:, n:])
+    nlp.yu[:, n:] = torch.where(hu[:, n:], nlp.yu[:, n:] * cs_I, nlp.yu[:, n:])
 
-    y = torch.cat([x, torch.zeros(mI, **f64)])
-    f, grad, g, jv = nlp.eval_all(y[:n])
-    y[n:] = g[nlp.ineq_t]
+    y = torch.cat([x, torch.zeros(B, mI, **f64)], 1)
+    f, grad, g, jv = nlp.eval_all(y[:, :n])
+    y[:, n:] = g[:, nlp.ineq_t]
     y = push(y)
-    lam = torch.zeros(m, **f64)
-    if lam0 is not None:
-        lam = torch.tensor(np.asarray(lam0, dtype=np.float64), **f64) / nlp.c_scale * nlp.obj_scale
-    zl = torch.where(hl, torch.ones(ny, **f64), torch.zeros(ny, **f64))
-    zu = torch.where(hu, torch.ones(ny, **f64), torch.zeros(ny, **f64))
+    lam = torch.zeros(B, m, **f64)
+    if warm:
+        lam = torch.tensor(_as_batch(lam0, B, m), **f64) / nlp.c_scale * nlp.obj_scale[:, None]
+    zl = torch.where(hl, torch.ones(B, ny, **f64), torch.zeros(B, ny, **f64))
+    zu = torch.where(hu, torch.ones(B, ny, **f64), torch.zeros(B, ny, **f64))
     if warm:
         floor = opts.warm_start_mult_bound_push
         if zl0 is not None:
-            zx = torch.tensor(np.asarray(zl0, dtype=np.float64)[nlp.free], **f64) * nlp.obj_scale
-            zl[:n] = torch.where(hl[:n], torch.clamp(zx, min=floor), zl[:n])
+            zx = torch.tensor(_as_batch(zl0, B, ev.n_v)[:, nlp.free], **f64) * nlp.obj_scale[:, None]
+            zl[:, :n] = torch.where(hl[:, :n], torch.clamp(zx, min=floor), zl[:, :n])
         if zu0 is not None:
-            zx = torch.tensor(np.asarray(zu0, dtype=np.float64)[nlp.free], **f64) * nlp.obj_scale
-            zu[:n] = torch.where(hu[:n], torch.clamp(zx, min=floor), zu[:n])
+            zx = torch.tensor(_as_batch(zu0, B, ev.n_v)[:, nlp.free], **f64) * nlp.obj_scale[:, None]
+            zu[:, :n] = torch.where(hu[:, :n], torch.clamp(zx, min=floor), zu[:, :n])
         # slack bound multipliers from the row multipliers: dL/ds = -lam - z_l + z_u = 0
-        lamI = lam[nlp.ineq_t]
-        zl[n:] = torch.where(hl[n:], torch.clamp(-lamI, min=floor), zl[n:])
-        zu[n:] = torch.where(hu[n:], torch.clamp(lamI, min=floor), zu[n:])
-    mu = opts.mu_init
+        lamI = lam[:, nlp.ineq_t]
+        zl[:, n:] = torch.where(hl[:, n:], torch.clamp(-lamI, min=floor), zl[:, n:])
+        zu[:, n:] = torch.where(hu[:, n:], torch.clamp(lamI, min=floor), zu[:, n:])
+
+    # ---- per-instance state (host) ---------------------------------------------------------
+    mu = np.full(B, opts.mu_init)
     mu_floor = max(opts.mu_target, opts.tol / 10)
-    tau = max(opts.tau_min, 1.0 - mu)
-    filt = []
-    c = nlp.constraints(g, y[n:])
-    theta0 = float(c.abs().sum().item())
-    theta_max = 1e4 * max(1.0, theta0)
-    theta_min = 1e-4 * max(1.0, theta0)
-    delta_w_last = 0.0
-    skkt = None
-    if opts.kkt == "structured" and getattr(ev, "layout", None) is not None:
-        try:
-            skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators,
-                                 deterministic=opts.deterministic)
-            skkt.force_btd = opts.separators == "btd"           # the block sweep on host tensors too
-        except ValueError:
-            skkt = None
-    K = torch.zeros(N, N, **f64) if skkt is None else None
+    tau = np.maximum(opts.tau_min, 1.0 - mu)
+    filt = [[] for _ in range(B)]
+    c = nlp.constraints(g, y[:, n:])
+    theta0 = c.abs().sum(1).cpu().numpy()
+    theta_max = 1e4 * np.maximum(1.0, theta0)
+    theta_min = 1e-4 * np.maximum(1.0, theta0)
+    delta_w_last = np.zeros(B)
+    status = np.array(["max_iter"] * B, dtype=object)
+    iters = np.zeros(B, dtype=np.int64)
+    kkt_err = np.full(B, math.inf)
+    active = np.ones(B, dtype=bool)
+    skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators)
+    skkt.force_btd = opts.separators == "btd"                   # the block sweep on host tensors too
     # exact inertia needs the separator pivot blocks of the block sweep on the device (a dense
     # Bunch-Kaufman pass over the whole Schur complement is ~1 s); otherwise the curvature test
-    exact_inertia = opts.inertia == "exact" and skkt is not None and (skkt.btd is not None or not dev.type == "cuda")
+    exact_inertia = opts.inertia == "exact" and (skkt.btd is not None or dev.type != "cuda")
     timing = {}
 
     class _Phase:
@@ -633,33 +634,32 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
 
         def __enter__(self):
             if opts.profile:
-                if torch.cuda.is_available() and str(dev).startswith("cuda"):
+                if dev.type == "cuda":
                     torch.cuda.synchronize()
                 self.t = time.perf_counter()
 
         def __exit__(self, *exc):
             if opts.profile:
-                if torch.cuda.is_available() and str(dev).startswith("cuda"):
+                if dev.type == "cuda":
                     torch.cuda.synchronize()
                 timing[self.key] = timing.get(self.key, 0.0) + time.perf_counter() - self.t
             return False
-    status = "max_iter"
-    it = 0
-    kkt_err = math.inf
 
     def gaps(yv):
         dl = torch.where(hl, yv - yl, torch.ones_like(yv))
         du = torch.where(hu, yu - yv, torch.ones_like(yv))
         return dl, du
 
-    def barrier_phi(fv, yv):
+    def barrier_phi(fv, yv, mu_t):
         dl, du = gaps(yv)
-        return fv - mu * (torch.log(dl[hl]).sum() + torch.log(du[hu]).sum())
+        lg = torch.where(hl, torch.log(dl), torch.zeros_like(dl)).sum(1) + \
+            torch.where(hu, torch.log(du), torch.zeros_like(du)).sum(1)
+        return fv - mu_t * lg
 
     def grad_y(gradv):
-        return torch.cat([gradv, torch.zeros(mI, **f64)])
+        return torch.cat([gradv, torch.zeros(B, mI, **f64)], 1)
 
-    Op = _GatherMv if opts.deterministic else _Csr
+    Op = _GatherMv
     jt_op = Op(nlp.j_col.cpu().numpy(), nlp.j_row.cpu().numpy(), (ny, m), dev)
     hr_np, hc_np = nlp.h_r.cpu().numpy(), nlp.h_c.cpu().numpy()
     off_np = hr_np != hc_np
@@ -667,325 +667,407 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
 
     def A_T_lam(jvv, lamv):
         r = jt_op.mv(jvv, lamv)
-        r[n:] -= lamv[nlp.ineq_t]
+        r[:, n:] -= lamv[:, nlp.ineq_t]
         return r
 
-    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_):
+    nb = int(hl[0].sum().item() + hu[0].sum().item())
+
+    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_t):
+        """IPOPT's scaled optimality error per instance (host [B] arrays): total, dual, primal,
+        complementarity at barrier parameter mu_t ([B] tensor)."""
         dl, du = gaps(yv)
         dual = grad_y(gradv) + A_T_lam(jvv, lamv) - zlv + zuv
-        compl_l = torch.where(hl, dl * zlv - mu_, torch.zeros_like(yv))
-        compl_u = torch.where(hu, du * zuv - mu_, torch.zeros_like(yv))
-        nb = int(hl.sum().item() + hu.sum().item())
-        s_d = max(opts.s_max, (lamv.abs().sum() + zlv.abs().sum() + zuv.abs().sum()).item() / max(1, m + nb)) / opts.s_max
-        s_c = max(opts.s_max, (zlv.abs().sum() + zuv.abs().sum()).item() / max(1, nb)) / opts.s_max
-        e_dual = dual.abs().max().item() / s_d
-        e_pr = cv.abs().max().item() if m else 0.0
-        e_c = max(compl_l.abs().max().item(), compl_u.abs().max().item()) / s_c
-        return max(e_dual, e_pr, e_c), e_dual, e_pr, e_c
+        compl_l = torch.where(hl, dl * zlv - mu_t[:, None], torch.zeros_like(yv))
+        compl_u = torch.where(hu, du * zuv - mu_t[:, None], torch.zeros_like(yv))
+        zsum = zlv.abs().sum(1) + zuv.abs().sum(1)
+        s_d = torch.clamp((lamv.abs().sum(1) + zsum) / max(1, m + nb), min=opts.s_max) / opts.s_max
+        s_c = torch.clamp(zsum / max(1, nb), min=opts.s_max) / opts.s_max
+        e_dual = dual.abs().amax(1) / s_d
+        e_pr = cv.abs().amax(1) if m else torch.zeros(B, **f64)
+        e_c = torch.maximum(compl_l.abs().amax(1), compl_u.abs().amax(1)) / s_c
+        e = torch.stack([torch.maximum(torch.maximum(e_dual, e_pr), e_c), e_dual, e_pr, e_c]).cpu().numpy()
+        return e[0], e[1], e[2], e[3]
 
-    def assemble(Kmat, hv, sigma, delta_w, delta_c):
-        Kmat.zero_()
-        if hv is not None:
-            Kmat[nlp.h_r, nlp.h_c] = hv
-            Kmat[nlp.h_c[nlp.h_offdiag], nlp.h_r[nlp.h_offdiag]] = hv[nlp.h_offdiag]
-        idx = torch.arange(ny, device=dev)
-        Kmat[idx, idx] += sigma + delta_w
-        _dense_A(nlp, jv, ny, Kmat)
-        if delta_c > 0:
-            idm = torch.arange(ny, N, device=dev)
-            Kmat[idm, idm] = -delta_c
+    def ftb(v, dv, mask_pos, tau_t):
+        """Fraction-to-the-boundary step per instance: min(1, min_i -tau v_i / dv_i) (host [B])."""
+        ratio = torch.where(mask_pos & (dv < 0), -tau_t[:, None] * v / dv, torch.full_like(v, math.inf))
+        return np.minimum(1.0, ratio.amin(1).cpu().numpy()) if ratio.shape[1] else np.ones(B)
 
-    def max_step(v, dv, mask_pos):
-        ratio = torch.where(mask_pos & (dv < 0), -tau * v / dv, torch.full_like(v, math.inf))
-        return min(1.0, float(ratio.min().item())) if ratio.numel() else 1.0
+    def filter_ok(b, theta_t, phi_t):
+        return all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt[b])
 
-    hv_zero = torch.zeros(len(nlp.h_keep), **f64)
+    hv_zero = torch.zeros(B, len(nlp.h_keep), **f64)
 
-    def restoration(y0, c0, theta0_, phi0_, max_steps=50):
-        """Minimum-norm Gauss-Newton corrections toward c(y) = 0, scaled by the barrier Sigma,
-        with backtracking on theta; returns (y, lam) once the point is acceptable to the filter."""
-        yv, cv, th = y0, c0, theta0_
-        lam_r = lam
-        for _ in range(max_steps):
-            _, _, g_c, jv_c = nlp.eval_all(yv[:n])
-            cv = nlp.constraints(g_c, yv[n:])
-            th = float(cv.abs().sum().item())
-            dlv, duv = gaps(yv)
-            sig = torch.where(hl, 1.0 / dlv ** 2, torch.zeros_like(yv)) + torch.where(hu, 1.0 / duv ** 2, torch.zeros_like(yv))
-            rhs = -torch.cat([torch.zeros(ny, **f64), cv])
-            try:
-                if skkt is not None:
-                    skkt.factor(hv_zero, sig + 1e-8, jv_c, 0.0, mI)
-                    sol = skkt.solve(rhs)
-                else:
-                    assemble_jv(K, jv_c, sig + 1e-8)
-                    sol = torch.linalg.solve(K, rhs)
-            except RuntimeError:
-                return None
-            dyv = sol[:ny]
-            a = min(max_step(dlv, dyv, hl), max_step(duv, -dyv, hu))
-            for _ in range(30):
-                yt = yv + a * dyv
-                ft, gt = nlp.eval_fg(yt[:n])
-                ct = nlp.constraints(gt, yt[n:])
-                tht = float(ct.abs().sum().item())
-                if math.isfinite(tht) and tht < (1 - 1e-4 * a) * th:
-                    break
-                a *= 0.5
+    def dev_b(a):
+        return torch.tensor(np.asarray(a, dtype=np.float64), **f64)
+
+    # ---- the newton direction with inertia correction (all instances in `want`) ------------------
+    def newton_direction(want, dw_floor, hv, sigma, rhs, mu_t):
+        """Per instance in `want`: (ok, sol, delta_w) of the primal-dual system with IPOPT's
+        inertia correction (exact inertia) or the curvature test.  The factorisation left in skkt
+        belongs to each accepted instance's final (delta_w, delta_c)."""
+        delta_w = np.where(want, dw_floor, 0.0)
+        delta_c = np.zeros(B)
+        done = ~want.copy()
+        ok = np.zeros(B, dtype=bool)
+        sol_out = torch.zeros(B, N, **f64)
+        dw_used = np.zeros(B)
+        for attempt in range(60):
+            with _Phase("kkt_factor"):
+                skkt.factor(hv, sigma + dev_b(delta_w)[:, None], jv, dev_b(delta_c), mI)
+            grow = ~done.copy()
+            if exact_inertia:
+                with _Phase("inertia"):
+                    inert = skkt.inertia().cpu().numpy()
+                pos, neg, zero = inert[:, 0], inert[:, 1], inert[:, 2]
+                # zero or missing negative eigenvalues: a (numerically) rank-deficient constraint
+                # Jacobian -> delta_c once; too few positive ones -> delta_w (Waechter & Biegler
+                # 2006, Alg. IC)
+                need_c = ~done & ((zero > 0) | (neg < m)) & (delta_c == 0.0)
+                delta_c = np.where(need_c, opts.delta_c * mu_t ** 0.25, delta_c)
+                good = ~done & ~need_c & (pos == ny) & (neg == m)
+                grow &= ~need_c
             else:
-                return None
-            yv = yt
-            lam_r = lam_r + a * sol[ny:]
-            pht = float(barrier_phi(ft, yt).item())
-            if tht <= 0.9 * theta0_ and all(not (tht >= th_f and pht >= ph_f) for th_f, ph_f in filt):
-                return yv, lam_r
-        return None
-
-    def assemble_jv(Kmat, jv_c, diag):
-        Kmat.zero_()
-        idx = torch.arange(ny, device=dev)
-        Kmat[idx, idx] = diag
-        _dense_A(nlp, jv_c, ny, Kmat)
-
-    while it < opts.max_iter:
-        c = nlp.constraints(g, y[n:])
-        kkt_err, e_d, e_p, e_c = errors(grad, jv, c, y, lam, zl, zu, opts.mu_target)
-        if kkt_err <= opts.tol:
-            status = "solve_succeeded"
-            break
-        # barrier update (monotone)
-        while True:
-            e_mu = errors(grad, jv, c, y, lam, zl, zu, mu)[0]
-            if e_mu > opts.kappa_eps * mu or mu <= mu_floor * 1.0000001:
-                break
-            mu = max(mu_floor, min(opts.kappa_mu * mu, mu ** opts.theta_mu))
-            tau = max(opts.tau_min, 1.0 - mu)
-            filt = []
-        # ---- Newton system --------------------------------------------------------------------
-        with _Phase("hessian"):
-            hv = nlp.hess(y[:n], lam)
-        dl, du = gaps(y)
-        sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
-        grad_phi = grad_y(grad) - torch.where(hl, mu / dl, torch.zeros_like(y)) + torch.where(hu, mu / du, torch.zeros_like(y))
-        theta = float(c.abs().sum().item())
-        phi = float(barrier_phi(f, y).item())
-
-        def newton_direction(dw_floor):
-            """(dy, dlam, delta_w) with the curvature-tested inertia correction."""
-            nonlocal delta_w_last
-            rhs = -torch.cat([grad_phi + A_T_lam(jv, lam), c])
-            delta_w = dw_floor
-            delta_c = 0.0
-            for attempt in range(60):
-                try:
-                    with _Phase("kkt_factor"):
-                        if skkt is not None:
-                            skkt.factor(hv, sigma + delta_w, jv, delta_c, mI)
-                        else:
-                            assemble(K, hv, sigma, delta_w, delta_c)
-                    if exact_inertia:
-                        # IPOPT's inertia correction (Waechter & Biegler 2006, Alg. IC): a singular
-                        # matrix gets delta_c once, a wrong inertia a larger delta_w
-                        with _Phase("inertia"):
-                            pos, neg, zero = skkt.inertia()
-                        # zero or missing negative eigenvalues: a (numerically) rank-deficient
-                        # constraint Jacobian -> delta_c; too few positive ones -> delta_w
-                        if (zero > 0 or neg < m) and delta_c == 0.0:
-                            delta_c = opts.delta_c * mu ** 0.25
-                            continue
-                        ok = pos == ny and neg == m
-                        if ok:
-                            with _Phase("kkt_solve"):
-                                sol = skkt.solve(rhs)
-                            if not bool(torch.isfinite(sol).all().item()):
-                                ok = False
-                        if ok:
-                            if delta_w > 0:
-                                delta_w_last = delta_w
-                            return sol[:ny], sol[ny:], delta_w
-                    else:
-                        with _Phase("kkt_solve"):
-                            sol = skkt.solve(rhs) if skkt is not None else torch.linalg.solve(K, rhs)
-                        ok = bool(torch.isfinite(sol).all().item())
-                        if ok:
-                            dy = sol[:ny]
-                            Wd = h_op.mv(torch.cat([hv, hv[nlp.h_offdiag]]), dy)
-                            curv = float((dy * (Wd + (sigma + delta_w) * dy)).sum().item())
-                            if curv >= opts.curvature_kappa * float((dy * dy).sum().item()):
-                                if delta_w > 0:
-                                    delta_w_last = delta_w
-                                return sol[:ny], sol[ny:], delta_w
-                        else:
-                            delta_c = opts.delta_c * mu ** 0.25
-                except RuntimeError:
-                    delta_c = opts.delta_c * mu ** 0.25
-                if delta_w == 0.0:
-                    delta_w = opts.delta_w0 if delta_w_last == 0.0 else max(opts.delta_w_min, delta_w_last / 3.0)
+                good = ~done
+            if good.any():
+                with _Phase("kkt_solve"):
+                    sol = skkt.solve(rhs)
+                fin = torch.isfinite(sol).all(1).cpu().numpy()
+                if not exact_inertia:
+                    dy = sol[:, :ny]
+                    Wd = h_op.mv(torch.cat([hv, hv[:, nlp.h_offdiag]], 1), dy)
+                    curv = (dy * (Wd + (sigma + dev_b(delta_w)[:, None]) * dy)).sum(1)
+                    cpass = (curv >= opts.curvature_kappa * (dy * dy).sum(1)).cpu().numpy()
+                    bad_fin = good & ~fin
+                    delta_c = np.where(bad_fin & (delta_c == 0.0), opts.delta_c * mu_t ** 0.25, delta_c)
+                    newly = good & fin & cpass
                 else:
-                    delta_w *= 8.0 if delta_w_last > 0 else 100.0
-                if delta_w > opts.delta_w_max:
-                    return None
-            return None
+                    newly = good & fin
+                    bad_fin = good & ~fin
+                    delta_c = np.where(bad_fin & (delta_c == 0.0), opts.delta_c * mu_t ** 0.25, delta_c)
+                if newly.any():
+                    idx = torch.tensor(np.where(newly)[0], device=dev)
+                    sol_out[idx] = sol[idx]
+                    ok |= newly
+                    dw_used = np.where(newly, delta_w, dw_used)
+                    delta_w_last[newly & (delta_w > 0)] = delta_w[newly & (delta_w > 0)]
+                    done |= newly
+                grow &= ~newly
+            # increase delta_w for the instances that still need it
+            first = grow & (delta_w == 0.0)
+            later = grow & (delta_w > 0.0)
+            delta_w = np.where(first, np.where(delta_w_last == 0.0, opts.delta_w0,
+                                               np.maximum(opts.delta_w_min, delta_w_last / 3.0)), delta_w)
+            delta_w = np.where(later, delta_w * np.where(delta_w_last > 0, 8.0, 100.0), delta_w)
+            done |= grow & (delta_w > opts.delta_w_max)
+            if done.all():
+                break
+        return ok, sol_out, dw_used, delta_w, delta_c
 
-        def acceptable(alpha, theta_t, phi_t, gphi_d):
-            """IPOPT's filter acceptance of a trial point (switching condition + Armijo, or
-            sufficient decrease of theta or phi, and acceptability to the filter)."""
+    def refactor_for(sel, hv, sigma, delta_w, delta_c):
+        """Leave skkt with the factorisation of the given per-instance (delta_w, delta_c)."""
+        skkt.factor(hv, sigma + dev_b(delta_w)[:, None], jv, dev_b(delta_c), mI)
+
+    # ---- the filter line search with second-order corrections (all instances in `want`) ---------
+    def line_search(want, dy, dlam, rhs_top, c_cur, dl, du, theta, phi, grad_phi, tau_t, mu_t):
+        """Per instance in `want`: (accepted, alpha, y_trial, dy_used, dlam_used, backtracks, socs)."""
+        alpha = np.minimum(ftb(dl, dy, hl, tau_t), ftb(du, -dy, hu, tau_t))
+        gphi_d = (grad_phi * dy).sum(1).cpu().numpy()
+        alpha_min = opts.alpha_min_frac * np.where(
+            gphi_d < 0, np.minimum(opts.gamma_theta, opts.gamma_phi * theta / np.maximum(-gphi_d, 1e-300)),
+            opts.gamma_theta)
+        live = want.copy()
+        acc = np.zeros(B, dtype=bool)
+        a_out = np.zeros(B)
+        y_out = y.clone()
+        dy_out, dlam_out = dy.clone(), dlam.clone()
+        nback = np.zeros(B, dtype=np.int64)
+        nsoc = np.zeros(B, dtype=np.int64)
+        first = want.copy()                    # the next trial is the first one (SOC eligible)
+        in_soc = np.zeros(B, dtype=bool)
+        soc_p = np.zeros(B, dtype=np.int64)
+        theta_old = np.zeros(B)
+        c_soc = torch.zeros(B, m, **f64)
+        dys = torch.zeros(B, ny, **f64)
+        dlam_s = torch.zeros(B, m, **f64)
+        a_s = np.zeros(B)
+
+        def accept_test(b, a, theta_t, phi_t):
             if not (math.isfinite(theta_t) and math.isfinite(phi_t)):
                 return False, False
-            switching = gphi_d < 0 and alpha * (-gphi_d) ** opts.s_phi > opts.delta_switch * theta ** opts.s_theta
-            if theta <= theta_min and switching:
-                ok = phi_t <= phi + opts.eta_phi * alpha * gphi_d
+            switching = gphi_d[b] < 0 and a * (-gphi_d[b]) ** opts.s_phi > opts.delta_switch * theta[b] ** opts.s_theta
+            if theta[b] <= theta_min[b] and switching:
+                ok_ = phi_t <= phi[b] + opts.eta_phi * a * gphi_d[b]
                 f_type = True
             else:
-                ok = theta_t <= theta_max and (theta_t <= (1 - opts.gamma_theta) * theta or
-                                               phi_t <= phi - opts.gamma_phi * theta)
+                ok_ = theta_t <= theta_max[b] and (theta_t <= (1 - opts.gamma_theta) * theta[b] or
+                                                   phi_t <= phi[b] - opts.gamma_phi * theta[b])
                 f_type = False
-            ok = ok and all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt)
-            return ok, f_type
+            return ok_ and filter_ok(b, theta_t, phi_t), f_type
 
-        def trial(yt):
+        for _round in range(opts.max_backtracks * (opts.max_soc + 1) + 1):
+            if not live.any():
+                break
+            a_t = dev_b(np.where(in_soc, a_s, alpha))[:, None]
+            yt = y + a_t * torch.where(dev_b(in_soc)[:, None] > 0, dys, dy)
             with _Phase("eval_fg"):
-                ft, gt = nlp.eval_fg(yt[:n])
-            ct = nlp.constraints(gt, yt[n:])
-            return ct, float(ct.abs().sum().item()), float(barrier_phi(ft, yt).item())
-
-        def line_search(dy, dlam, rhs_top):
-            """Filter line search from the fraction-to-the-boundary step, with IPOPT's second-order
-            corrections when the first trial is rejected with theta_trial >= theta.  Returns
-            (alpha, y_trial, dy, dlam) -- dy/dlam replaced by the corrected step when a
-            correction was accepted -- or None."""
-            nonlocal filt
-            alpha = min(max_step(dl, dy, hl), max_step(du, -dy, hu))
-            ls_info["alpha_max"] = alpha
-            if opts.verbose and alpha < 1.0:
-                rl = torch.where(hl & (dy < 0), -tau * dl / dy, torch.full_like(dy, math.inf))
-                ru = torch.where(hu & (dy > 0), tau * du / dy, torch.full_like(dy, math.inf))
-                r2 = torch.minimum(rl, ru)
-                ls_info["ftb_index"] = int(r2.argmin().item())
-            ls_info["backtracks"] = 0
-            ls_info["soc"] = 0
-            gphi_d = float((grad_phi * dy).sum().item())
-            alpha_min = opts.alpha_min_frac * min(opts.gamma_theta, opts.gamma_phi * theta / max(-gphi_d, 1e-300)
-                                                   if gphi_d < 0 else opts.gamma_theta)
-            for bt in range(opts.max_backtracks):
-                yt = y + alpha * dy
-                ct, theta_t, phi_t = trial(yt)
-                ok, f_type = acceptable(alpha, theta_t, phi_t, gphi_d)
-                if ok:
+                ft, gt = nlp.eval_fg(yt[:, :n])
+            ct = nlp.constraints(gt, yt[:, n:])
+            theta_t = ct.abs().sum(1)
+            phi_t = barrier_phi(ft, yt, dev_b(mu_t))
+            tp = torch.stack([theta_t, phi_t]).cpu().numpy()
+            start_soc = np.zeros(B, dtype=bool)
+            cont_soc = np.zeros(B, dtype=bool)
+            for b in np.where(live)[0]:
+                th_b, ph_b = float(tp[0, b]), float(tp[1, b])
+                ok_, f_type = accept_test(b, alpha[b], th_b, ph_b)
+                if ok_:
                     if not f_type:
-                        filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
-                    return alpha, yt, dy, dlam
-                if bt == 0 and opts.max_soc > 0 and skkt is not None and math.isfinite(theta_t) and theta_t >= theta:
-                    # second-order correction (Waechter & Biegler 2006, section 2.4): same matrix,
-                    # constraint part of the right-hand side c_soc = alpha c(y) + c(y_trial)
-                    c_soc = alpha * c + ct
-                    theta_old = theta_t
-                    for _p in range(opts.max_soc):
-                        with _Phase("kkt_solve"):
-                            sol = skkt.solve(torch.cat([rhs_top, -c_soc]))
-                        if not bool(torch.isfinite(sol).all().item()):
-                            break
-                        dys = sol[:ny]
-                        a_s = min(max_step(dl, dys, hl), max_step(du, -dys, hu))
-                        ys = y + a_s * dys
-                        cs_, theta_s, phi_s = trial(ys)
-                        ls_info["soc"] += 1
-                        ok, f_type = acceptable(alpha, theta_s, phi_s, gphi_d)
-                        if ok:
-                            if not f_type:
-                                filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
-                            return a_s, ys, dys, sol[ny:]
-                        if not math.isfinite(theta_s) or theta_s > opts.kappa_soc * theta_old:
-                            break
-                        theta_old = theta_s
-                        c_soc = a_s * c_soc + cs_
-                if opts.verbose and bt < 8:
-                    print(f"     ls bt={bt} alpha={alpha:.3e} theta {theta:.6e}->{theta_t:.6e} phi {phi:.10e}->{phi_t:.10e} "
-                          f"gphi_d={gphi_d:.3e} theta_min={theta_min:.2e} filt={len(filt)}", flush=True)
-                alpha *= 0.5
-                ls_info["backtracks"] += 1
-                if alpha < alpha_min:
-                    break
-            return None
+                        filt[b].append(((1 - opts.gamma_theta) * theta[b], phi[b] - opts.gamma_phi * theta[b]))
+                    acc[b], live[b] = True, False
+                    a_out[b] = a_s[b] if in_soc[b] else alpha[b]
+                    continue
+                if in_soc[b]:
+                    nsoc[b] += 1
+                    if math.isfinite(th_b) and th_b <= opts.kappa_soc * theta_old[b] and soc_p[b] + 1 < opts.max_soc:
+                        soc_p[b] += 1
+                        theta_old[b] = th_b
+                        cont_soc[b] = True
+                        continue
+                    in_soc[b] = False                       # corrections failed: back to backtracking
+                elif first[b] and opts.max_soc > 0 and math.isfinite(th_b) and th_b >= theta[b]:
+                    first[b] = False
+                    start_soc[b] = True
+                    theta_old[b] = th_b
+                    continue
+                first[b] = False
+                alpha[b] *= 0.5
+                nback[b] += 1
+                if alpha[b] < alpha_min[b] or nback[b] >= opts.max_backtracks:
+                    live[b] = False
+            if start_soc.any() or cont_soc.any():
+                # second-order correction (Waechter & Biegler 2006, section 2.4): same matrix,
+                # constraint part of the right-hand side c_soc = alpha c(y) + c(y_trial), then
+                # c_soc <- a_soc c_soc + c(y_soc)
+                st = dev_b(start_soc)[:, None] > 0
+                ctn = dev_b(cont_soc)[:, None] > 0
+                c_soc = torch.where(st, dev_b(alpha)[:, None] * c_cur + ct,
+                                    torch.where(ctn, dev_b(a_s)[:, None] * c_soc + ct, c_soc))
+                with _Phase("kkt_solve"):
+                    sol = skkt.solve(torch.cat([rhs_top, -c_soc], 1))
+                fin = torch.isfinite(sol).all(1).cpu().numpy()
+                upd = (start_soc | cont_soc) & fin
+                sel = dev_b(upd)[:, None] > 0
+                dys = torch.where(sel, sol[:, :ny], dys)
+                dlam_s = torch.where(sel, sol[:, ny:], dlam_s)
+                a_new = np.minimum(ftb(dl, dys, hl, tau_t), ftb(du, -dys, hu, tau_t))
+                a_s = np.where(upd, a_new, a_s)
+                in_soc |= upd
+                # a non-finite correction: plain backtracking
+                nf = (start_soc | cont_soc) & ~fin
+                in_soc &= ~nf
+                for b in np.where(nf)[0]:
+                    alpha[b] *= 0.5
+                    nback[b] += 1
+            # remember the accepted trial points
+            if acc.any():
+                sel = dev_b(acc & want)[:, None] > 0
+                y_out = torch.where(sel & (dev_b(in_soc)[:, None] > 0), y + dev_b(a_s)[:, None] * dys,
+                                    torch.where(sel, y + dev_b(alpha)[:, None] * dy, y_out))
+                dy_out = torch.where(sel & (dev_b(in_soc)[:, None] > 0), dys, dy_out)
+                dlam_out = torch.where(sel & (dev_b(in_soc)[:, None] > 0), dlam_s, dlam_out)
+                want = want & ~acc
+        return acc, a_out, y_out, dy_out, dlam_out, nback, nsoc
 
-        accepted = None
-        delta_w = 0.0
-        ls_info = {}
+    # ---- feasibility restoration (all instances in `want`) ---------------------------------------
+    def restoration(want, c0, theta0_, mu_t, max_steps=50):
+        """Minimum-norm Gauss-Newton corrections toward c(y) = 0, scaled by the barrier Sigma, with
+        backtracking on theta, until the filter accepts the point (IPOPT's restoration phase,
+        reduced to its core).  Returns (success [B], y, lam)."""
+        yv = y.clone()
+        lam_r = lam.clone()
+        live = want.copy()
+        succ = np.zeros(B, dtype=bool)
+        for _ in range(max_steps):
+            if not live.any():
+                break
+            _, _, g_c, jv_c = nlp.eval_all(yv[:, :n])
+            cv = nlp.constraints(g_c, yv[:, n:])
+            th = cv.abs().sum(1).cpu().numpy()
+            dlv, duv = gaps(yv)
+            sig = torch.where(hl, 1.0 / dlv ** 2, torch.zeros_like(yv)) + torch.where(hu, 1.0 / duv ** 2, torch.zeros_like(yv))
+            skkt.factor(hv_zero, sig + 1e-8, jv_c, 0.0, mI)
+            sol = skkt.solve(-torch.cat([torch.zeros(B, ny, **f64), cv], 1))
+            fin = torch.isfinite(sol).all(1).cpu().numpy()
+            live &= fin
+            dyv = torch.where(torch.isfinite(sol[:, :ny]), sol[:, :ny], torch.zeros_like(sol[:, :ny]))
+            a = np.minimum(ftb(dlv, dyv, hl, dev_b(tau)), ftb(duv, -dyv, hu, dev_b(tau)))
+            searching = live.copy()
+            a_acc = np.zeros(B)
+            for _bt in range(30):
+                if not searching.any():
+                    break
+                yt = yv + dev_b(a)[:, None] * dyv
+                ft, gt = nlp.eval_fg(yt[:, :n])
+                ct = nlp.constraints(gt, yt[:, n:])
+                tht = ct.abs().sum(1).cpu().numpy()
+                okb = searching & np.isfinite(tht) & (tht < (1 - 1e-4 * a) * th)
+                a_acc = np.where(okb, a, a_acc)
+                searching &= ~okb
+                a = np.where(searching, 0.5 * a, a)
+            live &= ~searching                                  # no decrease found: failed
+            if not live.any():
+                break
+            sel = dev_b(live)[:, None] > 0
+            yv = torch.where(sel, yv + dev_b(a_acc)[:, None] * dyv, yv)
+            lam_r = torch.where(sel, lam_r + dev_b(a_acc)[:, None] * sol[:, ny:], lam_r)
+            ft, gt = nlp.eval_fg(yv[:, :n])
+            ct = nlp.constraints(gt, yv[:, n:])
+            tp = torch.stack([ct.abs().sum(1), barrier_phi(ft, yv, dev_b(mu_t))]).cpu().numpy()
+            for b in np.where(live)[0]:
+                if tp[0, b] <= 0.9 * theta0_[b] and filter_ok(b, tp[0, b], tp[1, b]):
+                    succ[b], live[b] = True, False
+        return succ, yv, lam_r
+
+    # ---- main loop -------------------------------------------------------------------------------
+    it = 0
+    while it < opts.max_iter:
+        c = nlp.constraints(g, y[:, n:])
+        kkt_err, e_d, e_p, e_c = errors(grad, jv, c, y, lam, zl, zu, torch.full((B,), opts.mu_target, **f64))
+        conv = active & (kkt_err <= opts.tol)
+        status[conv] = "solve_succeeded"
+        active &= ~conv
+        if not active.any():
+            break
+        # barrier update (monotone), per instance
+        for _ in range(50):
+            e_mu = errors(grad, jv, c, y, lam, zl, zu, dev_b(mu))[0]
+            upd = active & (e_mu <= opts.kappa_eps * mu) & (mu > mu_floor * 1.0000001)
+            if not upd.any():
+                break
+            mu = np.where(upd, np.maximum(mu_floor, np.minimum(opts.kappa_mu * mu, mu ** opts.theta_mu)), mu)
+            tau = np.maximum(opts.tau_min, 1.0 - mu)
+            for b in np.where(upd)[0]:
+                filt[b] = []
+        # ---- Newton system ----------------------------------------------------------------------
+        with _Phase("hessian"):
+            hv = nlp.hess(y[:, :n], lam)
+        dl, du = gaps(y)
+        mu_d = dev_b(mu)
+        sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
+        grad_phi = grad_y(grad) - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
+            torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y))
+        theta = c.abs().sum(1).cpu().numpy()
+        phi = barrier_phi(f, y, mu_d).cpu().numpy()
+        rhs_top = -(grad_phi + A_T_lam(jv, lam))
+        rhs = torch.cat([rhs_top, -c], 1)
+        pending = active.copy()
+        acc_all = np.zeros(B, dtype=bool)
+        alpha_acc = np.zeros(B)
+        y_new, dy_new, dlam_new = y.clone(), torch.zeros(B, ny, **f64), torch.zeros(B, m, **f64)
+        dw_rec = np.zeros(B)
+        nback = np.zeros(B, dtype=np.int64)
+        nsoc = np.zeros(B, dtype=np.int64)
+        tau_d = dev_b(tau)
         for dw_floor in (0.0, 1e-2, 1.0, 1e2):
-            nd = newton_direction(dw_floor)
-            if nd is None:
-                continue
-            dy, dlam, delta_w = nd
-            accepted = line_search(dy, dlam, -(grad_phi + A_T_lam(jv, lam)))
-            if accepted is not None:
+            if not pending.any():
                 break
-        if accepted is None:
-            # feasibility restoration: Gauss-Newton steps on ||c|| inside the bounds until the
-            # filter accepts the point (IPOPT's restoration phase, reduced to its core)
-            rest = restoration(y, c, theta, phi)
-            if rest is None:
-                status = "restoration_failed"
-                break
-            y, lam = rest
-            filt.append(((1 - opts.gamma_theta) * theta, phi - opts.gamma_phi * theta))
-            dl, du = gaps(y)
-            f, grad, g, jv = nlp.eval_all(y[:n])
-            if skkt is not None and exact_inertia:
-                # IPOPT after restoration: bound multipliers kept within the kappa_sigma band of the
-                # new point, constraint multipliers by least squares on the dual infeasibility,
-                # [I A^T; A 0] (w, lam) = (-(grad f - z_L + z_U), 0)
-                zl = torch.where(hl, torch.clamp(zl, min=mu / (opts.kappa_sigma * dl), max=opts.kappa_sigma * mu / dl), zl)
-                zu = torch.where(hu, torch.clamp(zu, min=mu / (opts.kappa_sigma * du), max=opts.kappa_sigma * mu / du), zu)
-                try:
-                    skkt.factor(hv_zero, torch.ones(ny, **f64), jv, 0.0, mI)
-                    sol = skkt.solve(torch.cat([-(grad_y(grad) - zl + zu), torch.zeros(m, **f64)]))
-                    if bool(torch.isfinite(sol).all().item()):
-                        lam = sol[ny:]
-                except RuntimeError:
-                    pass
-            else:
-                zl = torch.where(hl, torch.clamp(mu / dl, max=1e3), zl)
-                zu = torch.where(hu, torch.clamp(mu / du, max=1e3), zu)
-            it += 1
-            log.append(dict(it=it, f=float(f.item()) / nlp.obj_scale, inf_pr=e_p, inf_du=e_d, mu=mu,
-                            alpha=0.0, alpha_z=0.0, delta_w=-1.0))
-            if opts.verbose:
-                print(f"{it:4d} restoration theta {theta:.3e} -> {float(nlp.constraints(g, y[n:]).abs().sum().item()):.3e}",
-                      flush=True)
-            continue
-        alpha, yt, dy, dlam = accepted
-        dzl = torch.where(hl, mu / dl - zl - zl / dl * dy, torch.zeros_like(y))
-        dzu = torch.where(hu, mu / du - zu + zu / du * dy, torch.zeros_like(y))
-        alpha_z = min(max_step(zl, dzl, hl), max_step(zu, dzu, hu))
-        y = yt
-        lam = lam + alpha * dlam
-        zl = zl + alpha_z * dzl
-        zu = zu + alpha_z * dzu
+            ok, sol, dw_used, dw_fin, dc_fin = newton_direction(pending, dw_floor, hv, sigma, rhs, mu)
+            want = pending & ok
+            if want.any():
+                # the factorisation in skkt is the last attempt's: the accepted (delta_w, delta_c)
+                # of every instance that found a direction (others were still growing)
+                acc, a_o, y_o, dy_o, dl_o, nb_, ns_ = line_search(
+                    want, sol[:, :ny], sol[:, ny:], rhs_top, c, dl, du, theta, phi, grad_phi, tau_d, mu)
+                sel = dev_b(acc)[:, None] > 0
+                y_new = torch.where(sel, y_o, y_new)
+                dy_new = torch.where(sel, dy_o, dy_new)
+                dlam_new = torch.where(sel, dl_o, dlam_new)
+                alpha_acc = np.where(acc, a_o, alpha_acc)
+                dw_rec = np.where(acc, dw_used, dw_rec)
+                nback += nb_
+                nsoc += ns_
+                acc_all |= acc
+                pending &= ~acc
+        # ---- restoration for the instances without an acceptable step ---------------------------
+        rest_ok = np.zeros(B, dtype=bool)
+        if pending.any():
+            succ, y_r, lam_r = restoration(pending, c, theta, mu)
+            failed = pending & ~succ
+            status[failed] = "restoration_failed"
+            active &= ~failed
+            rest_ok = succ
+            if succ.any():
+                for b in np.where(succ)[0]:
+                    filt[b].append(((1 - opts.gamma_theta) * theta[b], phi[b] - opts.gamma_phi * theta[b]))
+                sel = dev_b(succ)[:, None] > 0
+                y = torch.where(sel, y_r, y)
+                lam = torch.where(sel, lam_r, lam)
+        # ---- accepted steps: primal, multipliers, bound multipliers ------------------------------
+        if acc_all.any():
+            sel = dev_b(acc_all)[:, None] > 0
+            dzl = torch.where(hl, mu_d[:, None] / dl - zl - zl / dl * dy_new, torch.zeros_like(y))
+            dzu = torch.where(hu, mu_d[:, None] / du - zu + zu / du * dy_new, torch.zeros_like(y))
+            alpha_z = np.minimum(ftb(zl, dzl, hl, tau_d), ftb(zu, dzu, hu, tau_d))
+            az = dev_b(np.where(acc_all, alpha_z, 0.0))[:, None]
+            y = torch.where(sel, y_new, y)
+            lam = lam + dev_b(np.where(acc_all, alpha_acc, 0.0))[:, None] * dlam_new
+            zl = zl + az * dzl
+            zu = zu + az * dzu
+        else:
+            alpha_z = np.zeros(B)
         # kappa_sigma safeguard
         dl, du = gaps(y)
-        zl = torch.where(hl, torch.clamp(zl, min=mu / (opts.kappa_sigma * dl), max=opts.kappa_sigma * mu / dl), zl)
-        zu = torch.where(hu, torch.clamp(zu, min=mu / (opts.kappa_sigma * du), max=opts.kappa_sigma * mu / du), zu)
+        zl = torch.where(hl, torch.clamp(zl, min=mu_d[:, None] / (opts.kappa_sigma * dl),
+                                         max=opts.kappa_sigma * mu_d[:, None] / dl), zl)
+        zu = torch.where(hu, torch.clamp(zu, min=mu_d[:, None] / (opts.kappa_sigma * du),
+                                         max=opts.kappa_sigma * mu_d[:, None] / du), zu)
         with _Phase("eval_all"):
-            f, grad, g, jv = nlp.eval_all(y[:n])
+            f, grad, g, jv = nlp.eval_all(y[:, :n])
+        if rest_ok.any():
+            # IPOPT after restoration: constraint multipliers by least squares on the dual
+            # infeasibility, [I A^T; A 0] (w, lam) = (-(grad f - z_L + z_U), 0)
+            skkt.factor(hv_zero, torch.ones(B, ny, **f64), jv, 0.0, mI)
+            sol = skkt.solve(torch.cat([-(grad_y(grad) - zl + zu), torch.zeros(B, m, **f64)], 1))
+            fin = torch.isfinite(sol).all(1)
+            sel = (dev_b(rest_ok)[:, None] > 0) & fin[:, None]
+            lam = torch.where(sel, sol[:, ny:], lam)
         it += 1
-        rec = dict(it=it, f=float(f.item()) / nlp.obj_scale, inf_pr=e_p, inf_du=e_d, mu=mu, alpha=alpha,
-                   alpha_z=alpha_z, delta_w=delta_w, **ls_info)
-        log.append(rec)
+        stepped = acc_all | rest_ok
+        iters += stepped
+        f_host = (f / nlp.obj_scale).cpu().numpy()
+        for b in np.where(stepped)[0]:
+            rec = dict(it=int(iters[b]), f=float(f_host[b]), inf_pr=float(e_p[b]), inf_du=float(e_d[b]), mu=float(mu[b]),
+                       alpha=float(alpha_acc[b]) if acc_all[b] else 0.0,
+                       alpha_z=float(alpha_z[b]) if acc_all[b] else 0.0,
+                       delta_w=float(dw_rec[b]) if acc_all[b] else -1.0,
+                       backtracks=int(nback[b]), soc=int(nsoc[b]))
+            logs[b].append(rec)
         if opts.verbose:
-            print(f"{it:4d} f={rec['f']: .8e} pr={e_p:.2e} du={e_d:.2e} mu={mu:.1e} a={alpha:.2e} dw={delta_w:.1e}",
-                  flush=True)
-    if status == "max_iter" and kkt_err <= opts.acceptable_tol:
-        status = "solved_to_acceptable_level"
-    xf = nlp.x_fix.copy()
-    xf[nlp.free] = y[:n].cpu().numpy()
-    lam_out = (lam * nlp.c_scale / nlp.obj_scale).cpu().numpy()
-    c = nlp.constraints(g, y[n:])
-    zl_v = np.zeros(len(xf))
-    zu_v = np.zeros(len(xf))
-    zl_v[nlp.free] = (zl[:n] / nlp.obj_scale).cpu().numpy()
-    zu_v[nlp.free] = (zu[:n] / nlp.obj_scale).cpu().numpy()
-    return IpmResult(x=xf, lam_g=lam_out, f=float(f.item()) / nlp.obj_scale, status=status, iterations=it,
-                     kkt_error=kkt_err, constr_viol=float((c / nlp.c_scale).abs().max().item()) if m else 0.0,
-                     seconds=time.perf_counter() - t_start, zl=zl_v, zu=zu_v, log=log,
-                     kkt_solves=skkt.n_solve if skkt is not None else 0,
-                     kkt_dense=skkt.n_dense if skkt is not None else 0, timing=timing)
+            b0 = int(np.where(active)[0][0]) if active.any() else 0
+            print(f"{it:4d} active={int(active.sum())} [b{b0}] f={f_host[b0]: .8e} pr={e_p[b0]:.2e} "
+                  f"du={e_d[b0]:.2e} mu={mu[b0]:.1e} a={alpha_acc[b0]:.2e} dw={dw_rec[b0]:.1e}", flush=True)
+    for b in range(B):
+        if status[b] == "max_iter" and kkt_err[b] <= opts.acceptable_tol:
+            status[b] = "solved_to_acceptable_level"
+    c = nlp.constraints(g, y[:, n:])
+    yh = y[:, :n].cpu().numpy()
+    lam_out = (lam * nlp.c_scale / nlp.obj_scale[:, None]).cpu().numpy()
+    viol = (c / nlp.c_scale).abs().amax(1).cpu().numpy() if m else np.zeros(B)
+    zl_h = (zl[:, :n] / nlp.obj_scale[:, None]).cpu().numpy()
+    zu_h = (zu[:, :n] / nlp.obj_scale[:, None]).cpu().numpy()
+    f_out = (f / nlp.obj_scale).cpu().numpy()
+    seconds = time.perf_counter() - t_start
+    out = []
+    for b in range(B):
+        xf = nlp.x_fix.copy()
+        xf[nlp.free] = yh[b]
+        zl_v = np.zeros(len(xf))
+        zu_v = np.zeros(len(xf))
+        zl_v[nlp.free] = zl_h[b]
+        zu_v[nlp.free] = zu_h[b]
+        out.append(IpmResult(x=xf, lam_g=lam_out[b], f=float(f_out[b]), status=str(status[b]),
+                             iterations=int(iters[b]), kkt_error=float(kkt_err[b]), constr_viol=float(viol[b]),
+                             seconds=seconds, zl=zl_v, zu=zu_v, log=logs[b], kkt_solves=skkt.n_solve,
+                             kkt_dense=skkt.n_dense, timing=timing))
+    return out

@@ -62,6 +62,10 @@ class _Ap2:
     def optimize(self, ev, opts, device, v0, u):
         return optimize(self.consts, ev, opts, device=device, v_init=v0, u_ref=u)
 
+    def optimize_batch(self, ev, opts, device, v0, us):
+        from .trajectory import optimize_batch
+        return optimize_batch(self.consts, ev, us, opts, device=device, v_init=v0)
+
 
 class _Dual:
     """The dual-kite problem of config 4 (dual.py, dual_homotopy.py)."""
@@ -93,11 +97,15 @@ class _Dual:
 
 
 def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda", opts: IpmOptions | None = None,
-              verbose=False, point_solver=None, arch="single"):
+              verbose=False, point_solver=None, arch="single", mode="chain"):
     """Returns (on rank 0) dict with per-point outputs, V_opt [P, n_v] and timing; None elsewhere.
 
-    ``point_solver(u, prev) -> (V, outputs, iterations, ok, prev)`` replaces the per-point solve
-    (the default is the homotopy for a shard's first point and the warm-started final step after)."""
+    mode "chain": the reference's sweeping warm start within a shard -- the homotopy for the
+    shard's first point, then the warm-started final step for each next point;
+    ``point_solver(u, prev) -> (V, outputs, iterations, ok, prev)`` replaces the per-point solve.
+    mode "batch": the shard's points are independent trials solved side by side, the full homotopy
+    from the standard initial guess for every point as one batched interior-point solve per step
+    (``make_evaluator(consts, batch)``)."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     coll_dev = torch.device(device)
@@ -130,7 +138,7 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     my_u = [u for u in seeds.cpu().numpy() if np.isfinite(u)]
 
     # ---- local solves ---------------------------------------------------------------------------
-    if point_solver is None:
+    if point_solver is None and mode == "chain":
         ev = make_evaluator(consts)
         final = prob.final_step(v0)
         lbg, ubg = lay.g_bounds()
@@ -149,6 +157,22 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     res_o = torch.full((per, N_OUT), float("nan"), dtype=torch.float64, device=coll_dev)
     prev = None
     t_rank = time.perf_counter()
+    if mode == "batch" and my_u:
+        done = ("solve_succeeded", "solved_to_acceptable_level")
+        t0 = time.perf_counter()
+        evb = make_evaluator(consts, len(my_u))
+        Vb, summary, outs, _ = prob.optimize_batch(evb, opts, device, v0, my_u)
+        el = time.perf_counter() - t0
+        for i, u in enumerate(my_u):
+            iters = sum(r["iterations"][i] for r in summary)
+            ok = all(r["status"][i] in done for r in summary)
+            res_v[i] = torch.tensor(Vb[i], device=coll_dev)
+            res_o[i] = torch.tensor([u, outs[i]["avg_power_W"], outs[i]["period_s"], iters, float(ok), el],
+                                    device=coll_dev)
+            if verbose:
+                print(f"[rank {rank}] u_ref={u:.3f} P={outs[i]['avg_power_W']:.1f} W T={outs[i]['period_s']:.2f} s "
+                      f"iters={iters} ok={ok}", flush=True)
+        my_u = []
     for i, u in enumerate(my_u):
         t0 = time.perf_counter()
         try:
@@ -200,10 +224,11 @@ def main():
     ap.add_argument("--max-iter", type=int, default=600)
     ap.add_argument("--out", default="gpurun_out/sweep.json")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--separators", choices=["dense", "btd"], default="dense",
+    ap.add_argument("--separators", choices=["dense", "btd"], default="btd",
                     help="separator solve of the structured KKT (awebox_amd/btd.py for btd)")
-    ap.add_argument("--atomic-assembly", action="store_true",
-                    help="KKT assembly by atomic scatter-adds instead of the deterministic gather-sum")
+    ap.add_argument("--mode", choices=["chain", "batch"], default="batch",
+                    help="chain: warm-start chain per shard (the reference's sweep); batch: the shard's points "
+                         "as one batched homotopy")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -223,14 +248,14 @@ def main():
         from .dual_homotopy import make_evaluator
         mk = lambda c: make_evaluator(c, device=f"cuda:{local_rank}")  # noqa: E731
     else:
-        mk = lambda c: Ap2Evaluator(c, batch=1)  # noqa: E731
+        mk = lambda c, b=1: Ap2Evaluator(c, batch=b)  # noqa: E731
     res = run_sweep(u, n_k=args.n_k, d=args.d, make_evaluator=mk, dist=dist, device=f"cuda:{local_rank}",
                     opts=IpmOptions(max_iter=args.max_iter, separators=args.separators,
-                                    deterministic=not args.atomic_assembly), verbose=args.verbose, arch=args.arch)
+                                    ), verbose=args.verbose, arch=args.arch, mode=args.mode)
     if res is not None:
         res = dict(res)
         res.pop("V_opt")
-        res.update(n_k=args.n_k, d=args.d, arch=args.arch, gpus=world,
+        res.update(n_k=args.n_k, d=args.d, arch=args.arch, gpus=world, mode=args.mode,
                    metric=f"sweep trials/sec, {'dual-kite' if args.arch == 'dual' else 'AP2'} power curve")
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as fh:

@@ -13,7 +13,7 @@ import numpy as np
 from . import homotopy as hm
 from . import problem as pb
 from .initial_guess import initial_guess
-from .ipm import IpmOptions, solve
+from .ipm import IpmOptions, solve, solve_batch
 
 
 def hippo_options(label: str, base: IpmOptions | None = None) -> IpmOptions:
@@ -61,3 +61,35 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
         if final_step is not None and st.label == final_step:
             break
     return x, summary, hm.outputs(consts, lay, x), res
+
+
+def optimize_batch(consts: pb.Ap2Constants, ev, u_refs, opts: IpmOptions | None = None, device="cuda",
+                   v_init: np.ndarray | None = None, verbose=False):
+    """The homotopy for B = len(u_refs) wind speeds at once (ev.batch == B): every step is one
+    batched interior-point solve (ipm.solve_batch) in which each instance keeps its own IPOPT
+    iteration; all instances share the layout, bounds and schedule, and differ in P's u_ref.
+    Returns (V [B, n_v], per-step summaries (lists over instances), outputs per instance, results)."""
+    lay = pb.NlpLayout(consts.cfg.n_k, consts.cfg.d)
+    v0 = initial_guess(consts, lay) if v_init is None else v_init
+    B = len(u_refs)
+    steps = hm.schedule(consts, lay, v0)
+    lbg, ubg = lay.g_bounds()
+    x = np.tile(v0, (B, 1))
+    lam = zl = zu = None
+    summary = []
+    res = None
+    for st in steps:
+        P = np.stack([pb.pack_p(lay, consts, v0, step=st.cost_step, u_ref=u) for u in u_refs])
+        t0 = time.perf_counter()
+        res = solve_batch(ev, P, x, st.lbx, st.ubx, lbg, ubg, lam0=lam, zl0=zl, zu0=zu,
+                          opts=hippo_options(st.label, opts), device=device)
+        rec = dict(step=st.label, status=[r.status for r in res], iterations=[r.iterations for r in res],
+                   f=[r.f for r in res], seconds=time.perf_counter() - t0)
+        summary.append(rec)
+        if verbose:
+            print(rec, flush=True)
+        x = np.stack([r.x for r in res])
+        lam = np.stack([r.lam_g for r in res])
+        zl = np.stack([r.zl for r in res])
+        zu = np.stack([r.zu for r in res])
+    return x, summary, [hm.outputs(consts, lay, x[b]) for b in range(B)], res

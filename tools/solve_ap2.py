@@ -21,8 +21,6 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="the CPU port behind the device interface (test harness)")
     ap.add_argument("--iter-log", action="store_true", help="keep every step's per-iteration log in the output")
     ap.add_argument("--opts", default="{}", help="IpmOptions overrides as JSON")
-    ap.add_argument("--atomic-assembly", action="store_true",
-                    help="KKT assembly by atomic scatter-adds instead of the deterministic gather-sum")
     args = ap.parse_args()
     import torch
     from awebox_amd import problem as pb
@@ -39,8 +37,7 @@ def main():
         ev, device = Ap2Evaluator(consts, batch=1), "cuda"
     t0 = time.perf_counter()
     import dataclasses
-    base = dataclasses.replace(IpmOptions(max_iter=args.max_iter, verbose=args.verbose,
-                                          deterministic=not args.atomic_assembly), **json.loads(args.opts))
+    base = dataclasses.replace(IpmOptions(max_iter=args.max_iter, verbose=args.verbose), **json.loads(args.opts))
     V, summary, out, _ = optimize(consts, ev, base,
                                verbose=True, device=device, keep_logs=args.iter_log)
     rec = {"n_k": args.n_k, "d": args.d, "u_ref": args.u_ref, "seconds": time.perf_counter() - t0,
