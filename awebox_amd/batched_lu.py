@@ -9,7 +9,7 @@ import os
 _LIB = None
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libawelu.so")
 MAX_N = 1024
-BTD_MAX_M = 56                  # block size limit of the block-tridiagonal kernels (LDS)
+BTD_MAX_M = 48                  # block size limit of the block-tridiagonal kernels (LDS)
 
 
 def load_library(path: str = _PATH):
@@ -75,7 +75,7 @@ def lu_solve(LU, piv, B):
 
 def btd_factor(T):
     """Factor block-tridiagonal systems T [batch, nb, 3, m, m] (sub-, main, super-diagonal block of
-    every block row; float64 CUDA, m <= 56).  Returns (F, Dinv): F = T with W_k in the super-diagonal
+    every block row; float64 CUDA, m <= 48).  Returns (F, Dinv): F = T with W_k in the super-diagonal
     slots, Dinv [batch, nb, m, m] the inverted pivot blocks; T is not modified."""
     import torch
     if T.dtype != torch.float64 or not T.is_cuda or T.dim() != 5 or T.shape[2] != 3 or T.shape[3] != T.shape[4]:

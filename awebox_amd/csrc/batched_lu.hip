@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
 
 constexpr size_t kSolveLds = 144 * 1024;
 
-// Block-tridiagonal systems, one workgroup per system: nb diagonal blocks of m x m (m <= 56),
+// Block-tridiagonal systems, one workgroup per system: nb diagonal blocks of m x m (m <= 48),
 // T[b][k][3][m][m] = (sub-diagonal block L_k = (k, k-1), diagonal block D_k, super-diagonal block
 // U_k = (k, k+1)).  This is the separator system of the structured KKT in stage order (shooting
 // states and continuity multipliers alternate), and the sweep below is its Riccati recursion;
@@ -224,10 +224,11 @@ constexpr size_t kSolveLds = 144 * 1024;
 //
 // btd_factor_kernel:  D'_k = D_k - L_k W_{k-1},  [W_k | D'_k^-1] = D'_k^-1 [U_k | I]
 //   by Gauss-Jordan on the augmented block [D'_k | U_k | I] in LDS (per column: a pivot search by
-//   wave shuffles, one row interchange, the elimination of every other row; the 256 threads are a
+//   wave shuffles in every wave, the row interchange folded into the elimination of every other row,
+//   read from one LDS buffer and written to the other: one barrier per column; the 256 threads are a
 //   4 x 64 grid of (row group, column), so no integer division in the inner loops).  W_k
 //   overwrites U_k; D'_k^-1 goes to Dinv[b][k][m][m]; W_{k-1} stays in LDS for the next stage
-//   (the augmented block, L_k and W_{k-1} take 127 KB at m = 56).
+//   (two augmented blocks and W_{k-1} take 130 KB at m = 48).
 //   D'_k itself replaces D_k in T.
 // btd_apply_kernel:   Y_k = D'_k^-1 (X_k - L_k Y_{k-1}),  then x_k = Y_k - W_k x_{k+1}: matrix
 //   products streamed stage by stage, right-hand sides [j0, j0 + w) of X[b][nb m][ldx].  The
@@ -235,16 +236,18 @@ constexpr size_t kSolveLds = 144 * 1024;
 //   cond ~1e11), so every block solve takes one refinement step with D'_k: Y += D'^-1 (Z - D' Y).
 // The factorisation is reused by every solve of an interior-point iteration (iterative
 // refinement), and the apply is one launch per solve instead of a library LU's dozens.
-constexpr int kBtdMaxM = 56;
+constexpr int kBtdMaxM = 48;
 constexpr int kBtdMaxRhs = 64;
 constexpr int kRG = kThreads / 64;                            // row groups of the 4 x 64 grid
 
 __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, double* __restrict__ Ts,
                                                              double* __restrict__ Dinvs) {
-    __shared__ double R[kBtdMaxM][3 * kBtdMaxM + 1];          // [D | U | I] -> [. | W | D^-1]
-    __shared__ double Lk[kBtdMaxM][kBtdMaxM + 1];
+    // two buffers of the augmented block [D | U | I]: every Gauss-Jordan column reads one and writes
+    // the other (row interchange folded into the update), so a column costs one barrier; the
+    // second buffer holds L_k while D' = D - L_k W_{k-1} is formed
+    __shared__ double R0[kBtdMaxM][3 * kBtdMaxM + 1];
+    __shared__ double R1[kBtdMaxM][3 * kBtdMaxM + 1];
     __shared__ double Wp[kBtdMaxM][kBtdMaxM + 1];             // W_{k-1}
-    __shared__ int piv_s;
     const int tid = threadIdx.x, tj = tid & 63, ti = tid >> 6;
     const size_t mm = (size_t)m * m;
     double* T = Ts + (size_t)blockIdx.x * nb * 3 * mm;
@@ -258,68 +261,160 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
         const bool last = k == nb - 1;
         for (int i = ti; i < m; i += kRG) {
             for (int j = tj; j < m; j += 64) {
-                R[i][j] = Dg[i * m + j];
-                R[i][m + j] = last ? 0.0 : Ug[i * m + j];
-                R[i][2 * m + j] = i == j ? 1.0 : 0.0;
-                if (k > 0) Lk[i][j] = Lg[i * m + j];
+                R0[i][j] = Dg[i * m + j];
+                R0[i][m + j] = last ? 0.0 : Ug[i * m + j];
+                R0[i][2 * m + j] = i == j ? 1.0 : 0.0;
+                if (k > 0) R1[i][j] = Lg[i * m + j];
             }
         }
         __syncthreads();
         if (k > 0) {                                          // D -= L_k W_{k-1}
-            for (int i = ti; i < m; i += kRG) {
-                for (int j = tj; j < m; j += 64) {
-                    double acc = R[i][j];
-                    for (int c = 0; c < m; ++c) acc -= Lk[i][c] * Wp[c][j];
-                    R[i][j] = acc;
+            // thread (ti, tj): column j = tj (< m <= 48 < 64), rows ti, ti + 4, ...: 12 independent
+            // accumulators per thread, so the LDS loads of one c step pipeline
+            constexpr int kRows = kBtdMaxM / kRG;
+            const int j = tj;
+            if (j < m) {
+                double acc[kRows];
+#pragma unroll
+                for (int r = 0; r < kRows; ++r) acc[r] = 0.0;
+                for (int c = 0; c < m; ++c) {
+                    const double wc = Wp[c][j];
+#pragma unroll
+                    for (int r = 0; r < kRows; ++r) {
+                        const int i = ti + r * kRG;
+                        if (i < m) acc[r] += R1[i][c] * wc;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < kRows; ++r) {
+                    const int i = ti + r * kRG;
+                    if (i < m) R0[i][j] -= acc[r];
                 }
             }
             __syncthreads();
         }
         for (int i = ti; i < m; i += kRG)                     // keep D'_k for the solves' refinement
-            for (int j = tj; j < m; j += 64) Dg[i * m + j] = R[i][j];
-        for (int c = 0; c < m; ++c) {                         // Gauss-Jordan, partial pivoting
-            if (ti == 0) {
-                double best = -1.0;
-                int bi = c;
-                for (int r = c + tj; r < m; r += 64) {
-                    const double v = fabs(R[r][c]);
-                    if (v > best) { best = v; bi = r; }
+            for (int j = tj; j < m; j += 64) Dg[i * m + j] = R0[i][j];
+        // Gauss-Jordan with partial pivoting, the augmented block held in registers: thread t owns
+        // the 8 x 4 tile (rows 8 (t / 36) .., columns 4 (t % 36) ..) of [D' | U | I]; per column the
+        // owners publish column c and then the pivot row through LDS (two barriers), every thread
+        // updates its 32 entries.  Rows are not interchanged: row piv[c] ends as row c of
+        // [I | W | D'^-1] and is written there.
+        constexpr int kTR = 8, kTC = 4, kNCG = (3 * kBtdMaxM) / kTC;   // 36 column groups
+        const int rg = tid / kNCG, cg = tid - rg * kNCG;
+        const bool owner = rg < kBtdMaxM / kTR;
+        double a[kTR][kTC];
+        if (owner) {
+#pragma unroll
+            for (int r = 0; r < kTR; ++r)
+#pragma unroll
+                for (int q = 0; q < kTC; ++q) {
+                    const int i = rg * kTR + r, j = cg * kTC + q;
+                    a[r][q] = (i < m && j < na) ? R0[i][j] : 0.0;
                 }
-                for (int off = 32; off > 0; off >>= 1) {
-                    const double ob = __shfl_xor(best, off);
-                    const int oi = __shfl_xor(bi, off);
-                    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        }
+        double* colbuf = &R1[0][0];                           // column c of the current matrix
+        double* rowbuf = &R1[1][0];                           // the pivot row (3 m entries)
+        int* used = reinterpret_cast<int*>(&R1[3][0]);        // row already a pivot
+        int* pivrow = reinterpret_cast<int*>(&R1[4][0]);      // pivot row of column c
+        for (int i = tid; i < m; i += kThreads) used[i] = 0;
+        __syncthreads();
+        for (int c = 0; c < m; ++c) {
+            if (owner && cg == c / kTC) {
+#pragma unroll
+                for (int r = 0; r < kTR; ++r) {
+                    const int i = rg * kTR + r;
+#pragma unroll
+                    for (int q = 0; q < kTC; ++q)
+                        if (q == c % kTC && i < m) colbuf[i] = a[r][q];
                 }
-                if (tj == 0) piv_s = bi;
             }
             __syncthreads();
-            const int p = piv_s;
-            if (p != c) {
-                for (int j = c + tid; j < na; j += kThreads) {
-                    const double a = R[c][j];
-                    R[c][j] = R[p][j];
-                    R[p][j] = a;
-                }
-                __syncthreads();
+            double best = -1.0;                               // every wave finds the same pivot
+            int bi = m;
+            if (tj < m && !used[tj]) { best = fabs(colbuf[tj]); bi = tj; }
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ob = __shfl_xor(best, off);
+                const int oi = __shfl_xor(bi, off);
+                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
             }
-            const double rd = 1.0 / R[c][c];
-            for (int i = ti; i < m; i += kRG) {
-                if (i == c) continue;
-                const double f = R[i][c] * rd;
-                for (int j = c + 1 + tj; j < na; j += 64) R[i][j] -= f * R[c][j];
+            const int p = bi;
+            if (owner && rg == p / kTR) {
+#pragma unroll
+                for (int r = 0; r < kTR; ++r)
+                    if (rg * kTR + r == p)
+#pragma unroll
+                        for (int q = 0; q < kTC; ++q) rowbuf[cg * kTC + q] = a[r][q];
             }
             __syncthreads();
-            for (int j = c + 1 + tid; j < na; j += kThreads) R[c][j] *= rd;
+            const double rp = 1.0 / colbuf[p];
+            if (owner) {
+                double pr[kTC];
+#pragma unroll
+                for (int q = 0; q < kTC; ++q) pr[q] = rowbuf[cg * kTC + q] * rp;
+#pragma unroll
+                for (int r = 0; r < kTR; ++r) {
+                    const int i = rg * kTR + r;
+                    if (i < m) {
+                        const double f = colbuf[i];
+#pragma unroll
+                        for (int q = 0; q < kTC; ++q) a[r][q] = i == p ? pr[q] : a[r][q] - f * pr[q];
+                    }
+                }
+            }
+            if (tid == 0) { used[p] = 1; pivrow[c] = p; }
             __syncthreads();
         }
+        // row pivrow[c] holds row c of the result: scatter back to R0 in order
+        if (owner) {
+#pragma unroll
+            for (int r = 0; r < kTR; ++r)
+#pragma unroll
+                for (int q = 0; q < kTC; ++q) {
+                    const int i = rg * kTR + r, j = cg * kTC + q;
+                    if (i < m && j < na) R0[i][j] = a[r][q];
+                }
+        }
+        __syncthreads();
+        double (*src)[3 * kBtdMaxM + 1] = R0;
+        int* rowof = reinterpret_cast<int*>(&R1[5][0]);
+        for (int c = tid; c < m; c += kThreads) rowof[c] = pivrow[c];
+        __syncthreads();
         for (int i = ti; i < m; i += kRG) {
+            const int ri = rowof[i];
             for (int j = tj; j < m; j += 64) {
-                Wp[i][j] = R[i][m + j];
-                if (!last) Ug[i * m + j] = R[i][m + j];
-                Dinv[(size_t)k * mm + i * m + j] = R[i][2 * m + j];
+                Wp[i][j] = src[ri][m + j];
+                if (!last) Ug[i * m + j] = src[ri][m + j];
+                Dinv[(size_t)k * mm + i * m + j] = src[ri][2 * m + j];
             }
         }
         __syncthreads();
+    }
+}
+
+// Z[i][j] (-)= sum_c M[i][c] Y[c][j] for i < m, j < w: with few right-hand sides one wave per
+// (i, j) and the lanes over c (wave-shuffle sum) -- the one-right-hand-side solves of the
+// interior-point refinement would otherwise leave 60 of 64 lanes idle; with many, one thread per
+// (row group, column).
+template <int SIGN>
+__device__ __forceinline__ void btd_matmul(double (*M)[kBtdMaxM + 1], double (*Yv)[kBtdMaxRhs + 1],
+                                           double (*Zv)[kBtdMaxRhs + 1], double (*Out)[kBtdMaxRhs + 1],
+                                           int m, int w, int ti, int tj, bool init_zero) {
+    if (w <= 8) {
+        for (int p = ti; p < m * w; p += kRG) {
+            const int i = p / w, j = p - i * w;
+            double v = tj < m ? M[i][tj] * Yv[tj][j] : 0.0;
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (tj == 0) Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * v;
+        }
+    } else {
+        for (int i = ti; i < m; i += kRG) {
+            for (int j = tj; j < w; j += 64) {
+                double acc = 0.0;
+                for (int c = 0; c < m; ++c) acc += M[i][c] * Yv[c][j];
+                Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * acc;
+            }
+        }
     }
 }
 
@@ -346,14 +441,8 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
                 for (int j = tj; j < m; j += 64) A[i][j] = T[((size_t)k * 3 + 0) * mm + i * m + j];
         }
         __syncthreads();
-        if (k > 0) {
-            for (int i = ti; i < m; i += kRG) {
-                for (int j = tj; j < w; j += 64) {
-                    double acc = Z[i][j];
-                    for (int c = 0; c < m; ++c) acc -= A[i][c] * Y[c][j];
-                    Z[i][j] = acc;
-                }
-            }
+        if (k > 0) {                                          // Z -= L_k Y_{k-1}
+            btd_matmul<-1>(A, Y, Z, Z, m, w, ti, tj, false);
             __syncthreads();
         }
         for (int i = ti; i < m; i += kRG) {
@@ -363,31 +452,14 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
             }
         }
         __syncthreads();
-        for (int i = ti; i < m; i += kRG) {                   // Y = D'^-1 Z
-            for (int j = tj; j < w; j += 64) {
-                double acc = 0.0;
-                for (int c = 0; c < m; ++c) acc += A[i][c] * Z[c][j];
-                Y[i][j] = acc;
-            }
-        }
+        btd_matmul<1>(A, Z, Z, Y, m, w, ti, tj, true);        // Y = D'^-1 Z
         __syncthreads();
-        for (int i = ti; i < m; i += kRG) {                   // one refinement step: Q = Z - D' Y
-            for (int j = tj; j < w; j += 64) {
-                double acc = Z[i][j];
-                for (int c = 0; c < m; ++c) acc -= Dp[i][c] * Y[c][j];
-                Q[i][j] = acc;
-            }
-        }
+        btd_matmul<-1>(Dp, Y, Z, Q, m, w, ti, tj, false);     // one refinement step: Q = Z - D' Y
         __syncthreads();
-        for (int i = ti; i < m; i += kRG) {                   // Y += D'^-1 Q
-            for (int j = tj; j < w; j += 64) {
-                double acc = Y[i][j];
-                for (int c = 0; c < m; ++c) acc += A[i][c] * Q[c][j];
-                Y[i][j] = acc;
-                Xk[(size_t)i * ldx + j] = acc;
-            }
-        }
+        btd_matmul<1>(A, Q, Y, Y, m, w, ti, tj, false);       // Y += D'^-1 Q
         __syncthreads();
+        for (int i = ti; i < m; i += kRG)
+            for (int j = tj; j < w; j += 64) Xk[(size_t)i * ldx + j] = Y[i][j];
     }
     for (int k = nb - 2; k >= 0; --k) {                       // backward: x_k = Y_k - W_k x_{k+1}
         double* Xk = X + (size_t)k * m * ldx;
@@ -396,13 +468,7 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
             for (int j = tj; j < w; j += 64) Z[i][j] = Xk[(size_t)i * ldx + j];
         }
         __syncthreads();
-        for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < w; j += 64) {
-                double acc = Z[i][j];
-                for (int c = 0; c < m; ++c) acc -= A[i][c] * Y[c][j];
-                Z[i][j] = acc;
-            }
-        }
+        btd_matmul<-1>(A, Y, Z, Z, m, w, ti, tj, false);
         __syncthreads();
         for (int i = ti; i < m; i += kRG) {
             for (int j = tj; j < w; j += 64) {
@@ -619,11 +685,11 @@ int awelu_solve_batched(int n, int nrhs, int batch, const double* LU, const int*
 
 // Block-tridiagonal factorisation: T[b][nb][3][m][m] (sub-, main, super-diagonal block of each
 // block row; the sub-diagonal block of row 0 and the super-diagonal block of row nb-1 are
-// ignored), m <= 56.  In place: the super-diagonal blocks become W_k = D'_k^-1 U_k; Dinv[b][nb][m][m]
+// ignored), m <= 48.  In place: the super-diagonal blocks become W_k = D'_k^-1 U_k; Dinv[b][nb][m][m]
 // receives the inverted pivot blocks D'_k^-1.
 int awelu_btd_factor_batched(int nb, int m, int batch, double* T, double* Dinv, void* stream) {
     if (nb < 1 || m < 1 || m > kBtdMaxM || batch < 1 || !T || !Dinv) {
-        g_err = "need nb >= 1, 1 <= m <= 56, batch >= 1 and device pointers";
+        g_err = "need nb >= 1, 1 <= m <= 48, batch >= 1 and device pointers";
         return 1;
     }
     btd_factor_kernel<<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, T, Dinv);
@@ -640,7 +706,7 @@ int awelu_btd_factor_batched(int nb, int m, int batch, double* T, double* Dinv, 
 int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, const double* T, const double* Dinv, double* X,
                             void* stream) {
     if (nb < 1 || m < 1 || m > kBtdMaxM || nrhs < 1 || batch < 1 || !T || !Dinv || !X) {
-        g_err = "need nb >= 1, 1 <= m <= 56, nrhs >= 1, batch >= 1 and device pointers";
+        g_err = "need nb >= 1, 1 <= m <= 48, nrhs >= 1, batch >= 1 and device pointers";
         return 1;
     }
     for (int j0 = 0; j0 < nrhs; j0 += kBtdMaxRhs) {

@@ -26,7 +26,7 @@ int awelu_factor_batched(int n, int batch, double* A, int* piv, void* stream);
 int awelu_solve_batched(int n, int nrhs, int batch, const double* LU, const int* piv, double* X, void* stream);
 
 /* Block-tridiagonal systems (the stage-ordered separator system of the structured KKT):
- * T[b][nb][3][m][m] = (block (k, k-1), block (k, k), block (k, k+1)) of each block row, m <= 56.
+ * T[b][nb][3][m][m] = (block (k, k-1), block (k, k), block (k, k+1)) of each block row, m <= 48.
  * Block LU without interchanges between block rows (partial pivoting inside each diagonal block).
  * factor: in place, the diagonal blocks become D'_k, the super-diagonal blocks W_k = D'_k^-1 U_k,
  * and Dinv[b][nb][m][m] receives D'_k^-1;  solve: X[b][nb m][nrhs] <- T^-1 X in place with those factors. */

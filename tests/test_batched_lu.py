@@ -54,7 +54,7 @@ def test_lu_solve_matches_torch(gpu, batch, n, nrhs):
 
 
 @pytest.mark.parametrize("batch,nb,m,nrhs", [(1, 1, 1, 1), (4, 5, 7, 2), (256, 21, 22, 1), (3, 9, 32, 8),
-                                            (1, 81, 23, 30), (2, 41, 50, 70), (1, 7, 56, 3)])
+                                            (1, 81, 23, 30), (2, 41, 46, 70), (8, 41, 46, 1), (1, 7, 48, 3)])
 def test_btd_solve_matches_dense(gpu, batch, nb, m, nrhs):
     """awelu_btd_factor_batched + awelu_btd_solve_batched (chunked beyond 64 right-hand sides, as
     for nrhs = 70) against a dense solve of the assembled block-tridiagonal matrix;
