@@ -95,13 +95,13 @@ class BorderedBtd:
         T = T.view(B, nb, 3, m, m)
         self.B = B
         self.squeeze = squeeze
-        if T.is_cuda:
+        from .batched_lu import BTD_MAX_M
+        self.fused = T.is_cuda and m <= BTD_MAX_M
+        if self.fused:
             from .batched_lu import btd_factor
             self.Tf = btd_factor(T)
         else:
-            from .batched_lu import btd_dense
-            self.T_blocks = T
-            self.Tf = torch.linalg.lu_factor(btd_dense(T))
+            self._factor_blocks(T)
         self.Fm = Fm.view(B, nG, n_t)
         if nG:
             self.Z = self._t_solve(E.view(B, n_t, nG))                     # T^-1 E
@@ -117,17 +117,12 @@ class BorderedBtd:
         are taken out."""
         from .batched_lu import sym_inertia, sym_inertia_host
         B, nb, m = self.B, self.nb, self.m
-        if self.Tf[0].is_cuda:
+        f = sym_inertia if self.dev_is_cuda() else sym_inertia_host
+        if self.fused:
             F, Dinv = self.Tf                              # F's diagonal slots hold the pivot blocks D'_k
-            c = sym_inertia(F[:, :, 1].reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
-        else:                                              # host: the pivot blocks by the block recursion
-            T = self.T_blocks
-            D = T[:, 0, 1]
-            blocks = [D]
-            for k in range(1, nb):
-                D = T[:, k, 1] - T[:, k, 0] @ torch.linalg.solve(D, T[:, k - 1, 2])
-                blocks.append(D)
-            c = sym_inertia_host(torch.stack(blocks, 1).reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
+            c = f(F[:, :, 1].reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
+        else:
+            c = f(self.Dp.reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
         c = c.to(torch.int64)
         c[:, 0] -= self.n_unused
         if self.nG:
@@ -135,13 +130,50 @@ class BorderedBtd:
             c = c + cc.to(torch.int64)
         return c
 
+    def dev_is_cuda(self):
+        return torch.device(self.dev).type == "cuda"
+
+    def _factor_blocks(self, T):
+        """The block sweep by a block recursion over batched dense operations (blocks larger than
+        the fused kernels' LDS limit, and host tensors): D'_0 = D_0, W_k = D'_k^-1 U_k,
+        D'_k = D_k - L_k W_{k-1}, with an LU (partial pivoting) of every pivot block -- the awelu
+        kernels on the device, LAPACK on the host."""
+        B, nb, m = T.shape[0], self.nb, self.m
+        self.T_blocks = T
+        Dp, LUs, Ws = [], [], []
+        D = T[:, 0, 1]
+        for k in range(nb):
+            if k > 0:
+                D = T[:, k, 1] - T[:, k, 0] @ Ws[k - 1]
+            LU = self._lu(D.contiguous())
+            Dp.append(D)
+            LUs.append(LU)
+            if k < nb - 1:
+                Ws.append(self._lu_solve(LU, T[:, k, 2].contiguous()))
+        self.Dp = torch.stack(Dp, 1)
+        self.LUs, self.Ws = LUs, Ws
+
+    def _lu_solve(self, LU, X):
+        if X.is_cuda:
+            from .batched_lu import lu_solve
+            return lu_solve(LU[0], LU[1], X)
+        return torch.linalg.lu_solve(LU[0], LU[1], X)
+
     def _t_solve(self, X):
         B, nb, m = self.B, self.nb, self.m
-        if X.is_cuda:
+        if self.fused:
             from .batched_lu import btd_solve
             F, Dinv = self.Tf
             return btd_solve(F, Dinv, X.reshape(B, nb, m, -1)).view(B, nb * m, -1)
-        return torch.linalg.lu_solve(*self.Tf, X)
+        Xb = X.reshape(B, nb, m, -1)
+        T = self.T_blocks
+        Y = []
+        for k in range(nb):                                # forward: Y_k = D'_k^-1 (X_k - L_k Y_{k-1})
+            rk = Xb[:, k] if k == 0 else Xb[:, k] - T[:, k, 0] @ Y[k - 1]
+            Y.append(self._lu_solve(self.LUs[k], rk.contiguous()))
+        for k in range(nb - 2, -1, -1):                    # backward: x_k = Y_k - W_k x_{k+1}
+            Y[k] = Y[k] - self.Ws[k] @ Y[k + 1]
+        return torch.stack(Y, 1).reshape(B, nb * m, -1)
 
     @staticmethod
     def _lu(A):

@@ -194,11 +194,12 @@ def outputs(mc: du.MultiConstants, lay: du.MultiLayout, V: np.ndarray) -> dict:
     return {"avg_power_W": energy / T, "period_s": T, "energy_J": energy, "t_f": [t0, t1]}
 
 
-def make_evaluator(mc: du.MultiConstants, device="cuda"):
-    """Batch-1 dual-kite evaluator with the coloured central-difference Hessian (fd_hessian.py)."""
+def make_evaluator(mc: du.MultiConstants, device="cuda", batch: int = 1):
+    """Dual-kite evaluator of `batch` instances with the coloured central-difference Hessian
+    (fd_hessian.py)."""
     from .dual_evaluator import DualEvaluator
     from .fd_hessian import FdHessian
-    ev = DualEvaluator(mc, batch=1)
+    ev = DualEvaluator(mc, batch=batch)
     return FdHessian(ev, lambda B: DualEvaluator(mc, batch=B), ev.layout, device=device)
 
 
@@ -231,3 +232,36 @@ def optimize(mc: du.MultiConstants, ev, opts=None, device="cuda", v_init=None, v
         if final_step is not None and st.label == final_step:
             break
     return x, summary, outputs(mc, lay, x), res
+
+
+def optimize_batch(mc: du.MultiConstants, ev, u_refs, opts=None, device="cuda", v_init=None, verbose=False):
+    """The homotopy for B = len(u_refs) wind speeds at once (ev.batch == B), one batched
+    interior-point solve per step (ipm.solve_batch); returns (V [B, n_v], per-step summaries,
+    outputs per instance, results)."""
+    from .ipm import solve_batch
+    from .trajectory import hippo_options
+    lay = du.layout_for(mc)
+    v0 = du.initial_guess(mc, lay) if v_init is None else v_init
+    B = len(u_refs)
+    steps = schedule(mc, lay, v0)
+    lbg, ubg = lay.g_bounds()
+    x = np.tile(v0, (B, 1))
+    lam = zl = zu = None
+    summary = []
+    res = None
+    for st in steps:
+        P = np.stack([du.pack_p(lay, mc, v0, step=st.cost_step, u_ref=u) for u in u_refs])
+        t0 = time.perf_counter()
+        res = solve_batch(ev, P, x, st.lbx, st.ubx, lbg, ubg, lam0=lam, zl0=zl, zu0=zu,
+                          opts=hippo_options(st.label, opts), device=device)
+        rec = dict(step=st.label, status=[r.status for r in res], iterations=[r.iterations for r in res],
+                   f=[r.f for r in res], seconds=time.perf_counter() - t0,
+                   timing={k: round(v, 3) for k, v in res[0].timing.items()})
+        summary.append(rec)
+        if verbose:
+            print(rec, flush=True)
+        x = np.stack([r.x for r in res])
+        lam = np.stack([r.lam_g for r in res])
+        zl = np.stack([r.zl for r in res])
+        zu = np.stack([r.zu for r in res])
+    return x, summary, [outputs(mc, lay, x[b]) for b in range(B)], res

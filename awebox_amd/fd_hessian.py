@@ -13,8 +13,8 @@ directional differences give Hessian columns.  Structure of the collocation NLP 
   taken from the global columns by symmetry.
 
 n_colours = n_globals + interval stride (348 for the dual kites at d=4, 164 for AP2); one Hessian
-costs 2 n_colours gradient evaluations, done as ONE batched launch of the evaluator, and one
-batched sparse J^T lambda product.  The pattern is dense per interval block (upper triangle).
+costs 2 n_colours gradient evaluations, done as ONE batched launch of the evaluator (for B
+instances at once: B x 2 n_colours), and one fixed-order gather-sum for J^T lambda.  The pattern is dense per interval block (upper triangle).
 Truncation error of central differences with h = 1e-5 (1 + |x|) is O(h^2) of the third
 derivatives: ~1e-9 relative, checked against the exact AP2 Hessian kernel on the GPU
 (tests/test_fd_hessian.py).
@@ -25,7 +25,7 @@ import numpy as np
 
 
 class FdHessian:
-    """Adds ``sparsity_hess`` / ``nnz_h`` / ``eval_hess_device`` to a batch-1 evaluator ``ev``.
+    """Adds ``sparsity_hess`` / ``nnz_h`` / ``eval_hess_device`` to an evaluator ``ev`` (any batch).
 
     ``make_batched(B)`` must return an evaluator of the same NLP for B instances; ``layout``
     provides ``n_k``, ``interval_stride``, ``v_intervals``, ``n_v``.
@@ -41,7 +41,6 @@ class FdHessian:
         n_v, v0, stride, n_k = lay.n_v, lay.v_intervals, lay.interval_stride, lay.n_k
         self.n_glob = v0
         self.n_col = v0 + stride
-        self.evb = make_batched(2 * self.n_col)
         # colour of every column, and its "row block" (interval of a non-global column)
         colour = np.full(n_v, -1, dtype=np.int64)
         colour[:v0] = np.arange(v0)
@@ -79,26 +78,36 @@ class FdHessian:
         self.both = t.tensor(both, device=device)
         self.src_b_col = t.tensor(np.where(both, colour[row], 0), device=device)
         self.src_b_row = t.tensor(np.where(both, col, 0), device=device)
-        # J^T lambda as a sparse (n_v x nnz) CSR of ones times [nnz, B]
+        # J^T lambda: a fixed-order gather-sum of the entries' products into their columns
         colind, jrow = ev.sparsity_jac()
         self.jrow = t.tensor(jrow.astype(np.int64), device=device)
-        nnz = len(jrow)
-        self.S = t.sparse_csr_tensor(t.tensor(colind.astype(np.int64), device=device),
-                                     t.arange(nnz, device=device), t.ones(nnz, dtype=t.float64, device=device),
-                                     size=(n_v, nnz))
-        B = 2 * self.n_col
-        f64 = dict(dtype=t.float64, device=device)
-        self.Vb = t.zeros(B, n_v, **f64)
-        self.Pb = t.zeros(B, ev.n_p, **f64)
-        self.fb = t.zeros(B, **f64)
-        self.gb = t.zeros(B, ev.n_g, **f64)
-        self.gradb = t.zeros(B, n_v, **f64)
-        self.jacb = t.zeros(B, ev.nnz, **f64)
+        from .ipm import _ScatterSum
+        self.jt_sum = _ScatterSum(np.repeat(np.arange(n_v), np.diff(colind)), device)
+        self.make_batched = make_batched
+        self.evb, self.nb_inst = None, 0
         self.colour_t = t.tensor(colour, device=device)
+        f64 = dict(dtype=t.float64, device=device)
         mask = np.zeros((self.n_col, n_v))
         valid = colour >= 0
         mask[colour[valid], np.where(valid)[0]] = 1.0
         self.mask = t.tensor(mask, **f64)              # [n_col, n_v] direction of each colour
+
+    def _buffers(self, B):
+        """A batched evaluator of B x 2 n_col perturbed instances (built on first use per B)."""
+        import torch as t
+        if self.nb_inst != B:
+            nb = 2 * self.n_col * B
+            f64 = dict(dtype=t.float64, device=self.dev)
+            self.evb = None
+            self.evb = self.make_batched(nb)
+            ev, n_v = self.ev, self.layout.n_v
+            self.Vb = t.zeros(nb, n_v, **f64)
+            self.Pb = t.zeros(nb, ev.n_p, **f64)
+            self.fb = t.zeros(nb, **f64)
+            self.gb = t.zeros(nb, ev.n_g, **f64)
+            self.gradb = t.zeros(nb, n_v, **f64)
+            self.jacb = t.zeros(nb, ev.nnz, **f64)
+            self.nb_inst = B
 
     # ---- evaluator surface used by the solver --------------------------------------------
     def __getattr__(self, name):
@@ -108,29 +117,34 @@ class FdHessian:
         return self.hcolind.copy(), self.hrow.copy()
 
     def eval_hess_device(self, V, P, sigma, lam_g, H, stream=None):
-        """Upper-triangular CCS values of sigma f + lam_g^T g at V (one instance, B = 1)."""
+        """Upper-triangular CCS values of sigma f + lam_g^T g at V for every instance: V [B, n_v],
+        P [B, n_p], sigma [B], lam_g [B, n_g], H [B, nnz_h]; one batched launch of B x 2 n_col
+        perturbed evaluations."""
         import torch
-        x = V.reshape(-1)
-        h = self.rel_step * (1.0 + x.abs())                           # [n_v]
-        dirs = self.mask * h[None, :]                                # [n_col, n_v]
-        self.Vb[: self.n_col] = x[None, :] + dirs
-        self.Vb[self.n_col:] = x[None, :] - dirs
-        self.Pb[:] = P.reshape(1, -1)
+        x = V.reshape(-1, self.layout.n_v)
+        B, nc = x.shape[0], self.n_col
+        self._buffers(B)
+        h = self.rel_step * (1.0 + x.abs())                           # [B, n_v]
+        dirs = self.mask[None, :, :] * h[:, None, :]                 # [B, n_col, n_v]
+        Vb = self.Vb.view(B, 2, nc, -1)
+        Vb[:, 0] = x[:, None, :] + dirs
+        Vb[:, 1] = x[:, None, :] - dirs
+        self.Pb.view(B, 2 * nc, -1)[:] = P.reshape(B, 1, -1)
         self.evb.eval_nlp_device(self.Vb, self.Pb, self.fb, self.gb, self.gradb, self.jacb, stream=stream)
-        lam = lam_g.reshape(-1)
-        prod = self.jacb * lam[self.jrow][None, :]                   # [B, nnz]
-        jtl = (self.S @ prod.T).T                                    # [B, n_v]
-        gl = sigma.reshape(-1)[0] * self.gradb + jtl
-        step = (2.0 * h)                                             # per column
-        D = (gl[: self.n_col] - gl[self.n_col:])                     # [n_col, n_v]
+        lam = lam_g.reshape(B, -1)
+        prod = self.jacb.view(B, 2 * nc, -1) * lam[:, self.jrow][:, None, :]      # [B, 2 n_col, nnz]
+        jtl = self.jt_sum.add_into(torch.zeros(B, 2 * nc, x.shape[1], dtype=torch.float64, device=x.device), prod)
+        gl = sigma.reshape(B, 1, 1) * self.gradb.view(B, 2 * nc, -1) + jtl
+        step = 2.0 * h                                               # [B, n_v]
+        D = gl[:, :nc] - gl[:, nc:]                                  # [B, n_col, n_v]
         # divide each colour row by the step of the column it perturbs for that entry
-        va = D[self.src_a_col, self.src_a_row]
+        va = D[:, self.src_a_col, self.src_a_row]
         ca = torch.where(self.src_a_col < self.n_glob, self.src_a_col, self._col_of(self.src_a_col, self.src_a_row))
-        va = va / step[ca]
-        vb = D[self.src_b_col, self.src_b_row]
+        va = va / step[:, ca]
+        vb = D[:, self.src_b_col, self.src_b_row]
         cb = self._col_of(self.src_b_col, self.src_b_row)
-        vb = vb / step[cb]
-        H.reshape(-1)[:] = torch.where(self.both, 0.5 * (va + vb), va)
+        vb = vb / step[:, cb]
+        H.reshape(B, -1)[:] = torch.where(self.both, 0.5 * (va + vb), va)
 
     def _col_of(self, colour, row):
         """The column of `colour` perturbed in the row block of `row` (interval-own columns)."""

@@ -355,8 +355,7 @@ class StructuredKKT:
         self.btd = None
         self.force_btd = False                                  # CPU tests: the BTD path on host
         self.btd_off = False                                    # the dense separator LU even when btd exists
-        from .batched_lu import BTD_MAX_M
-        if lu_backend == "awelu" and separators == "btd" and 2 * nx <= BTD_MAX_M:
+        if lu_backend == "awelu" and separators == "btd":
             stage_of = np.full(self.nS, -1, dtype=np.int64)
             pos_of = np.zeros(self.nS, dtype=np.int64)
             free = np.asarray(nlp.free.cpu().numpy() if torch.is_tensor(nlp.free) else nlp.free)
@@ -632,6 +631,8 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     # exact inertia needs the separator pivot blocks of the block sweep on the device (a dense
     # Bunch-Kaufman pass over the whole Schur complement is ~1 s); otherwise the curvature test
     exact_inertia = opts.inertia == "exact" and (skkt.btd is not None or dev.type != "cuda")
+    if skkt.btd is not None and dev.type == "cuda":
+        skkt.force_btd = True
     timing = {}
 
     class _Phase:

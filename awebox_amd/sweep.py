@@ -33,7 +33,7 @@ import torch
 from . import homotopy as hm
 from . import problem as pb
 from .initial_guess import initial_guess
-from .ipm import IpmOptions, solve
+from .ipm import IpmOptions, solve, solve_batch
 from .trajectory import hippo_options, optimize
 
 N_OUT = 6   # u_ref, avg power, period, iterations, status ok, seconds
@@ -62,9 +62,9 @@ class _Ap2:
     def optimize(self, ev, opts, device, v0, u):
         return optimize(self.consts, ev, opts, device=device, v_init=v0, u_ref=u)
 
-    def optimize_batch(self, ev, opts, device, v0, us):
+    def optimize_batch(self, ev, opts, device, v0, us, verbose=False):
         from .trajectory import optimize_batch
-        return optimize_batch(self.consts, ev, us, opts, device=device, v_init=v0)
+        return optimize_batch(self.consts, ev, us, opts, device=device, v_init=v0, verbose=verbose)
 
 
 class _Dual:
@@ -95,6 +95,10 @@ class _Dual:
         from . import dual_homotopy as dh
         return dh.optimize(self.consts, ev, opts, device=device, v_init=v0, u_ref=u)
 
+    def optimize_batch(self, ev, opts, device, v0, us, verbose=False):
+        from . import dual_homotopy as dh
+        return dh.optimize_batch(self.consts, ev, us, opts, device=device, v_init=v0, verbose=verbose)
+
 
 def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda", opts: IpmOptions | None = None,
               verbose=False, point_solver=None, arch="single", mode="chain"):
@@ -105,7 +109,9 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     ``point_solver(u, prev) -> (V, outputs, iterations, ok, prev)`` replaces the per-point solve.
     mode "batch": the shard's points are independent trials solved side by side, the full homotopy
     from the standard initial guess for every point as one batched interior-point solve per step
-    (``make_evaluator(consts, batch)``)."""
+    (``make_evaluator(consts, batch)``).
+    mode "fan": the homotopy for the shard's first point, then the other points warm-started from
+    its solution in one batched final-step solve."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     coll_dev = torch.device(device)
@@ -157,11 +163,49 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     res_o = torch.full((per, N_OUT), float("nan"), dtype=torch.float64, device=coll_dev)
     prev = None
     t_rank = time.perf_counter()
+    if mode == "fan" and my_u:
+        # the reference's sweeping warm start, fanned out: the shard's first point runs the full
+        # homotopy, then every other point of the shard is warm-started from that solution (the
+        # final homotopy step's costs and bounds), all of them in one batched solve
+        done = ("solve_succeeded", "solved_to_acceptable_level")
+        t0 = time.perf_counter()
+        ev1 = make_evaluator(consts, 1)
+        V0, summary, out0, res0 = prob.optimize(ev1, opts, device, v0, my_u[0])
+        it0 = sum(r["iterations"] for r in summary)
+        ok0 = all(r["status"] in done for r in summary)
+        el0 = time.perf_counter() - t0
+        res_v[0] = torch.tensor(V0, device=coll_dev)
+        res_o[0] = torch.tensor([my_u[0], out0["avg_power_W"], out0["period_s"], it0, float(ok0), el0], device=coll_dev)
+        if verbose:
+            print(f"[rank {rank}] u_ref={my_u[0]:.3f} P={out0['avg_power_W']:.1f} W T={out0['period_s']:.2f} s "
+                  f"iters={it0} ok={ok0} {el0:.1f} s", flush=True)
+        rest = my_u[1:]
+        if rest:
+            del ev1
+            t1 = time.perf_counter()
+            final = prob.final_step(v0)
+            lbg, ubg = lay.g_bounds()
+            evb = make_evaluator(consts, len(rest))
+            P = np.stack([prob.pack_p(v0, final.cost_step, u) for u in rest])
+            rb = len(rest)
+            res = solve_batch(evb, P, np.tile(res0.x, (rb, 1)), final.lbx, final.ubx, lbg, ubg,
+                              lam0=np.tile(res0.lam_g, (rb, 1)), zl0=np.tile(res0.zl, (rb, 1)),
+                              zu0=np.tile(res0.zu, (rb, 1)), opts=hippo_options("final", opts), device=device)
+            el1 = time.perf_counter() - t1
+            for i, (u, r) in enumerate(zip(rest, res)):
+                out = prob.outputs(r.x)
+                res_v[1 + i] = torch.tensor(r.x, device=coll_dev)
+                res_o[1 + i] = torch.tensor([u, out["avg_power_W"], out["period_s"], r.iterations,
+                                             float(r.status in done), el1], device=coll_dev)
+                if verbose:
+                    print(f"[rank {rank}] u_ref={u:.3f} P={out['avg_power_W']:.1f} W T={out['period_s']:.2f} s "
+                          f"iters={r.iterations} ok={r.status in done} (batched warm start, {el1:.1f} s)", flush=True)
+        my_u = []
     if mode == "batch" and my_u:
         done = ("solve_succeeded", "solved_to_acceptable_level")
         t0 = time.perf_counter()
         evb = make_evaluator(consts, len(my_u))
-        Vb, summary, outs, _ = prob.optimize_batch(evb, opts, device, v0, my_u)
+        Vb, summary, outs, _ = prob.optimize_batch(evb, opts, device, v0, my_u, verbose=verbose)
         el = time.perf_counter() - t0
         for i, u in enumerate(my_u):
             iters = sum(r["iterations"][i] for r in summary)
@@ -224,11 +268,15 @@ def main():
     ap.add_argument("--max-iter", type=int, default=600)
     ap.add_argument("--out", default="gpurun_out/sweep.json")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--ipm-verbose", action="store_true", help="print every interior-point iteration")
+    ap.add_argument("--profile", action="store_true", help="phase timings of the interior-point solver")
     ap.add_argument("--separators", choices=["dense", "btd"], default="btd",
                     help="separator solve of the structured KKT (awebox_amd/btd.py for btd)")
-    ap.add_argument("--mode", choices=["chain", "batch"], default="batch",
+    ap.add_argument("--mode", choices=["chain", "batch", "fan"], default="fan",
                     help="chain: warm-start chain per shard (the reference's sweep); batch: the shard's points "
-                         "as one batched homotopy")
+                         "as one batched homotopy; fan: homotopy for the first point, batched warm start for the rest")
+    ap.add_argument("--grid", type=int, default=0,
+                    help="take the points from linspace(u-min, u-max, GRID) (config 4: 64), the first --points of it")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -244,14 +292,16 @@ def main():
     if dist is not None:
         dist.barrier()
     u = np.linspace(args.u_min, args.u_max, args.points)
+    if args.grid:
+        u = np.linspace(args.u_min, args.u_max, args.grid)[:args.points]
     if args.arch == "dual":
         from .dual_homotopy import make_evaluator
-        mk = lambda c: make_evaluator(c, device=f"cuda:{local_rank}")  # noqa: E731
+        mk = lambda c, b=1: make_evaluator(c, device=f"cuda:{local_rank}", batch=b)  # noqa: E731
     else:
         mk = lambda c, b=1: Ap2Evaluator(c, batch=b)  # noqa: E731
     res = run_sweep(u, n_k=args.n_k, d=args.d, make_evaluator=mk, dist=dist, device=f"cuda:{local_rank}",
-                    opts=IpmOptions(max_iter=args.max_iter, separators=args.separators,
-                                    ), verbose=args.verbose, arch=args.arch, mode=args.mode)
+                    opts=IpmOptions(max_iter=args.max_iter, separators=args.separators, verbose=args.ipm_verbose,
+                                    profile=args.profile), verbose=args.verbose, arch=args.arch, mode=args.mode)
     if res is not None:
         res = dict(res)
         res.pop("V_opt")
