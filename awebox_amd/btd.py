@@ -153,10 +153,11 @@ class BorderedBtd:
         self.Dp = torch.stack(Dp, 1)
         self.LUs, self.Ws = LUs, Ws
 
-    def _lu_solve(self, LU, X):
-        if X.is_cuda:
-            from .batched_lu import lu_solve
-            return lu_solve(LU[0], LU[1], X)
+    @staticmethod
+    def _lu_solve(LU, X):
+        """D'^-1 X from an LU of the pivot block (LAPACK convention: the awelu factors on the
+        device): rocBLAS/LAPACK triangular solves -- for the block recursion's few large blocks
+        the library's batched trsm beats the one-workgroup-per-matrix awelu solve."""
         return torch.linalg.lu_solve(LU[0], LU[1], X)
 
     def _t_solve(self, X):

@@ -179,6 +179,8 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
         if verbose:
             print(f"[rank {rank}] u_ref={my_u[0]:.3f} P={out0['avg_power_W']:.1f} W T={out0['period_s']:.2f} s "
                   f"iters={it0} ok={ok0} {el0:.1f} s", flush=True)
+            if res0.timing:
+                print(f"[rank {rank}] first point, final step timing {res0.timing}", flush=True)
         rest = my_u[1:]
         if rest:
             del ev1
@@ -192,6 +194,8 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
                               lam0=np.tile(res0.lam_g, (rb, 1)), zl0=np.tile(res0.zl, (rb, 1)),
                               zu0=np.tile(res0.zu, (rb, 1)), opts=hippo_options("final", opts), device=device)
             el1 = time.perf_counter() - t1
+            if verbose and res[0].timing:
+                print(f"[rank {rank}] batched warm start timing {res[0].timing}", flush=True)
             for i, (u, r) in enumerate(zip(rest, res)):
                 out = prob.outputs(r.x)
                 res_v[1 + i] = torch.tensor(r.x, device=coll_dev)

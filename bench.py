@@ -16,8 +16,10 @@ Also reported:
                   profiles/pmc_traffic.json, used only when that record was taken for the same
                   kernel sources and batch size (else null); the same record carries the FP64
                   VALU instruction counts behind `fp64`.
-  sweep        -- the metric's second half: wind-speed sweep trials/s, --sweep-points per GPU
-                  (first point: full homotopy; then warm starts), collectives over RCCL.
+  sweep        -- the metric's second half: wind-speed sweep trials/s, --sweep-points per GPU of
+                  config 4's grid linspace(5, 8, 64) (first point: full homotopy; the rest: one
+                  batched warm-started solve), collectives over RCCL; dual_sweep: the same for the
+                  dual kites (config 4 itself).
   cpu_baseline -- the CPU port of the evaluator (oracle/cpu, C++ with OpenMP over (instance,
                   interval), "port"; the reference CasADi/IPOPT stack cannot be installed) on a
                   bounded sample, rank 0, N=1 only, at all host threads and at one thread.
@@ -113,8 +115,9 @@ def main():
                     help="MPC instances for the config-5 block (3-DOF tracking MPC, N=20 d=4; 0: skip)")
     ap.add_argument("--dual-batch", type=int, default=128,
                     help="dual-kite NLP instances for the config-3 block (N=60 d=4 single_reelout; 0: skip)")
-    ap.add_argument("--dual-sweep-points", type=int, default=2,
-                    help="dual-kite u_ref sweep points per GPU (config 4 recipe, example discretization N=20; 0: skip)")
+    ap.add_argument("--dual-sweep-points", type=int, default=8,
+                    help="dual-kite u_ref sweep points per GPU (config 4: 8 of linspace(5, 8, 64), example "
+                         "discretization N=20; 0: skip)")
     ap.add_argument("--sweep-points", type=int, default=8,
                     help="u_ref sweep points solved per GPU for the sweep block, as one batched homotopy (0: skip)")
     args = ap.parse_args()
@@ -474,68 +477,83 @@ def rti_block(c, B, dev, dist, world, steps=10, warmup=3):
             "finite": bool(torch.isfinite(r.V).all().item())}
 
 
-def sweep_block(per_gpu, world, dist, dev, consts):
-    """Second half of the headline metric: wind-speed sweep trials/s (config 4's recipe,
-    u_ref = linspace(5, 8), contiguous blocks per GPU, template broadcast / seed scatter / solution
-    gather over RCCL).  Weak scaling: `per_gpu` points per rank, solved as independent trials side
-    by side -- the full homotopy from the standard initial guess for every point, one batched
-    interior-point solve per homotopy step (ipm.solve_batch on a batch-`per_gpu` evaluator).  The
-    whole sweep is timed between barriers, max over ranks (run_sweep's own clock, all-reduced)."""
+SWEEP_GRID = 64       # config 4: u_ref = linspace(5, 8, 64), 8 contiguous points per GPU
+
+
+def _grid_points(per_gpu, world):
+    """The points of the sweep: the first per_gpu x world of linspace(5, 8, 64) (config 4's grid;
+    rank r gets the contiguous block [r per_gpu, (r + 1) per_gpu)), or an even spread over 5..8 m/s
+    when more points are asked for than the grid holds."""
     import numpy as np
+    n_pts = per_gpu * world
+    if n_pts <= SWEEP_GRID:
+        return np.linspace(5.0, 8.0, SWEEP_GRID)[:n_pts]
+    return np.linspace(5.0, 8.0, n_pts)
+
+
+def sweep_block(per_gpu, world, dist, dev, consts):
+    """Second half of the headline metric: wind-speed sweep trials/s on config 4's recipe (points of
+    u_ref = linspace(5, 8, 64), contiguous blocks of `per_gpu` per GPU, template broadcast / seed
+    scatter / solution gather over RCCL), the AP2 N=40 d=4 trial.  Per shard (weak scaling): the
+    full homotopy for the first point, then the other points warm-started from its solution in one
+    batched interior-point solve (sweep.py mode "fan": the reference's sweeping warm start,
+    fanned out).  Timed between barriers, max over ranks (run_sweep's clock, all-reduced)."""
     import torch
 
     from awebox_amd.evaluator import Ap2Evaluator
     from awebox_amd.ipm import IpmOptions
     from awebox_amd.sweep import run_sweep
 
-    n_pts = per_gpu * world
-    u = np.linspace(5.0, 8.0, n_pts)
+    u = _grid_points(per_gpu, world)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     res = run_sweep(u, n_k=consts.cfg.n_k, d=consts.cfg.d, make_evaluator=lambda c, b=1: Ap2Evaluator(c, batch=b),
-                    dist=dist, device=str(dev), opts=IpmOptions(max_iter=1000), mode="batch")
+                    dist=dist, device=str(dev), opts=IpmOptions(max_iter=1000), mode="fan")
     if res is None:
         return None
     return {"metric": "sweep trials/sec, AP2 N=40 d=4 power curve", "value": res["trials_per_s"],
-            "unit": "trials/s", "points": n_pts, "points_per_gpu": per_gpu, "wall_s": res["wall_s"],
+            "unit": "trials/s", "points": len(u), "points_per_gpu": per_gpu, "wall_s": res["wall_s"],
+            "u_ref": [round(x, 4) for x in res["u_ref"]],
             "all_converged": bool(all(res["ok"])), "iterations": res["iterations"],
             "avg_power_W": [round(p, 1) for p in res["avg_power_W"]],
             "period_s": [round(t, 2) for t in res["period_s"]], "scaling": "weak",
-            "solver": "GPU interior point (awebox_amd/ipm.py solve_batch): the shard's points as one batched "
-                      "homotopy; structured KKT (batched interval LU + block-tridiagonal separators), exact "
-                      "Hessian, IPOPT inertia correction from exact KKT inertia, second-order corrections"}
+            "solver": "GPU interior point (awebox_amd/ipm.py): homotopy for the shard's first point, batched "
+                      "warm start (solve_batch) for the rest; structured KKT (batched interval LU + "
+                      "block-tridiagonal separators), exact Hessian, IPOPT inertia correction from exact KKT "
+                      "inertia, second-order corrections"}
 
 
 def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
     """Config 4: the dual-kite power curve (examples/dual_kites_power_curve.py: architecture
-    {1:0, 2:1, 3:1}, N=20 d=4 as in the example, u_ref = linspace(5, 8)), `per_gpu` points per
-    rank in contiguous blocks (weak scaling), template broadcast / seed scatter / solution gather
-    over RCCL; per point the GPU interior-point solver with the HIP dual-kite evaluator and the
-    coloured central-difference Hessian.  Timed by run_sweep between barriers, max over ranks."""
-    import numpy as np
+    {1:0, 2:1, 3:1}, N=20 d=4 as in the example, single_reelout), each GPU's shard of
+    u_ref = linspace(5, 8, 64): `per_gpu` contiguous points (weak scaling), template broadcast / seed
+    scatter / solution gather over RCCL; per shard the homotopy for the first point and one batched
+    warm-started solve for the rest (the HIP dual-kite evaluator, coloured central-difference
+    Hessian, exact-inertia interior point).  Timed by run_sweep between barriers, max over ranks."""
     import torch
 
     from awebox_amd.dual_homotopy import make_evaluator
     from awebox_amd.ipm import IpmOptions
     from awebox_amd.sweep import run_sweep
 
-    n_pts = per_gpu * world
-    u = np.linspace(5.0, 8.0, n_pts)
+    u = _grid_points(per_gpu, world)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    res = run_sweep(u, n_k=n_k, d=d, make_evaluator=lambda c: make_evaluator(c, device=str(dev)), dist=dist,
-                    device=str(dev), opts=IpmOptions(max_iter=1500), arch="dual")
+    res = run_sweep(u, n_k=n_k, d=d, make_evaluator=lambda c, b=1: make_evaluator(c, device=str(dev), batch=b),
+                    dist=dist, device=str(dev), opts=IpmOptions(max_iter=3000), arch="dual", mode="fan")
     if res is None:
         return None
     return {"metric": f"sweep trials/sec, dual-kite power curve N={n_k} d={d} (config 4)",
-            "value": res["trials_per_s"], "unit": "trials/s", "points": n_pts, "points_per_gpu": per_gpu,
+            "value": res["trials_per_s"], "unit": "trials/s", "points": len(u), "points_per_gpu": per_gpu,
+            "grid": f"linspace(5, 8, {SWEEP_GRID}), contiguous shards", "u_ref": [round(x, 4) for x in res["u_ref"]],
             "wall_s": res["wall_s"], "all_converged": bool(all(res["ok"])), "iterations": res["iterations"],
             "avg_power_W": [round(p, 1) for p in res["avg_power_W"]],
             "period_s": [round(t, 2) for t in res["period_s"]], "scaling": "weak",
-            "solver": "GPU interior point (awebox_amd/ipm.py), structured KKT with batched LU (batched_lu.hip), "
-                      "Hessian by coloured central differences of the HIP gradient (fd_hessian.py)"}
+            "solver": "GPU interior point (awebox_amd/ipm.py): homotopy for the shard's first point, batched warm "
+                      "start for the rest; structured KKT with the block-recursion separator sweep, exact KKT "
+                      "inertia; Hessian by coloured central differences of the HIP gradient (fd_hessian.py)"}
 
 
 def hessian_block(ev, V, P, B, lay, dev, steps=10):
