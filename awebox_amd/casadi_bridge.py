@@ -1,21 +1,29 @@
 """Drop-in for ``casadi.nlpsol``'s NLP functions -- active only where ``import casadi`` works.
 
 In the reference the NLP handed to IPOPT is ``{'x': V, 'p': P, 'f': f_fun(V, P), 'g': g_fun(V, P)}``
-(awebox/opti/preparation.py:366-400) and CasADi generates nlp_f / nlp_g / nlp_grad_f / nlp_jac_g
-from the expanded SX graph.  Here ``f`` and ``g`` are ``casadi.Callback`` objects backed by the HIP
-evaluator, following the in-tree Callback idiom (awebox/tools/callback.py:31-60:
-get_n_in / get_sparsity_in / eval) plus ``has_jacobian`` / ``get_jacobian`` so that CasADi asks the
-evaluator for J_g (in its fixed CCS pattern) and grad f instead of differentiating.
+(awebox/opti/preparation.py:366-400) and CasADi generates nlp_f / nlp_g / nlp_grad_f / nlp_jac_g /
+nlp_hess_l from the expanded SX graph.  Here ``f`` and ``g`` are ``casadi.Callback`` objects backed
+by the HIP evaluator, following the in-tree Callback idiom (awebox/tools/callback.py:31-60:
+get_n_in / get_sparsity_in / eval):
+
+* f and g values come from the value-only kernel (``awe_eval_f_host`` / ``awe_eval_g_host``: the
+  model in plain double, no derivatives) -- IPOPT's line-search trials;
+* ``has_jacobian`` / ``get_jacobian`` make CasADi ask the evaluator for grad f and J_g (the fused
+  derivative kernel, J_g in its fixed CCS pattern) instead of differentiating;
+* the exact Hessian of the Lagrangian (IPOPT's default, awebox/opts/default.py:323 and
+  preparation.py:272-273) comes from the hyper-dual Hessian kernel through the ``hess_lag``
+  option of nlpsol: a Callback (x, p, lam_f, lam_g) -> upper triangle of sigma f + lam^T g.
+
+The reference's P struct is fed unchanged: ``make_nlp`` takes the reference's P *layout* through
+``p_from_reference`` -- by default problem.pack_p_from_reference, which reads the struct entry by
+entry by name (discretization.py:168-179) -- so ``solver(x0=..., p=p_fix_num, ...)`` at
+optimization.py:363 keeps working.
 
 Use (inside awebox.opti.preparation, in place of the MX expressions):
 
-    from awebox_amd.casadi_bridge import make_nlp
-    nlp = make_nlp(evaluator)             # {'x','p','f','g'} built from Callbacks
-    solver = cas.nlpsol('solver', 'ipopt', nlp, {**opts, 'expand': False,
-                        'ipopt.hessian_approximation': 'limited-memory'})
-
-The exact Hessian of the Lagrangian (default in awebox, default.py:323) is the next kernel
-(DESIGN.md, row f1); until then IPOPT runs with L-BFGS through this bridge.
+    from awebox_amd.casadi_bridge import make_nlp, solver_options
+    nlp = make_nlp(evaluator, P_struct=nlp.P)       # {'x','p','f','g'} built from Callbacks
+    solver = cas.nlpsol('solver', 'ipopt', nlp, {**opts, **solver_options(nlp)})
 """
 from __future__ import annotations
 
@@ -36,38 +44,73 @@ def _require():
         raise ImportError("casadi is not importable here; the bridge is only needed where IPOPT runs via CasADi")
 
 
-def make_nlp(evaluator):
-    """Return {'x': V, 'p': P, 'f': f(V,P), 'g': g(V,P)} with MX symbols and Callback outputs."""
+def reference_p_reader(P_struct):
+    """A function turning the reference's numeric P (a DM of P_struct's size) into this library's
+    flat P, reading P_struct's entries by name (problem.pack_p_from_reference)."""
+    from . import problem as pb
+
+    def convert(p_num, layout):
+        s = P_struct(p_num)
+
+        def get(path):
+            try:
+                return np.asarray(s[path]).ravel()
+            except Exception as exc:                           # missing entry name in the struct
+                raise KeyError(path) from exc
+        return pb.pack_p_from_reference(get, layout)
+    return convert
+
+
+def make_nlp(evaluator, P_struct=None):
+    """Return {'x': V, 'p': P, 'f': f(V,P), 'g': g(V,P)} with MX symbols and Callback outputs.
+    With ``P_struct`` (the reference's casadi.tools P struct) the p input has the reference's size
+    and is converted by name on every call; without it, p is this library's flat P."""
     _require()
-    n_v, n_p = evaluator.n_v, evaluator.n_p
+    n_v = evaluator.n_v
+    convert = None
+    n_p = evaluator.n_p
+    if P_struct is not None:
+        convert = reference_p_reader(P_struct)
+        n_p = P_struct.size
     V = cas.MX.sym("V", n_v)
     P = cas.MX.sym("P", n_p)
-    F = _FCallback("awe_f", evaluator)
-    G = _GCallback("awe_g", evaluator)
-    keep = [F, G]
+    F = _FCallback("awe_f", evaluator, convert, n_p)
+    G = _GCallback("awe_g", evaluator, convert, n_p)
+    H = _HessCallback("awe_hess_l", evaluator, convert, n_p)
     nlp = {"x": V, "p": P, "f": F(V, P), "g": G(V, P)}
-    nlp["_callbacks"] = keep  # callbacks must outlive the solver
+    nlp["_callbacks"] = [F, G, H]  # callbacks must outlive the solver
+    nlp["_hess_lag"] = H
     return nlp
+
+
+def solver_options(nlp):
+    """nlpsol options that keep IPOPT's exact Hessian with the HIP Hessian kernel."""
+    return {"hess_lag": nlp["_hess_lag"], "expand": False}
 
 
 if cas is not None:  # pragma: no cover - exercised only where casadi is installed
 
     class _Base(cas.Callback):
-        def __init__(self, name, ev, opts=None):
+        def __init__(self, name, ev, convert, n_p, opts=None):
             cas.Callback.__init__(self)
-            self.ev = ev
+            self.ev, self.convert, self.n_p = ev, convert, n_p
             self.construct(name, opts or {})
 
         def get_n_in(self):
             return 2
 
         def get_sparsity_in(self, i):
-            return cas.Sparsity.dense(self.ev.n_v if i == 0 else self.ev.n_p)
+            return cas.Sparsity.dense(self.ev.n_v if i == 0 else self.n_p)
+
+        def _xp(self, arg):
+            x = np.asarray(arg[0]).reshape(1, -1)
+            p = np.asarray(arg[1]).reshape(-1)
+            if self.convert is not None:
+                p = self.convert(p, self.ev.layout)
+            return x, p.reshape(1, -1)
 
         def _call(self, arg):
-            x = np.asarray(arg[0]).reshape(-1)
-            p = np.asarray(arg[1]).reshape(-1)
-            return self.ev.eval_nlp(x.reshape(1, -1), p.reshape(1, -1))
+            return self.ev.eval_nlp(*self._xp(arg))
 
     class _GCallback(_Base):
         def get_n_out(self):
@@ -77,17 +120,17 @@ if cas is not None:  # pragma: no cover - exercised only where casadi is install
             return cas.Sparsity.dense(self.ev.n_g)
 
         def eval(self, arg):
-            return [self._call(arg)["g"][0]]
+            return [self.ev.eval_g(*self._xp(arg))[0]]
 
         def has_jacobian(self):
             return True
 
         def get_jacobian(self, name, inames, onames, opts):
-            self._jac = _JacGCallback(name, self.ev, opts)
+            self._jac = _JacGCallback(name, self.ev, self.convert, self.n_p, opts)
             return self._jac
 
     class _JacGCallback(_Base):
-        # inputs: x, p, g (nominal output); outputs: d g/d x (CCS), d g/d p (structurally zero)
+        # inputs: x, p, g (nominal output); outputs: d g/d x (CCS), d g/d p (not needed by IPOPT)
         def get_n_in(self):
             return 3
 
@@ -103,13 +146,13 @@ if cas is not None:  # pragma: no cover - exercised only where casadi is install
             if i == 0:
                 colind, row = self.ev.sparsity_jac()
                 return cas.Sparsity(self.ev.n_g, self.ev.n_v, colind.tolist(), row.tolist())
-            return cas.Sparsity(self.ev.n_g, self.ev.n_p)
+            return cas.Sparsity(self.ev.n_g, self.n_p)
 
         def eval(self, arg):
             out = self._call(arg)
             colind, row = self.ev.sparsity_jac()
             J = cas.DM(cas.Sparsity(self.ev.n_g, self.ev.n_v, colind.tolist(), row.tolist()), out["jac"][0])
-            return [J, cas.DM(cas.Sparsity(self.ev.n_g, self.ev.n_p))]
+            return [J, cas.DM(cas.Sparsity(self.ev.n_g, self.n_p))]
 
     class _FCallback(_Base):
         def get_n_out(self):
@@ -119,13 +162,13 @@ if cas is not None:  # pragma: no cover - exercised only where casadi is install
             return cas.Sparsity.dense(1)
 
         def eval(self, arg):
-            return [self._call(arg)["f"][0]]
+            return [self.ev.eval_f(*self._xp(arg))[0]]
 
         def has_jacobian(self):
             return True
 
         def get_jacobian(self, name, inames, onames, opts):
-            self._jac = _GradFCallback(name, self.ev, opts)
+            self._jac = _GradFCallback(name, self.ev, self.convert, self.n_p, opts)
             return self._jac
 
     class _GradFCallback(_Base):
@@ -141,10 +184,45 @@ if cas is not None:  # pragma: no cover - exercised only where casadi is install
             return 2
 
         def get_sparsity_out(self, i):
-            return cas.Sparsity.dense(1, self.ev.n_v) if i == 0 else cas.Sparsity(1, self.ev.n_p)
+            return cas.Sparsity.dense(1, self.ev.n_v) if i == 0 else cas.Sparsity(1, self.n_p)
 
         def eval(self, arg):
             out = self._call(arg)
-            return [cas.DM(out["grad_f"][0]).T, cas.DM(cas.Sparsity(1, self.ev.n_p))]
+            return [cas.DM(out["grad_f"][0]).T, cas.DM(cas.Sparsity(1, self.n_p))]
+
+    class _HessCallback(_Base):
+        """nlp_hess_l: (x, p, lam_f, lam_g) -> upper triangle of lam_f f + lam_g^T g in the
+        kernel's fixed CCS pattern (nlpsol's hess_lag option)."""
+
+        def get_n_in(self):
+            return 4
+
+        def get_name_in(self, i):
+            return ["x", "p", "lam_f", "lam_g"][i]
+
+        def get_name_out(self, i):
+            return "hess_gamma_x_x"
+
+        def get_sparsity_in(self, i):
+            if i == 2:
+                return cas.Sparsity.dense(1)
+            if i == 3:
+                return cas.Sparsity.dense(self.ev.n_g)
+            return _Base.get_sparsity_in(self, i)
+
+        def get_n_out(self):
+            return 1
+
+        def get_sparsity_out(self, i):
+            colind, row = self.ev.sparsity_hess()
+            return cas.Sparsity(self.ev.n_v, self.ev.n_v, colind.tolist(), row.tolist())
+
+        def eval(self, arg):
+            x, p = self._xp(arg)
+            lam_f = float(np.asarray(arg[2]).reshape(-1)[0])
+            lam_g = np.asarray(arg[3]).reshape(1, -1)
+            H = self.ev.eval_hess(x, p, lam_f, lam_g)[0]
+            colind, row = self.ev.sparsity_hess()
+            return [cas.DM(cas.Sparsity(self.ev.n_v, self.ev.n_v, colind.tolist(), row.tolist()), H)]
 else:
-    _FCallback = _GCallback = None
+    _FCallback = _GCallback = _HessCallback = None

@@ -617,6 +617,130 @@ __global__ __launch_bounds__(64) void ap2_finalize_kernel(KArgs a) {
 }
 
 
+
+// =========================================================================================
+// Value-only evaluation (nlp_f / nlp_g): the model in plain double, one thread per node
+// =========================================================================================
+// The derivative kernel carries 32 colour lanes of dual numbers per node; nlp_f and nlp_g (IPOPT's
+// line-search trials) need none of it.  One 64-thread workgroup per (instance, interval): the
+// interval's V slice is staged in LDS, node values as in the derivative kernel, then thread n < d+1
+// evaluates node n of the same templated model (ap2_model.hpp) with T = double and inline
+// sub-models, and the objective terms of its Radau node serially; continuity rows and the
+// interval's objective partial follow, and ap2_finalize_kernel adds the global terms and the
+// periodicity rows.  Same formulas as the derivative kernel, summed in another order (values agree
+// to roundoff, tests/test_gpu_parity.py).
+struct ValueIn {
+    const double* w;
+    __device__ __forceinline__ double operator()(int i) const { return w[i]; }
+};
+
+struct ValueSink {
+    double* gv;
+    __device__ __forceinline__ void eq_row(int r, double v) { gv[r] = v; }
+    __device__ __forceinline__ void ineq_row(int r, double v) { gv[AWE_N_EQ + r] = v; }
+    __device__ __forceinline__ void power(double v) { gv[kRowPower] = v; }
+    __device__ __forceinline__ void beta(double v) { gv[kRowBeta] = v; }
+};
+
+template <int D>
+__global__ __launch_bounds__(64) void ap2_value_kernel(KArgs a) {
+    constexpr int NN = D + 1;
+    const int tid = threadIdx.x;
+    const int k = blockIdx.x % a.n_k;
+    const int b = blockIdx.x / a.n_k;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const double* th = P + a.n_v + AWE_NW + AWE_NCOST;
+    const double* cost = P + a.n_v + AWE_NW;
+    const double* wts = P + a.n_v;
+    const double* vref = P;
+    double* g = a.g + (size_t)b * a.n_g;
+    const double* C = a.coll.C;
+    __shared__ double vloc[nloc_pad<D>()];
+    __shared__ double wn[NN * 64];
+    __shared__ double gval[NN * kGvalStride];
+    __shared__ double fnode[NN + 1];
+    const int base = a.v_int0 + k * a.stride;
+    for (int i = tid; i < 9; i += 64) vloc[i] = V[i];
+    for (int i = tid; i < a.stride + AWE_NX; i += 64) vloc[9 + i] = V[base + i];
+    __syncthreads();
+    node_values_pass<D, 64>(vloc, C, a.n_k, wn, tid);
+    const double* vt = vloc;
+    const double* vx = vloc + 9;
+    const double* vcoll = vx + AWE_NX + AWE_NU + AWE_NX + AWE_NZ;
+    const double* vx1 = vcoll + D * (AWE_NX + AWE_NZ);
+    if (tid < NN) {
+        const int n = tid;
+        ValueIn in{wn + n * 64};
+        ValueSink sink{gval + n * kGvalStride};
+        awe::ap2_node<double>(in, vt[2 + kPhiGamma], th, a.cst, sink, n == 0, awe::InlineSubmodels());
+        double fn = 0.0;
+        if (n > 0) {                                         // objective at Radau node j (objective.py)
+            const int j = n - 1;
+            const double wj = a.coll.w[j];
+            const double* w = wn + n * 64;
+            const double* rb = vref + base;
+            const double* rcx = rb + 2 * AWE_NX + AWE_NU + AWE_NZ + j * (AWE_NX + AWE_NZ);
+            const double* ru = rb + AWE_NX;
+            const double psi = vt[2 + kPhiPsi];
+            const double w_track = cost[kCostTracking] / a.cst[AWE_C_NORM_TRACKING];
+            const double w_xdot = cost[kCostXdotRegularisation] / a.cst[AWE_C_NORM_XDOT_REG];
+            const double w_ureg = cost[kCostURegularisation] / a.cst[AWE_C_NORM_U_REG];
+            const double w_fict = cost[kCostFictitious] / a.cst[AWE_C_NORM_FICTITIOUS];
+            const double w_theta = cost[kCostThetaRegularisation] / a.cst[AWE_C_NORM_THETA_REG];
+            double trk = 0.0, xdr = 0.0, oth = 0.0;
+            for (int i = 0; i < AWE_NX; ++i) {
+                const double e = w[i] - rcx[i];
+                trk += wts[i] * w_track * (e * e);
+                const double xdv = w[AWE_NX + i];
+                xdr += wts[AWE_NX + i] * w_xdot * (xdv * xdv);
+            }
+            for (int i = 0; i < AWE_NU; ++i) {
+                const double e = w[2 * AWE_NX + i] - ru[i];
+                oth += wts[2 * AWE_NX + i] * (i < 6 ? w_fict : w_ureg) * (e * e);
+            }
+            {
+                const double e = w[kDirZ] - rcx[AWE_NX];
+                trk += wts[kDirZ] * w_track * (e * e);
+                const double et = w[kDirDiam] - vref[0];
+                oth += wts[kDirDiam] * w_theta * (et * et);
+            }
+            const double bv = gval[n * kGvalStride + kRowBeta];
+            const double pv = gval[n * kGvalStride + kRowPower];
+            const double cb = cost[kCostBeta] * wj / a.cst[AWE_C_NORM_BETA];
+            const double cp = -cost[kCostPower] * wj / (double)a.n_k;
+            fn = wj * (psi * trk + xdr + oth) + cb * (bv * bv) + (1.0 - psi) * (cp * pv);
+        }
+        fnode[n] = fn;
+    }
+    __syncthreads();
+    const DevColl* cc = &a.coll;
+    for (int r = tid; r < a.rows; r += 64) {
+        double val;
+        if (r < AWE_N_EQ + AWE_N_INEQ) {
+            val = gval[r];
+        } else if (r < AWE_N_EQ + AWE_N_INEQ + D * AWE_N_EQ) {
+            const int q = r - (AWE_N_EQ + AWE_N_INEQ);
+            val = gval[(1 + q / AWE_N_EQ) * kGvalStride + q % AWE_N_EQ];
+        } else {
+            const int i = r - (AWE_N_EQ + AWE_N_INEQ + D * AWE_N_EQ);
+            double xf = 0.0;
+            for (int rr = 0; rr < NN; ++rr) {
+                if (cc->D[rr] == 0.0) continue;
+                const double Xr = (rr == 0) ? vx[i] : vcoll[(rr - 1) * (AWE_NX + AWE_NZ) + i];
+                xf += cc->D[rr] * Xr;
+            }
+            val = vx1[i] - xf;
+        }
+        g[k * a.rows + r] = val;
+    }
+    if (tid == 0) {
+        double s = 0.0;
+        for (int n = 1; n < NN; ++n) s += fnode[n];
+        a.partial[((size_t)b * a.n_k + k) * kNPartial] = s;
+    }
+}
+
 // =========================================================================================
 // Hessian of the Lagrangian sigma f + lam^T g (nlp_hess_l)
 // =========================================================================================
@@ -971,13 +1095,25 @@ int launch(awe_handle h, const double* V, const double* P, double* f, double* g,
     a.v_int0 = h->t.lay.v_int0; a.tang_total = h->t.tang_total;
     a.want_derivs = want_derivs;
     HIP_TRY(hipEventRecord(h->ev[0], stream));
-    switch (h->t.d) {
-        case 1: launch_interval<1>(h, a, stream); break;
-        case 2: launch_interval<2>(h, a, stream); break;
-        case 3: launch_interval<3>(h, a, stream); break;
-        case 4: launch_interval<4>(h, a, stream); break;
-        case 5: launch_interval<5>(h, a, stream); break;
-        default: return fail(AWE_ERR_ARG, "unsupported collocation degree");
+    if (want_derivs) {
+        switch (h->t.d) {
+            case 1: launch_interval<1>(h, a, stream); break;
+            case 2: launch_interval<2>(h, a, stream); break;
+            case 3: launch_interval<3>(h, a, stream); break;
+            case 4: launch_interval<4>(h, a, stream); break;
+            case 5: launch_interval<5>(h, a, stream); break;
+            default: return fail(AWE_ERR_ARG, "unsupported collocation degree");
+        }
+    } else {                                          // nlp_f / nlp_g: the value-only kernel
+        const dim3 grid(h->batch * h->t.n_k), block(64);
+        switch (h->t.d) {
+            case 1: hipLaunchKernelGGL(ap2_value_kernel<1>, grid, block, 0, stream, a); break;
+            case 2: hipLaunchKernelGGL(ap2_value_kernel<2>, grid, block, 0, stream, a); break;
+            case 3: hipLaunchKernelGGL(ap2_value_kernel<3>, grid, block, 0, stream, a); break;
+            case 4: hipLaunchKernelGGL(ap2_value_kernel<4>, grid, block, 0, stream, a); break;
+            case 5: hipLaunchKernelGGL(ap2_value_kernel<5>, grid, block, 0, stream, a); break;
+            default: return fail(AWE_ERR_ARG, "unsupported collocation degree");
+        }
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev[1], stream));
@@ -1208,6 +1344,40 @@ int awe_eval_nlp_host(awe_handle h, const double* V, const double* P, double* f,
         !finite(jac, nb * h->t.nnz))
         return fail(AWE_ERR_NONFINITE, "non-finite value in NLP evaluation");
     return AWE_OK;
+}
+
+static int eval_value_host(awe_handle h, const double* V, const double* P, double* f, double* g) {
+    int rc = ensure_scratch(h);
+    if (rc) return rc;
+    const size_t nb = (size_t)h->batch;
+    if (!h->d_in_V) HIP_TRY(hipMalloc((void**)&h->d_in_V, sizeof(double) * nb * h->t.lay.n_v));
+    if (!h->d_in_P) HIP_TRY(hipMalloc((void**)&h->d_in_P, sizeof(double) * nb * h->t.lay.n_p));
+    HIP_TRY(hipMemcpy(h->d_in_V, V, sizeof(double) * nb * h->t.lay.n_v, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->d_in_P, P, sizeof(double) * nb * h->t.lay.n_p, hipMemcpyHostToDevice));
+    rc = launch(h, h->d_in_V, h->d_in_P, h->d_scr_f, h->d_scr_g, h->d_scr_grad, h->d_scr_jac, 0, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    bool ok = true;
+    if (f) {
+        HIP_TRY(hipMemcpy(f, h->d_scr_f, sizeof(double) * nb, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < nb; ++i) ok = ok && std::isfinite(f[i]);
+    }
+    if (g) {
+        HIP_TRY(hipMemcpy(g, h->d_scr_g, sizeof(double) * nb * h->t.lay.n_g, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < nb * (size_t)h->t.lay.n_g; ++i) ok = ok && std::isfinite(g[i]);
+    }
+    if (!ok) return fail(AWE_ERR_NONFINITE, "non-finite value in NLP evaluation");
+    return AWE_OK;
+}
+
+int awe_eval_f_host(awe_handle h, const double* V, const double* P, double* f) {
+    if (!h || !V || !P || !f) return fail(AWE_ERR_ARG, "null argument");
+    return eval_value_host(h, V, P, f, nullptr);
+}
+
+int awe_eval_g_host(awe_handle h, const double* V, const double* P, double* g) {
+    if (!h || !V || !P || !g) return fail(AWE_ERR_ARG, "null argument");
+    return eval_value_host(h, V, P, nullptr, g);
 }
 
 int awe_hess_nnz(awe_handle h, int* nnz_h) {

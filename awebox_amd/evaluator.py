@@ -25,7 +25,8 @@ AWE_OK, AWE_ERR_ARG, AWE_ERR_HIP, AWE_ERR_NONFINITE, AWE_ERR_NODEVICE = 0, 1, 2,
 
 EXPORTED_SYMBOLS = ["awe_create", "awe_destroy", "awe_last_error", "awe_sizes", "awe_sparsity_jac",
                     "awe_sparsity_jac_static",
-                    "awe_eval_nlp", "awe_eval_g", "awe_eval_f", "awe_eval_nlp_host",
+                    "awe_eval_nlp", "awe_eval_g", "awe_eval_f", "awe_eval_nlp_host", "awe_eval_f_host",
+                    "awe_eval_g_host",
                     "awe_last_kernel_ms", "awe_device_count", "awe_hess_nnz", "awe_sparsity_hess",
                     "awe_sparsity_hess_static", "awe_eval_hess", "awe_eval_hess_host", "awe_last_hess_ms"]
 
@@ -58,6 +59,8 @@ def load_library(path: str = _LIB_PATH):
     lib.awe_eval_g.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.awe_eval_f.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.awe_eval_nlp_host.argtypes = [h, dp, dp, dp, dp, dp, dp]
+    lib.awe_eval_f_host.argtypes = [h, dp, dp, dp]
+    lib.awe_eval_g_host.argtypes = [h, dp, dp, dp]
     lib.awe_last_kernel_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.awe_device_count.restype = ctypes.c_int
     lib.awe_sparsity_jac_static.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip]
@@ -266,11 +269,31 @@ class Ap2Evaluator:
             raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
         return self.eval_nlp(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1))
 
+    def eval_f(self, V, P):
+        """Host arrays in: f [B] from the value-only kernel (no derivatives)."""
+        V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))
+        P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(self.batch, self.n_p))
+        f = np.zeros(self.batch)
+        self._check(self._lib.awe_eval_f_host(self._h, _dptr(V), _dptr(P), _dptr(f)))
+        return f
+
+    def eval_g(self, V, P):
+        """Host arrays in: g [B, n_g] from the value-only kernel (no derivatives)."""
+        V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))
+        P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(self.batch, self.n_p))
+        g = np.zeros((self.batch, self.n_g))
+        self._check(self._lib.awe_eval_g_host(self._h, _dptr(V), _dptr(P), _dptr(g)))
+        return g
+
     def nlp_f(self, x, p):
-        return float(self._single(x, p)["f"][0])
+        if self.batch != 1:
+            raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
+        return float(self.eval_f(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1))[0])
 
     def nlp_g(self, x, p):
-        return self._single(x, p)["g"][0]
+        if self.batch != 1:
+            raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
+        return self.eval_g(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1))[0]
 
     def nlp_grad_f(self, x, p):
         out = self._single(x, p)

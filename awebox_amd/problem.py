@@ -488,3 +488,66 @@ def pack_p(layout: NlpLayout, consts: Ap2Constants, v_ref: np.ndarray, step: str
 
 def collocation(d: int = 4):
     return coefficients(d, "radau")
+
+
+def pack_p_from_reference(get, layout: NlpLayout) -> np.ndarray:
+    """P in this library's flat layout from the reference's P struct, read entry by entry by name.
+
+    The reference hands IPOPT ``p = P(p_fix_num)`` with ``P = struct([p: [ref (the V struct),
+    weights (model.variables)], cost (setup_nlp_cost's 20 entries), theta0 (the params tree)])``
+    (ocp/discretization.py:129-179; theta0 = struct_op.generate_nested_dict_struct(options['params']),
+    mdl/system.py:417-432).  ``get(path)`` returns the entry at ``path`` as an array, e.g.
+    ``get(('p', 'ref'))``, ``get(('cost', 'power'))``, ``get(('theta0', 'wind', 'u_ref'))`` or
+    ``get(('theta0', 'aero', 'stab_derivs', 'CX', 'alpha'))``; with a casadi.tools struct
+    ``P_num``: ``get = lambda path: np.asarray(P_num[path]).ravel()``.  The flat order of the
+    theta0 tree is never used, only the names of the entries the evaluator reads; a stability
+    derivative absent from the reference's tree (KeyError) is zero, as in its data file."""
+    p = np.zeros(layout.n_p)
+    p[layout.p_ref:layout.p_ref + layout.n_v] = np.asarray(get(("p", "ref")), dtype=np.float64).ravel()
+    p[layout.p_weights:layout.p_weights + NW] = np.asarray(get(("p", "weights")), dtype=np.float64).ravel()
+    for i, name in enumerate(COST_NAMES):
+        p[layout.p_cost + i] = float(np.asarray(get(("cost", name))).ravel()[0])
+    th = np.zeros(NTHETA0)
+    for name, size in THETA0_ENTRIES:
+        o, _ = THETA0_OFF[name]
+        if name == "aero.stab_derivs":
+            for ci, cname in enumerate(SD_COEFFS):
+                for ii, iname in enumerate(SD_INPUTS):
+                    try:
+                        v = np.asarray(get(("theta0", "aero", "stab_derivs", cname, iname)), dtype=np.float64).ravel()
+                    except KeyError:
+                        continue
+                    if len(v) > SD_MAXLEN:
+                        raise ValueError(f"stability derivative {cname}.{iname} has {len(v)} > {SD_MAXLEN} terms")
+                    b = o + (ci * len(SD_INPUTS) + ii) * SD_MAXLEN
+                    th[b:b + len(v)] = v
+        else:
+            v = np.asarray(get(("theta0",) + tuple(name.split("."))), dtype=np.float64).ravel()
+            if v.size != size:
+                raise ValueError(f"theta0 entry {name} has {v.size} values, expected {size}")
+            th[o:o + size] = v
+    p[layout.p_theta0:layout.p_theta0 + NTHETA0] = th
+    return p
+
+
+def reference_p_entries(P: np.ndarray, layout: NlpLayout) -> dict:
+    """The inverse view: {path: array} of a flat P under the reference's entry names (the paths
+    pack_p_from_reference reads); stability derivatives with their used terms only."""
+    P = np.asarray(P, dtype=np.float64)
+    out = {("p", "ref"): P[layout.p_ref:layout.p_ref + layout.n_v].copy(),
+           ("p", "weights"): P[layout.p_weights:layout.p_weights + NW].copy()}
+    for i, name in enumerate(COST_NAMES):
+        out[("cost", name)] = np.array([P[layout.p_cost + i]])
+    th = P[layout.p_theta0:layout.p_theta0 + NTHETA0]
+    for name, size in THETA0_ENTRIES:
+        o, _ = THETA0_OFF[name]
+        if name == "aero.stab_derivs":
+            for ci, cname in enumerate(SD_COEFFS):
+                for ii, iname in enumerate(SD_INPUTS):
+                    vals = AP2_STAB_DERIVS.get(cname, {}).get(iname)
+                    if vals:
+                        b = o + (ci * len(SD_INPUTS) + ii) * SD_MAXLEN
+                        out[("theta0", "aero", "stab_derivs", cname, iname)] = th[b:b + len(vals)].copy()
+        else:
+            out[("theta0",) + tuple(name.split("."))] = th[o:o + size].copy()
+    return out

@@ -283,6 +283,8 @@ def main():
         line["dual_sweep"] = dual_sweep
     if not args.no_hessian:
         line["hessian"] = hessian_block(ev, V, P, B, lay, dev)
+    if world == 1:
+        line["latency_batch1"] = latency_block(consts, lay, v0, with_cpu=not args.no_cpu_baseline)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(consts, lay, v0, args.cpu_seconds)
     print(json.dumps(line))
@@ -576,6 +578,39 @@ def hessian_block(ev, V, P, B, lay, dev, steps=10):
     return {"metric": "nlp_hess_l evals/sec", "value": B / dt, "unit": "evals/s", "ms_per_step": dt * 1e3,
             "kernel_ms": float(np.mean(kms)), "nnz_h": ev.nnz_h, "batch": B,
             "finite": bool(torch.isfinite(H).all().item())}
+
+
+def latency_block(consts, lay, v0, with_cpu=True, reps=50):
+    """Config 2's drop-in case: IPOPT on the host calls one NLP evaluation at a time through the
+    CasADi Callback.  Host round-trip latency (host arrays in and out, one instance) of the C-ABI's
+    host entry points -- awe_eval_f_host / awe_eval_g_host (value-only kernel) and
+    awe_eval_nlp_host (f, g, grad f, J_g) -- median of `reps`, beside the 1-thread CPU port."""
+    import numpy as np
+
+    from awebox_amd import problem as pb
+    from awebox_amd.evaluator import Ap2Evaluator
+    from awebox_amd.initial_guess import batch_member
+    ev = Ap2Evaluator(consts, batch=1)
+    V = batch_member(v0, lay, 0).reshape(1, -1)
+    P = pb.pack_p(lay, consts, v0).reshape(1, -1)
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3
+
+    out = {"unit": "ms", "instances": 1,
+           "nlp_f_host": med(lambda: ev.eval_f(V, P)), "nlp_g_host": med(lambda: ev.eval_g(V, P)),
+           "nlp_f_g_grad_jac_host": med(lambda: ev.eval_nlp(V, P))}
+    if with_cpu:
+        from oracle.cpu_port import CpuPort
+        port = CpuPort(consts)
+        out["cpu_port_1thread_f_g_grad_jac"] = med(lambda: port.eval_nlp(V, P, threads=1))
+    return out
 
 
 def cpu_baseline(consts, lay, v0, seconds):

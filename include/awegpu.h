@@ -134,6 +134,12 @@ int awe_eval_f(awe_handle h, const double* V, const double* P, double* f, void* 
 /* Host-pointer wrappers: copy in, evaluate, copy out, synchronise, check finiteness. */
 int awe_eval_nlp_host(awe_handle h, const double* V, const double* P, double* f, double* g,
                       double* grad_f, double* jac);
+/* Host-pointer value-only entry points (nlp_f / nlp_g of one call from IPOPT through CasADi): copy
+ * in, the value-only kernel (the model in plain double, no derivatives), copy out; a NaN/Inf in
+ * the output returns AWE_ERR_NONFINITE.  Replace CasADi's nlp_f / nlp_g SX evaluation
+ * (awebox/opti/preparation.py:366-400, ocp/nlp.py:77-161). */
+int awe_eval_f_host(awe_handle h, const double* V, const double* P, double* f);
+int awe_eval_g_host(awe_handle h, const double* V, const double* P, double* g);
 
 /* Hessian of the Lagrangian sigma f + lam_g^T g (nlp_hess_l):
  * values of its upper triangle (row <= col) in the fixed CCS pattern of awe_sparsity_hess.

@@ -100,3 +100,30 @@ def test_initial_guess_is_a_closed_circular_orbit():
     np.testing.assert_allclose(R.T @ R, np.eye(3), atol=1e-12)
     vb = batch_member(v0, lay, 3)
     assert vb[0] == v0[0] and not np.allclose(vb[20:], v0[20:])
+
+
+def test_pack_p_from_reference_round_trips_by_name():
+    """The boundary adapter from the reference's P struct (discretization.py:168-179), read by
+    entry name: a name-keyed view of a packed P packs back to the same vector, and a P assembled
+    from the reference's own named values (ampyx_data.py stability derivatives, the power cost,
+    u_ref by name) equals pack_p's."""
+    from awebox_amd.initial_guess import initial_guess
+    consts = pb.build_constants()
+    lay = pb.NlpLayout()
+    v0 = initial_guess(consts, lay)
+    P = pb.pack_p(lay, consts, v0, step="power1", u_ref=7.25)
+    entries = pb.reference_p_entries(P, lay)
+    assert np.array_equal(pb.pack_p_from_reference(entries.__getitem__, lay), P)
+    # built from names only: nested dicts as the reference's struct holds them
+    tree = {("p", "ref"): v0, ("p", "weights"): consts.weights}
+    for i, name in enumerate(pb.COST_NAMES):
+        tree[("cost", name)] = consts.cost_steps["power1"][i]
+    for (name, size) in pb.THETA0_ENTRIES:
+        if name != "aero.stab_derivs":
+            o, _ = pb.THETA0_OFF[name]
+            tree[("theta0",) + tuple(name.split("."))] = consts.theta0[o:o + size]
+    tree[("theta0", "wind", "u_ref")] = 7.25
+    for c, d in pb.AP2_STAB_DERIVS.items():
+        for inp, vals in d.items():
+            tree[("theta0", "aero", "stab_derivs", c, inp)] = np.asarray(vals)
+    assert np.array_equal(pb.pack_p_from_reference(tree.__getitem__, lay), P)
