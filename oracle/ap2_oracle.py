@@ -700,6 +700,59 @@ class Ap2Oracle:
         return grad(lambda v: self.nlp_f(v, P, layout, theta0_offsets, cost_names, phi_names))(V)
 
 
+# ---------------------------------------------------------------------------------------------
+# frame conversions (mdl/aero/kite_dir/frames.py:39-120) and the tether moment of a stick
+# attachment (holonomics.py:205-265, forces.py:174-190, vector_operations.py:238-262): restated
+# for the reference's own self-tests (frames.py:206-417, test/units/test_model.py:255-318); the
+# AP2 model uses com attachment (n = 0) and control-frame coefficients
+# ---------------------------------------------------------------------------------------------
+def smooth_normalize(v, eps=1e-8):
+    return v / smooth_norm(v, eps)
+
+
+def smooth_normed_cross(a, b, eps=1e-8):
+    return smooth_normalize(cross(a, b), eps)
+
+
+def wind_dcm(vec_u, kite_dcm):
+    """frames.get_wind_dcm: [D_hat, S_hat, L_hat] from the apparent wind and the span axis."""
+    d_hat = smooth_normalize(vec_u)
+    l_hat = smooth_normed_cross(vec_u, kite_dcm[:, 1])
+    s_hat = smooth_normed_cross(l_hat, d_hat)
+    return torch.stack([d_hat, s_hat, l_hat], dim=1)
+
+
+def from_body_to_earth(kite_dcm, v):
+    return kite_dcm @ v
+
+
+def from_earth_to_body(kite_dcm, v):
+    return torch.linalg.inv(kite_dcm) @ v                   # an inverse, not R^T (frames.py:50-55)
+
+
+def from_body_to_wind(vec_u, kite_dcm, v):
+    return torch.linalg.inv(wind_dcm(vec_u, kite_dcm)) @ from_body_to_earth(kite_dcm, v)
+
+
+def from_wind_to_body(vec_u, kite_dcm, v):
+    return from_earth_to_body(kite_dcm, wind_dcm(vec_u, kite_dcm) @ v)
+
+
+def tether_moment_stick(q, r_flat, lam, r_tether, l_t):
+    """forces.generate_tether_moments for a 6-DOF kite on tether node 1 with the stick attachment:
+    n = 2 jacobian_dcm(lam c, R)^T with c = 1/2 (|q + R r_tether|^2 - l_t^2) (holonomics.py:
+    205-265) and jacobian_dcm(expr) = unskew(R^T reshape(d expr / d r)) (vector_operations.py:
+    238-262); r_flat is the DCM in CasADi's column-major flat order."""
+    r_flat = r_flat.detach().clone().requires_grad_(True)
+    R = reshape33(r_flat)
+    node = q + R @ r_tether
+    W = lam * 0.5 * (torch.dot(node, node) - l_t ** 2)
+    (dW_dr,) = torch.autograd.grad(W, r_flat)
+    Rn = reshape33(r_flat.detach())
+    A = Rn.T @ reshape33(dW_dr)
+    return 2. * 0.5 * torch.stack([A[2, 1] - A[1, 2], A[0, 2] - A[2, 0], A[1, 0] - A[0, 1]])
+
+
 def _periodic_order():
     off, pos = {}, 0
     for n, s in _X:
