@@ -31,7 +31,11 @@ class FdHessian:
     provides ``n_k``, ``interval_stride``, ``v_intervals``, ``n_v``.
     """
 
-    def __init__(self, ev, make_batched, layout, device="cuda", rel_step=1e-5):
+    def __init__(self, ev, make_batched, layout, device="cuda", rel_step=1e-5, tail=False):
+        """``tail``: the columns after the last interval (x[n_k]) get the colours of the first
+        interval positions and a dense block of their own -- for an objective that is nonlinear
+        in x[n_k] (the MPC's terminal cost, pmpc.py:356-358); such columns may enter g only
+        linearly (the continuity rows).  Without it they have no Hessian entries."""
         import torch
         self.ev = ev
         self.layout = layout
@@ -46,15 +50,21 @@ class FdHessian:
         colour[:v0] = np.arange(v0)
         own = np.arange(v0, v0 + n_k * stride)
         colour[own] = v0 + (own - v0) % stride
+        n_tail = n_v - v0 - n_k * stride if tail else 0
+        if n_tail > stride:
+            raise ValueError("tail longer than an interval")
+        tail_cols = np.arange(v0 + n_k * stride, v0 + n_k * stride + n_tail)
+        colour[tail_cols] = v0 + (tail_cols - v0 - n_k * stride)
+        self.n_blocks = n_k + (1 if n_tail else 0)
         self.colour = colour
         # upper-triangular pattern: globals x everything below, interval blocks dense
         cols, rows = [], []
         for c in range(v0):
             cols.append(np.full(c + 1, c))
             rows.append(np.arange(c + 1))
-        for k in range(n_k):
+        for k in range(self.n_blocks):
             b = v0 + k * stride
-            for p in range(stride):
+            for p in range(stride if k < n_k else n_tail):
                 c = b + p
                 cols.append(np.full(v0 + p + 1, c))
                 rows.append(np.concatenate([np.arange(v0), np.arange(b, c + 1)]))
@@ -150,5 +160,5 @@ class FdHessian:
         """The column of `colour` perturbed in the row block of `row` (interval-own columns)."""
         lay = self.layout
         v0, stride = lay.v_intervals, lay.interval_stride
-        k = ((row - v0).clamp(min=0) // stride).clamp(max=lay.n_k - 1)
+        k = ((row - v0).clamp(min=0) // stride).clamp(max=self.n_blocks - 1)
         return v0 + k * stride + (colour - v0).clamp(min=0)

@@ -286,12 +286,18 @@ class StructuredKKT:
                 k, o = divmod(v - v0, stride)
                 if k < n_k and o >= nx:
                     owner[p] = k
+        # interval rows start at g0: the MPC NLP leads with nx initial-condition rows
+        # (ocp/operation.py:303-326), the periodic NLP has none
+        g0 = getattr(lay, "g_int0", 0)
+        if g0 > nx:
+            raise ValueError("more leading rows than states per node")
         for i, r in enumerate(nlp.ineq):
-            owner[n + i] = r // rows if r < n_k * rows else -1     # global rows (t_f bounds): separators
+            rr_ = r - g0
+            owner[n + i] = rr_ // rows if 0 <= rr_ < n_k * rows else -1    # global rows (t_f bounds): separators
         # interval rows, except the continuity rows: an interval has more rows than interior
         # unknowns (x[k], x[k+1] close the count), so their multipliers join the separators
-        rr = np.arange(m)
-        owner[ny + rr] = np.where((rr < n_k * rows) & (rr % rows < rows - nx), rr // rows, -1)
+        rr = np.arange(m) - g0
+        owner[ny + np.arange(m)] = np.where((rr >= 0) & (rr < n_k * rows) & (rr % rows < rows - nx), rr // rows, -1)
         self.owner = owner
         sep = np.where(owner < 0)[0]
         self.nS = len(sep)
@@ -367,8 +373,10 @@ class StructuredKKT:
                         if o < nx and k <= n_k:
                             stage_of[q], pos_of[q] = k, nx + o
                 elif p >= ny:
-                    r = p - ny
-                    if r < n_k * rows and r % rows >= rows - nx:
+                    r = p - ny - g0
+                    if r < 0:                                   # initial-condition rows: stage 0 beside x[0]
+                        stage_of[q], pos_of[q] = 0, r + g0
+                    elif r < n_k * rows and r % rows >= rows - nx:
                         stage_of[q], pos_of[q] = r // rows + 1, r % rows - (rows - nx)
             ss_r, ss_c = sep_id[P_[ss]], sep_id[Q_[ss]]
             sch_r, sch_c = lsep_arr[:, :, None].repeat(L, 2), lsep_arr[:, None, :].repeat(L, 1)
@@ -934,6 +942,9 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             for b in np.where(live)[0]:
                 if tp[0, b] <= 0.9 * theta0_[b] and filter_ok(b, tp[0, b], tp[1, b]):
                     succ[b], live[b] = True, False
+            if opts.verbose:
+                print(f"      restoration: theta {np.round(tp[0][want], 6).tolist()} a {a_acc[want].tolist()} "
+                      f"live {live[want].tolist()}", flush=True)
         return succ, yv, lam_r
 
     # ---- main loop -------------------------------------------------------------------------------
@@ -1051,9 +1062,12 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                        backtracks=int(nback[b]), soc=int(nsoc[b]))
             logs[b].append(rec)
         if opts.verbose:
-            b0 = int(np.where(active)[0][0]) if active.any() else 0
-            print(f"{it:4d} active={int(active.sum())} [b{b0}] f={f_host[b0]: .8e} pr={e_p[b0]:.2e} "
-                  f"du={e_d[b0]:.2e} mu={mu[b0]:.1e} a={alpha_acc[b0]:.2e} dw={dw_rec[b0]:.1e}", flush=True)
+            shown = np.where(active | (pending & ~rest_ok))[0]
+            for b0 in (shown if B <= 4 else shown[:1]):
+                print(f"{it:4d} active={int(active.sum())} [b{b0}] f={f_host[b0]: .8e} pr={e_p[b0]:.2e} "
+                      f"du={e_d[b0]:.2e} mu={mu[b0]:.1e} a={alpha_acc[b0]:.2e} dw={dw_rec[b0]:.1e} "
+                      f"bt={nback[b0]} soc={nsoc[b0]} th={theta[b0]:.2e}"
+                      + (" RESTORATION" if pending[b0] else ""), flush=True)
     for b in range(B):
         if status[b] == "max_iter" and kkt_err[b] <= opts.acceptable_tol:
             status[b] = "solved_to_acceptable_level"

@@ -197,6 +197,7 @@ class MpcLayout:
 
     def __init__(self, n_k: int = 20, d: int = 4):
         self.n_k, self.d = n_k, d
+        self.nx = NX                                                       # states per shooting node
         self.n_coll_var = NX + NZ
         self.interval_stride = NX + NU + NX + NZ + d * self.n_coll_var      # 77 for d=4
         self.v_theta, self.v_phi, self.v_xi = 0, NTH, NTH + NPHI
@@ -273,6 +274,48 @@ class MpcLayout:
             lb[self.g_path(k)] = -np.inf
         ub[self.g_path(0)] = np.inf          # path constraints at k = 0 released (pmpc.py:128-134)
         return lb, ub
+
+
+def fict_columns(lay: MpcLayout) -> np.ndarray:
+    """V indices of the fictitious forces f_fict10 of every interval's zoh control."""
+    o = W_OFF[("u", "f_fict10")][0] - NX - NX                      # offset inside u
+    return np.concatenate([lay.u(k)[o:o + 3] for k in range(lay.n_k)])
+
+
+def variable_bounds(consts: Kite3Constants, lay: MpcLayout):
+    """Scaled (lbx, ubx) of the MPC NLP.
+
+    ``var_bounds.get_scaled_variable_bounds`` (ocp/var_bounds.py:42-103) for a non-periodic
+    ('mpc') trajectory with zoh controls: the model's system bounds (opts/default.py:190-210,
+    model_funcs.py:897-914 for the tether control) on the shooting states x[k] of every node
+    k = 0..N, on u[k] and z[k]; collocation variables and xdot unbounded; then the MPC
+    overrides of pmpc.py: x[0] released (:120-121, the initial-condition rows fix it), phi <= 0
+    and xi = 0 (:177-179), f_fict fixed to 0 (:181-190), theta fixed to (diam_t, t_f = N ts)
+    (user_options.trajectory.fixed_params, :75-82).  phi's lower bound 0 comes from
+    model.parameter_bounds (the homotopy parameters' [0, 1]).  Names carry their node identifier
+    in the model (q10, coeff10, lambda10); define_bounds (mdl/system.py:353-383) looks them up
+    without it."""
+    cfg, s = consts.cfg, consts.scaling
+    inf = np.inf
+    lb, ub = np.full(lay.n_v, -inf), np.full(lay.n_v, inf)
+    x_lb = np.concatenate([[-inf, -inf, 10.0], [-inf] * 3, cfg.coeff_min, [1e-2, -30.0, cfg.ddl_t_bounds[0]]])
+    x_ub = np.concatenate([[inf] * 3, [inf] * 3, cfg.coeff_max, [1e3, 30.0, cfg.ddl_t_bounds[1]]])
+    dcoeff_max = np.asarray(cfg.dcoeff_max)
+    u_lb = np.concatenate([[-inf] * 3, -dcoeff_max, [cfg.dddl_t_bounds[0]]])
+    u_ub = np.concatenate([[inf] * 3, dcoeff_max, [cfg.dddl_t_bounds[1]]])
+    sx, su, sz = s[:NX], s[2 * NX:2 * NX + NU], s[2 * NX + NU:2 * NX + NU + NZ]
+    for k in range(1, lay.n_k + 1):
+        lb[lay.x(k)], ub[lay.x(k)] = x_lb / sx, x_ub / sx
+    for k in range(lay.n_k):
+        lb[lay.u(k)], ub[lay.u(k)] = u_lb / su, u_ub / su
+        lb[lay.z(k)], ub[lay.z(k)] = 0.0, inf
+    fict = fict_columns(lay)
+    lb[fict] = ub[fict] = 0.0
+    theta = np.array([cfg.diam_t, lay.n_k * cfg.ts]) / s[2 * NX + NU + NZ:]
+    lb[lay.theta()] = ub[lay.theta()] = theta
+    lb[lay.phi()] = ub[lay.phi()] = 0.0
+    lb[lay.xi()] = ub[lay.xi()] = 0.0
+    return lb, ub
 
 
 # ---------------------------------------------------------------------------------------

@@ -21,8 +21,9 @@ step per sampling time for every loop, all loops batched:
 
 The path inequalities (tether stress, acceleration) and variable bounds are not part of the
 step: along the tracked orbit they are inactive and the driver reports their maximum residual
-(``rti_step`` output ``path_max``) instead of enforcing them.  Fixed globals (theta, phi, xi)
-are not unknowns.
+(``rti_step`` output ``path_max``) instead of enforcing them; ``mpc_solve.BatchedPmpc`` solves the
+same loops with bounds and inequalities to convergence (Pmpc.step).  Fixed globals (theta, phi,
+xi) and the fictitious forces f_fict (fixed to 0 by pmpc.py:181-190) are not unknowns.
 """
 from __future__ import annotations
 
@@ -61,12 +62,13 @@ class BatchedRti:
     """B tracking-MPC closed loops advanced by one real-time iteration per call of ``step``."""
 
     def __init__(self, consts: k3.Kite3Constants, batch: int, device="cuda", delta_w=1e-8, delta_c=0.0,
-                 evaluator=None, plant="collocation", n_fe=20):
+                 evaluator=None, plant="collocation", n_fe=20, fix_fict=True):
         """``evaluator``: anything with MpcEvaluator's device interface (sparsity_jac, n_p, nnz,
         eval_nlp_device); default = the HIP evaluator (awempc) for ``batch`` instances.
         ``plant``: "collocation" (interval 0's Radau collocation) or "rk4root" (the reference's
         sim integrator: ``n_fe`` RK4 steps per sampling time, the algebraic and derivative
-        variables by a Newton rootfinder at every stage; tools/integrator_routines.py:32-96)."""
+        variables by a Newton rootfinder at every stage; tools/integrator_routines.py:32-96).
+        ``fix_fict``: the fictitious forces stay at 0 (pmpc.py:181-190); False frees them."""
         self.consts, self.B, self.dev = consts, batch, torch.device(device)
         cfg = consts.cfg
         self.lay = lay = k3.MpcLayout(cfg.n_k, cfg.d)
@@ -81,6 +83,8 @@ class BatchedRti:
         nx, nk, st, v0 = k3.NX, lay.n_k, lay.interval_stride, lay.v_intervals
         # ---- unknowns: free V entries (interval variables + x[n_k]) and equality multipliers
         self.free = np.arange(v0, n_v)
+        self.fict = k3.fict_columns(lay) if fix_fict else np.zeros(0, dtype=np.int64)
+        self.free = np.setdiff1d(self.free, self.fict)
         path = np.concatenate([lay.g_path(k) for k in range(nk)])
         self.eq = np.setdiff1d(np.arange(n_g), path)
         self.path = path
@@ -296,16 +300,23 @@ class BatchedRti:
         R[:, r["idx"].reshape(-1)] = X.reshape(t0.shape[0], -1)
         return R
 
-    def start(self, seed: int = 99, sigma: float = 0.01):
+    def start(self, seed: int = 99, sigma: float = 0.01, x0_entries=None):
         """Loop i starts at phase i T / B with x0 and the initial guess perturbed by sigma N(0,1)
-        (SURVEY 8(d) config 5)."""
+        (SURVEY 8(d) config 5); ``x0_entries`` restricts the x0 perturbation to those state
+        indices (default: all)."""
         B, lay = self.B, self.lay
         self.t0 = np.arange(B) * self.orbit.period / B
         ref = self.reference(self.t0)
         rng = [np.random.default_rng(seed + i) for i in range(B)]
-        x0 = ref[:, lay.x(0)] + sigma * np.stack([r.standard_normal(k3.NX) for r in rng])
+        noise = sigma * np.stack([r.standard_normal(k3.NX) for r in rng])
+        if x0_entries is not None:
+            keep = np.zeros(k3.NX, dtype=bool)
+            keep[np.asarray(x0_entries)] = True
+            noise[:, ~keep] = 0.0
+        x0 = ref[:, lay.x(0)] + noise
         V = ref + sigma * np.stack([r.standard_normal(lay.n_v) for r in rng])
         V[:, :lay.v_intervals] = ref[:, :lay.v_intervals]
+        V[:, self.fict] = 0.0
         P = np.stack([k3.pack_p(lay, self.consts, x0[i], ref[i]) for i in range(B)])
         self.V.copy_(torch.tensor(V))
         self.P.copy_(torch.tensor(P))
@@ -428,6 +439,7 @@ class BatchedRti:
             LU, piv = self._lu(A.view(self.B, n, n))
             Vp[:, self.pl_cols] -= self._solve(LU, piv, r.unsqueeze(-1).contiguous()).squeeze(-1)
         x1 = sum(float(self.D[r_]) * Vp[:, self.x_idx[r_]] for r_ in range(self.lay.d + 1))
+        self.plant_V = Vp                       # interval 0's solved variables (simulated references)
         return x1, res
 
     def _rk4root(self, max_newton=6, tol=1e-11):

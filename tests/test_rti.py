@@ -98,7 +98,7 @@ def test_structured_kkt_matches_dense(cpu_rti):
         K, _ = _dense_kkt(r, ev, b)
         x = np.linalg.solve(K, rhs[b].numpy())
         assert np.abs(x - sol[b].numpy()).max() <= 1e-9 * np.abs(x).max()
-    assert (r.nI, r.L) == (6 + 11 + 1 + 2 * 12 + 12 + 2 * 12, 2 * k3.NX)
+    assert (r.nI, r.L) == (3 + 11 + 1 + 2 * 12 + 12 + 2 * 12, 2 * k3.NX)     # u without f_fict
 
 
 def test_gauss_newton_hessian_is_the_cost_hessian(cpu_rti):
@@ -162,7 +162,7 @@ def test_rti_full_config_256_loops(gpu):
     c = k3.build_constants()
     r = BatchedRti(c, 256, device="cuda")
     r.start()
-    assert (r.nI, r.nS, r.L) == (126, 462, 22)
+    assert (r.nI, r.nS, r.L) == (123, 462, 22)
     for _ in range(3):
         out = r.step()
         torch.cuda.synchronize()
