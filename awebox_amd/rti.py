@@ -222,6 +222,8 @@ class BatchedRti:
         if plant not in ("collocation", "rk4root"):
             raise ValueError(f"unknown plant {plant!r}")
         self.plant, self.n_fe = plant, n_fe
+        self.plant_tol = 1e-9                   # step(): plant_converged = residual <= plant_tol
+        self.sim_blocks = self.sim_xs = None
         # rk4root: the shooting-node rows of interval 0 against (xdot[0], z[0])
         self.rk_rows = t(lay.g_shooting(0))
         self.rk_cols = t(np.concatenate([lay.xdot(0), lay.z(0)]))
@@ -322,10 +324,69 @@ class BatchedRti:
         self.P.copy_(torch.tensor(P))
         self.lam = torch.zeros(B, self.ne, dtype=torch.float64, device=self.dev)
         self.step_count = 0
+        self.sim_blocks = self.sim_xs = None
         self.t0_dev = torch.tensor(self.t0, dtype=torch.float64, device=self.dev)
         self._reference_setup()
         if self.hdiag is None:
             self._hessian_diagonal()
+
+    def simulate_reference(self, n_nodes: int, u_c: torch.Tensor | None = None):
+        """Track a trajectory of the 3-DOF model instead of the synthetic circle.
+
+        The reference's MPC tracks an optimised power cycle, a solution of the model by
+        construction (pmpc.py:__create_reference_interpolator); the circle of
+        kite3.reference_window is not one without the fictitious forces, so a loop tracking it
+        keeps a tracking error of order 1 and never converges.  Here every loop's reference is the
+        plant (interval 0's radau collocation) integrated on the sampling grid for ``n_nodes``
+        sampling times from the circle's state at the loop's phase with the constant control
+        ``u_c`` (default zero rates: CL, roll and reel acceleration hold), so each window
+        (shooting states, collocation states and z, controls) is an exact solution of the MPC's
+        own discretisation.  The current perturbations of x0 and of the initial guess are kept
+        relative to the new windows; ``_shift`` then reads windows of this trajectory."""
+        lay, B = self.lay, self.B
+        nx, st, v0, nk = k3.NX, lay.interval_stride, lay.v_intervals, lay.n_k
+        if n_nodes < nk:
+            raise ValueError("the simulated reference must cover at least one horizon")
+        if u_c is None:
+            u_c = torch.zeros(B, k3.NU, dtype=torch.float64, device=self.dev)
+        ref_old = self.P[:, lay.p_ref:lay.p_ref + lay.n_v].clone()
+        dx0 = self.P[:, lay.p_x0:lay.p_x0 + nx] - ref_old[:, lay.x(0)[0]:lay.x(0)[0] + nx]
+        dV = self.V - ref_old
+        V_save = self.V.clone()
+        blocks = torch.zeros(B, n_nodes, st, dtype=torch.float64, device=self.dev)
+        xs = torch.zeros(B, n_nodes + 1, nx, dtype=torch.float64, device=self.dev)
+        x = ref_old[:, lay.x(0)[0]:lay.x(0)[0] + nx].clone()
+        u0 = self.u0_idx
+        for j in range(n_nodes):
+            self.P[:, lay.p_x0:lay.p_x0 + nx] = x
+            self.V[:, u0] = u_c
+            x1, res = self._plant()
+            if float(res.max()) > 1e-9:
+                raise RuntimeError(f"reference simulation: plant residual {float(res.max()):.2e} at node {j}")
+            blocks[:, j] = self.plant_V[:, v0:v0 + st]
+            xs[:, j] = x
+            self.V[:, v0:v0 + st] = self.plant_V[:, v0:v0 + st]
+            x = x1
+        xs[:, n_nodes] = x
+        self.sim_blocks, self.sim_xs = blocks, xs
+        R = self._reference_sim(0)
+        self.P[:, lay.p_ref:lay.p_ref + lay.n_v] = R
+        self.P[:, lay.p_x0:lay.p_x0 + nx] = R[:, lay.x(0)[0]:lay.x(0)[0] + nx] + dx0
+        self.V.copy_(R + dV)
+        self.V[:, :v0] = V_save[:, :v0]
+        self.V[:, self.fict] = V_save[:, self.fict]
+
+    def _reference_sim(self, s: int) -> torch.Tensor:
+        """Window s (sampling times s .. s + N) of the simulated reference trajectory."""
+        lay = self.lay
+        nx, st, v0, nk = k3.NX, lay.interval_stride, lay.v_intervals, lay.n_k
+        if s + nk > self.sim_blocks.shape[1]:
+            raise ValueError(f"the simulated reference ends before window {s}; simulate more nodes")
+        R = self._ref["base"].repeat(self.B, 1)
+        R[:, v0:v0 + nk * st] = self.sim_blocks[:, s:s + nk].reshape(self.B, nk * st)
+        xN = lay.x(nk)[0]
+        R[:, xN:xN + nx] = self.sim_xs[:, s + nk]
+        return R
 
     def _hessian_diagonal(self):
         """The tracking cost is quadratic and separable: grad(V + h) - grad(V) = h diag(H)."""
@@ -419,6 +480,7 @@ class BatchedRti:
         self.step_count += 1
         x_ref = self.P[:, self.lay.p_ref + self.lay.x(0)[0]:self.lay.p_ref + self.lay.x(0)[0] + k3.NX]
         return {"eq_residual": kkt_res, "path_max": path_max, "plant_residual": plant_res,
+                "plant_converged": plant_res <= self.plant_tol,
                 "tracking_error": (x1 - x_ref).norm(dim=1), "x0": x1, "u0": self.u0}
 
     def _plant(self, max_newton=8, tol=1e-11):
@@ -462,7 +524,7 @@ class BatchedRti:
                 self.ev.eval_nlp_device(Vp, self.P, self.f, self.g, self.grad, self.jac)
                 r = self.g[:, self.rk_rows]
                 res = r.abs().amax(dim=1)
-                if it == max_newton or (it >= 1 and float(res.max()) < tol):
+                if it == max_newton or float(res.max()) < tol:
                     break
                 A = torch.zeros(B, n * n, dtype=torch.float64, device=self.dev)
                 A[:, self.rk_dst] = self.jac[:, self.rk_keep]
@@ -488,5 +550,14 @@ class BatchedRti:
         shifted = torch.cat([body[:, 1:], body[:, -1:]], dim=1).reshape(self.B, nk * st)
         self.V[:, v0:v0 + nk * st] = shifted
         self.P[:, lay.p_x0:lay.p_x0 + k3.NX] = x1
-        self.P[:, lay.p_ref:lay.p_ref + lay.n_v] = self._reference_device(
-            self.t0_dev + (self.step_count + 1) * self.consts.cfg.ts)
+        if self.sim_blocks is not None:
+            R = self._reference_sim(self.step_count + 1)
+            self.P[:, lay.p_ref:lay.p_ref + lay.n_v] = R
+            # the new last interval and x[N]: the reference's (a solution of the dynamics) instead of
+            # a copy of the old last interval
+            tail = slice(v0 + (nk - 1) * st, lay.n_v)
+            self.V[:, tail] = R[:, tail]
+            self.V[:, self.fict] = 0.0
+        else:
+            self.P[:, lay.p_ref:lay.p_ref + lay.n_v] = self._reference_device(
+                self.t0_dev + (self.step_count + 1) * self.consts.cfg.ts)

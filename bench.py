@@ -457,7 +457,8 @@ def rti_block(c, B, dev, dist, world, steps=10, warmup=3):
     from awebox_amd.rti import BatchedRti
 
     r = BatchedRti(c, B, device=str(dev))
-    r.start(seed=99 + dist.get_rank() * B if dist is not None else 99)
+    r.start(seed=99 + dist.get_rank() * B if dist is not None else 99, x0_entries=CONSISTENT_X0)
+    r.simulate_reference(warmup + steps + c.cfg.n_k + 1)
     for _ in range(warmup):
         r.step()
     torch.cuda.synchronize()
@@ -481,7 +482,16 @@ def rti_block(c, B, dev, dist, world, steps=10, warmup=3):
             "kkt_blocks": {"interval": [B * r.nk, r.nI], "separator": [B, r.nS]},
             "plant_residual_max": float(out["plant_residual"].max()),
             "eq_residual_median": float(out["eq_residual"].median()),
+            "tracking_error_median": float(out["tracking_error"].median()),
+            "tracking_error_max": float(out["tracking_error"].max()),
+            "reference": REFERENCE_NOTE,
             "finite": bool(torch.isfinite(r.V).all().item())}
+
+
+CONSISTENT_X0 = (6, 7, 10)     # CL, roll, reel acceleration: x0 noise that keeps the tether invariants
+REFERENCE_NOTE = ("each loop tracks a trajectory of the 3-DOF model (BatchedRti.simulate_reference: the plant "
+                  "integrated from the circle's state at the loop's phase), x0 = reference + 0.01 N(0,1) on CL, "
+                  "roll and reel acceleration")
 
 
 def pmpc_block(c, B, dev, dist, world, steps=3, warmup=1):
@@ -497,6 +507,7 @@ def pmpc_block(c, B, dev, dist, world, steps=3, warmup=1):
 
     r = BatchedPmpc(c, B, device=str(dev))
     r.start(seed=99 + dist.get_rank() * B if dist is not None else 99)
+    r.simulate_reference(warmup + steps + c.cfg.n_k + 1)
     for _ in range(warmup):
         r.step()
     torch.cuda.synchronize()
@@ -523,6 +534,9 @@ def pmpc_block(c, B, dev, dist, world, steps=3, warmup=1):
             "realtime_factor": c.cfg.ts / (el / steps), "solved_fraction": float(ok.mean()),
             "ipm_iterations_median": float(np.median(its)), "ipm_iterations_max": int(its.max()),
             "plant_residual_max": float(out["plant_residual"].max()),
+            "tracking_error_median": float(out["tracking_error"].median()),
+            "tracking_error_max": float(out["tracking_error"].max()),
+            "reference": REFERENCE_NOTE,
             "solver": "batched IPM (mu_init 1e-3, tol 1e-6, 2-iteration homotopy pre-solve), bounds and path "
                       "inequalities, exact Hessian by coloured central differences of the HIP gradient"}
 
