@@ -34,6 +34,7 @@
 #include "../../include/awegpu.h"
 #include "dual_model.hpp"
 #include "dual_tables.hpp"
+#include "dual_hess_tables.hpp"
 
 namespace {
 
@@ -184,29 +185,52 @@ constexpr int kBlock = 256;
 #define ADL_MIN_BLOCKS 2    // __launch_bounds__ minimum waves per SIMD: two workgroups per CU
 #endif
 
+// LDS image of the first-order front (staging, node values, sub-models, model pass), shared by
+// the first-order kernel and the Hessian kernel
 template <int D>
-__global__ __launch_bounds__(kBlock, ADL_MIN_BLOCKS) void dual_interval_kernel(DArgs a) {
+struct FrontLds {
+    static constexpr int NN = D + 1;
+    static constexpr int STRIDE = 2 * ADL_NX + ADL_NU + ADL_NZ + D * (ADL_NX + ADL_NZ);
+    static constexpr int NLOC = ADL_NTHV + 7 + STRIDE + ADL_NX;
+    double vloc[NLOC];                 // theta_v, phi, x[k], u, xdot, z, coll.., x[k+1]
+    double rloc[ADL_NTHV + STRIDE];    // p.ref: theta_v, interval slice
+    double wtr[ADL_NW];                // effective weights (x psi for tracking)
+    double wef[ADL_NW];                // effective weights
+    double wn[NN][128];                // node values (scaled), [126] = phi.gamma
+    double rn[D][ADL_NW];              // reference values at the Radau nodes
+    double gval[NN][kGvalStride];
+    double dumpbuf[kBlock];
+    int8_t colb[2][128];
+    double pre[NN][kPreStride];        // preaccumulated tether drags
+    double atmo[NN][3 * kMaxElements * 4];
+};
+
+// Interval geometry the passes after the front share
+struct FrontGeo {
+    int tfi;          // index of the interval's t_f in theta_v
+    double tf, ihtf;  // t_f(k), n_k / t_f(k)
+    double psi;
+};
+
+// Stages the interval, forms the node values, preaccumulates the tether drags and runs the
+// compressed forward-mode model pass (node tangents into `tang`, node values into s.gval).
+template <int D>
+__device__ __forceinline__ FrontGeo dual_front(const DArgs& a, FrontLds<D>& s, double* tang, int b, int k, int tid) {
     constexpr int NN = D + 1;
     constexpr int NT = kBlock;
-    constexpr int STRIDE = 2 * ADL_NX + ADL_NU + ADL_NZ + D * (ADL_NX + ADL_NZ);
-    constexpr int NLOC = ADL_NTHV + 7 + STRIDE + ADL_NX;
-    __shared__ double vloc[NLOC];               // theta_v, phi, x[k], u, xdot, z, coll.., x[k+1]
-    __shared__ double rloc[ADL_NTHV + STRIDE];  // p.ref: theta_v, interval slice
-    __shared__ double wtr[ADL_NW];              // effective weights (x psi for tracking)
-    __shared__ double wef[ADL_NW];              // effective weights
-    __shared__ double wn[NN][128];              // node values (scaled), [126] = phi.gamma
-    __shared__ double rn[D][ADL_NW];            // reference values at the Radau nodes
-    __shared__ double gval[NN][kGvalStride];
-    __shared__ double obj[D][128];
-    __shared__ double fterm[D][128];
-    __shared__ double dumpbuf[NT];
-    __shared__ int8_t colb[2][128];
-    __shared__ double pre[NN][kPreStride];      // preaccumulated tether drags
-    __shared__ double atmo[NN][3 * kMaxElements * 4];
-    extern __shared__ double tang[];            // [tang_total]
-
-    const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
-    const int tid = threadIdx.x;
+    constexpr int STRIDE = FrontLds<D>::STRIDE;
+    constexpr int NLOC = FrontLds<D>::NLOC;
+    auto& vloc = s.vloc;
+    auto& rloc = s.rloc;
+    auto& wtr = s.wtr;
+    auto& wef = s.wef;
+    auto& wn = s.wn;
+    auto& rn = s.rn;
+    auto& gval = s.gval;
+    auto& dumpbuf = s.dumpbuf;
+    auto& colb = s.colb;
+    auto& pre = s.pre;
+    auto& atmo = s.atmo;
     const double* V = a.V + (size_t)b * a.n_v;
     const double* P = a.P + (size_t)b * a.n_p;
     const int nthv = a.n_thv;
@@ -376,6 +400,37 @@ __global__ __launch_bounds__(kBlock, ADL_MIN_BLOCKS) void dual_interval_kernel(D
         }
     }
     __syncthreads();
+
+    return FrontGeo{tfi, tf, ihtf, psi};
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock, ADL_MIN_BLOCKS) void dual_interval_kernel(DArgs a) {
+    constexpr int NN = D + 1;
+    constexpr int NT = kBlock;
+    constexpr int STRIDE = FrontLds<D>::STRIDE;
+    __shared__ FrontLds<D> s;
+    __shared__ double obj[D][128];
+    __shared__ double fterm[D][128];
+    extern __shared__ double tang[];            // [tang_total]
+    const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
+    const int tid = threadIdx.x;
+    const FrontGeo geo = dual_front<D>(a, s, tang, b, k, tid);
+    auto& wtr = s.wtr;
+    auto& wef = s.wef;
+    auto& wn = s.wn;
+    auto& rn = s.rn;
+    auto& gval = s.gval;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const double* cost = P + a.n_v + ADL_NW;
+    const double* C = a.coll.C;
+    const double tf = geo.tf, ihtf = geo.ihtf, psi = geo.psi;
+    const int base = a.v_int0 + k * STRIDE;
+    const double* xk = s.vloc + ADL_NTHV + 7;
+    const double* coll = xk + ADL_NX + ADL_NU + ADL_NX + ADL_NZ;
+    const double* xk1 = coll + D * (ADL_NX + ADL_NZ);
+    auto Xv = [&](int r, int i) -> double { return r == 0 ? xk[i] : coll[(r - 1) * (ADL_NX + ADL_NZ) + i]; };
 
     // ---- objective: directional derivatives at the Radau nodes (objective.py:45-544) ------
     const double T = time_period(V, a);
@@ -558,6 +613,315 @@ __global__ __launch_bounds__(64) void dual_finalize_kernel(DArgs a) {
     for (int i = lane; i < ADL_NX; i += 64) g[gp + i] = V[x0 + kOrder[i]] - V[xT + kOrder[i]];
 }
 
+// =========================================================================================
+// Hessian of the Lagrangian sigma f + lam^T g (nlp_hess_l), exact (dual_hess_tables.hpp)
+// =========================================================================================
+struct HDArgs {
+    DArgs a;                       // V, P, tables and sizes of the first-order kernel
+    const DHessTabs* ht;
+    const int* tasks;              // colour pairs (c1 | c2 << 8) per node kind
+    const short* task_target;      // [task][kHRowStride] direction-pair index of each row
+    const int* ent_off;            // [n_k + 1]
+    const int* term_off;
+    const unsigned* terms;
+    const int* slot0;
+    const int* nslot;
+    const int* gslot;
+    const int* gcol;
+    const int* grow;
+    const double* sigma;           // [batch]
+    const double* lam;             // [batch][n_g]
+    double* H;                     // [batch][nnz_h] upper-triangular CCS values
+    double* gpart;                 // [batch][n_k][ng] interval partials of the global entries
+    double* apart;                 // [batch][n_k] interval power integrals A_k
+    int hnnz, ng, hd_total;
+};
+
+// hyper-dual node variable i: e1 along colour c1, e2 along colour c2 (DLaneIn twice)
+struct DLaneHIn {
+    const double* w;
+    const int8_t* col;
+    int c1, c2;
+    double cxx, t1, t2;
+    __device__ __forceinline__ awe::HDual operator()(int i) const {
+        double x = (col[i] == c1) ? 1.0 : 0.0;
+        double y = (col[i] == c2) ? 1.0 : 0.0;
+        if (i >= ADL_NX && i < 2 * ADL_NX) {
+            if (col[i - ADL_NX] == c1) x += cxx;
+            if (col[i - ADL_NX] == c2) y += cxx;
+            x += t1 * w[i];
+            y += t2 * w[i];
+        }
+        return awe::HDual(w[i], x, y, 0.0);
+    }
+};
+
+// accumulates mu_r d2F_r/de1de2 into the node's direction-pair Hessian (branch-free); the
+// colouring makes each (task, row) own its pair slot, so no two threads meet
+struct DLaneHSink {
+    double* hd;
+    double* dump;
+    const double* mu;
+    const short* tt;
+    __device__ __forceinline__ void emit(int r, const awe::HDual& v) {
+        const int idx = tt[r];
+        double* adr = idx >= 0 ? hd + idx : dump;
+        *adr += mu[r] * v.ab;
+    }
+    __device__ __forceinline__ void eq_row(int r, const awe::HDual& v) { emit(r, v); }
+    __device__ __forceinline__ void ineq_row(int r, const awe::HDual& v) { emit(ADL_N_EQ + r, v); }
+    __device__ __forceinline__ void power(const awe::HDual& v) { emit(kRowPower, v); }
+    __device__ __forceinline__ void beta(int k, const awe::HDual& v) { emit(kRowBeta0 + k, v); }
+};
+
+constexpr int kGStride = ADL_NX + 2;      // G[n][i] i < 50, [50] = sum_i G 2 xdot_i / tf^2
+
+// dynamic LDS of the Hessian kernel in doubles after the tangent buffer
+template <int D>
+constexpr int hess_dyn_fixed_doubles() {
+    return (D + 1) * kHRowStride + (D + 1) * kGStride + 40 + 2 * D * 128;
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void dual_hess_kernel(HDArgs ha) {
+    const DArgs& a = ha.a;
+    constexpr int NN = D + 1;
+    constexpr int NT = kBlock;
+    __shared__ FrontLds<D> s;
+    extern __shared__ double dyn[];
+    const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
+    const int tid = threadIdx.x;
+    const DHessTabs* ht = ha.ht;
+    const ColorTabs* ct = a.ct;
+    double* tang = dyn;
+    double* hd = tang + a.tang_total;
+    double* mu = hd + ha.hd_total;                 // [NN][kHRowStride]
+    double* G = mu + NN * kHRowStride;             // [NN][kGStride]
+    double* scl = G + NN * kGStride;               // [1 + NN NN]
+    double* tfp = scl + 40;                        // [D][128]
+    double* gtp = tfp + D * 128;                   // [D][128]
+    for (int i = tid; i < ha.hd_total; i += NT) hd[i] = 0.0;
+    const FrontGeo geo = dual_front<D>(a, s, tang, b, k, tid);   // ends with a barrier
+
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const double* cost = P + a.n_v + ADL_NW;
+    const double* th = P + a.n_v + ADL_NW + 20;
+    const double* lam = ha.lam + (size_t)b * a.n_g;
+    const double sigma = ha.sigma[b];
+    const double* C = a.coll.C;
+    const double* wq_all = a.coll.w;
+    const double tf = geo.tf, ihtf = geo.ihtf, psi = geo.psi;
+    const double inv_tf = 1.0 / tf;
+    const double T = time_period(V, a);
+    const double cp = cost[kCostPower];
+    const double cb = cost[kCostBeta] / a.cst[ADL_C_NORM_BETA];
+    const bool ph1 = a.single && k >= a.nkr;
+    const double n_own = a.single ? (ph1 ? (double)(a.n_k - a.nkr) / a.n_k : (double)a.nkr / a.n_k) : 1.0;
+    const double n_oth = a.single ? 1.0 - n_own : 0.0;
+    constexpr int ROWS = ADL_N_EQ + ADL_N_INEQ + D * ADL_N_EQ + ADL_NX;
+    auto toff = [&](int n) { return n == 0 ? 0 : ct->tsize[0] + (n - 1) * ct->tsize[1]; };
+    auto hoff = [&](int n) { return n == 0 ? 0 : ht->npairs[0] + (n - 1) * ht->npairs[1]; };
+
+    // ---- row weights: lam for constraint rows, sigma-scaled objective weights -----------------
+    for (int t = tid; t < NN * kHRowStride; t += NT) {
+        const int n = t / kHRowStride, r = t % kHRowStride;
+        double m = 0.0;
+        if (n == 0) {
+            if (r < kRowPower) m = lam[k * ROWS + r];
+        } else {
+            const double wq = wq_all[n - 1];
+            if (r < ADL_N_EQ) m = lam[k * ROWS + ADL_N_EQ + ADL_N_INEQ + (n - 1) * ADL_N_EQ + r];
+            else if (r == kRowPower) m = sigma * (1.0 - psi) * (-cp) * wq * tf / ((double)a.n_k * T);
+            else if (r == kRowBeta0 || r == kRowBeta0 + 1) m = sigma * 2.0 * wq * cb * s.gval[n][r];
+        }
+        mu[t] = m;
+    }
+    for (int i = tid; i < 1 + NN * NN; i += NT) scl[i] = i == 0 ? 1.0 : C[i - 1] * ihtf;
+    __syncthreads();
+
+    // ---- second-order pass: one (node, colour pair) per thread ---------------------------------
+    const int nt0 = ht->ntask[0], nt1 = ht->ntask[1];
+    for (int t = tid; t < nt0 + D * nt1; t += NT) {
+        const int n = t < nt0 ? 0 : 1 + (t - nt0) / nt1;
+        const int kind = n > 0 ? 1 : 0;
+        const int ti = (kind == 0 ? t : (t - nt0) % nt1) + ht->task_off[kind];
+        const int task = ha.tasks[ti];
+        const int c1 = task & 0xff, c2 = task >> 8;
+        const int ctf = s.colb[1][awe::dl::kTf];
+        DLaneHIn in{s.wn[n], s.colb[kind], c1, c2, n > 0 ? C[n * NN + n] * ihtf : 0.0,
+                    (n > 0 && c1 == ctf) ? -inv_tf : 0.0, (n > 0 && c2 == ctf) ? -inv_tf : 0.0};
+        DLaneHSink sink{hd + hoff(n), &s.dumpbuf[tid], mu + n * kHRowStride, ha.task_target + (size_t)ti * kHRowStride};
+        const int8_t cg = s.colb[kind][awe::dl::kGamma];
+        const awe::HDual gamma(s.wn[n][awe::dl::kGamma], cg == c1 ? 1.0 : 0.0, cg == c2 ? 1.0 : 0.0, 0.0);
+        awe::dual_node<awe::HDual>(in, gamma, th, a.cst, sink, n == 0);
+    }
+    __syncthreads();
+
+    // ---- objective terms in direction space and the xdot(t_f) map terms (Radau nodes) --------
+    for (int t = tid; t < D * 128; t += NT) {
+        const int j = t >> 7, p = t & 127, n = j + 1;
+        const double wq = wq_all[j];
+        const double* w = s.wn[n];
+        const double* rv = s.rn[j];
+        const double cxx = C[n * NN + n] * ihtf;
+        const double* tp = tang + toff(n);
+        double* hn = hd + hoff(n);
+        auto addp = [&](int q1, int q2, double v) { hn[ht->pidx[1][q1][q2]] += sigma * v; };
+        double tfpart = 0.0, gt = 0.0;
+        if (p < ADL_NX) {
+            const double ai = s.wef[p], bi = s.wef[ADL_NX + p], xd = w[ADL_NX + p];
+            addp(p, p, 2.0 * wq * psi * ai + cxx * cxx * 2.0 * wq * bi);
+            addp(p, ADL_NX + p, cxx * 2.0 * wq * bi);
+            addp(p, awe::dl::kTf, cxx * (-xd * inv_tf) * 2.0 * wq * bi);
+            addp(p, kHDirPsi, 2.0 * wq * ai * (w[p] - rv[p]));
+        } else if (p < 2 * ADL_NX) {
+            const int i = p - ADL_NX;
+            const double bi = s.wef[p], xd = w[p];
+            addp(p, p, 2.0 * wq * bi);
+            addp(p, awe::dl::kTf, (-xd * inv_tf) * 2.0 * wq * bi);
+            tfpart = (xd * inv_tf) * (xd * inv_tf) * 2.0 * wq * bi;
+            // gradient of the node Lagrangian w.r.t. xdot_i: rows (first-order tangents) + objective
+            double gi = sigma * wq * 2.0 * bi * xd;
+            const int c = s.colb[1][p];
+            if (c >= 0) {
+                const uint64_t cl = ct->cm_lo[1][c], chh = ct->cm_hi[1][c];
+                const double* tc = tp + ct->off[1][c];
+                for (uint64_t mm = ht->dm_lo[1][p]; mm; mm &= mm - 1ull) {
+                    const int r = __builtin_ctzll(mm);
+                    gi += mu[n * kHRowStride + r] * tc[__popcll(cl & ((1ull << r) - 1ull))];
+                }
+                for (uint64_t mm = ht->dm_hi[1][p]; mm; mm &= mm - 1ull) {
+                    const int r = __builtin_ctzll(mm);
+                    gi += mu[n * kHRowStride + 64 + r] * tc[__popcll(cl) + __popcll(chh & ((1ull << r) - 1ull))];
+                }
+            }
+            G[n * kGStride + i] = gi;
+            gt = gi * 2.0 * xd * inv_tf * inv_tf;
+        } else if (p < 2 * ADL_NX + ADL_NU) {
+            addp(p, p, 2.0 * wq * s.wef[p]);
+        } else if (p < 2 * ADL_NX + ADL_NU + ADL_NZ) {                  // lambda: tracked
+            addp(p, p, 2.0 * wq * psi * s.wef[p]);
+            addp(p, kHDirPsi, 2.0 * wq * s.wef[p] * (w[p] - rv[p]));
+        } else if (p < ADL_NW) {
+            addp(p, p, 2.0 * wq * s.wef[p]);                             // theta (t_f weight is 0)
+        }
+        if (p < kDirs) {
+            const int ip = ct->obj_tang[p][0];
+            if (ip >= 0) {                                               // power cost over the period
+                const double tpv = tp[ip];
+                const double c0 = (-cp) * wq / (double)a.n_k;
+                addp(p, kHDirPsi, -c0 * tf / T * tpv);
+                addp(p, awe::dl::kTf, (1.0 - psi) * c0 * (1.0 / T - tf * n_own / (T * T)) * tpv);
+                if (a.single) addp(p, kHDirTfOther, (1.0 - psi) * c0 * (-tf * n_oth / (T * T)) * tpv);
+            }
+            for (int kk = 0; kk < 2; ++kk) {                             // beta cost: Gauss-Newton part
+                const int ib = ct->obj_tang[p][1 + kk];
+                if (ib < 0) continue;
+                const double bp = 2.0 * cb * wq * tp[ib];
+                for (int q = p; q < kDirs; ++q) {
+                    const int iq = ct->obj_tang[q][1 + kk];
+                    if (iq >= 0) addp(p, q, bp * tp[iq]);
+                }
+            }
+        }
+        tfp[t] = tfpart;
+        gtp[t] = gt;
+    }
+    __syncthreads();
+    if (tid < D) {                                                       // fixed-order reductions
+        const int n = tid + 1;
+        double a1 = 0.0, a2 = 0.0;
+        for (int p = 0; p < 128; ++p) { a1 += tfp[tid * 128 + p]; a2 += gtp[tid * 128 + p]; }
+        hd[hoff(n) + ht->pidx[1][awe::dl::kTf][awe::dl::kTf]] += sigma * a1;
+        G[n * kGStride + ADL_NX] = a2;
+    }
+    if (tid == 64) {                                                     // power integral A_k
+        double A = 0.0;
+        for (int j = 0; j < D; ++j) A += wq_all[j] * s.gval[j + 1][kRowPower] / a.n_k;
+        ha.apart[(size_t)b * a.n_k + k] = A;
+    }
+    __syncthreads();
+
+    // ---- V-space entries: local CCS slots (contiguous) and the global-global partials ---------
+    const int nloc = ha.nslot[k];
+    const int e0 = ha.ent_off[k];
+    const double ctf2 = ihtf * inv_tf;
+    double* Hb = ha.H + (size_t)b * ha.hnnz + ha.slot0[k];
+    double* gp = ha.gpart + ((size_t)b * a.n_k + k) * ha.ng;
+    for (int e = tid; e < nloc + ha.ng; e += NT) {
+        double v = 0.0;
+        for (int t = ha.term_off[e0 + e]; t < ha.term_off[e0 + e + 1]; ++t) {
+            const unsigned term = ha.terms[t];
+            const int type = term >> 30, n = (term >> 27) & 7;
+            if (type == kHTypeA) {
+                v += scl[(term >> 7) & 127] * scl[term & 127] * hd[hoff(n) + ((term >> 14) & 8191)];
+            } else if (type == kHTypeB) {
+                const int i = (term >> 21) & 63, r = (term >> 18) & 7;
+                v += G[n * kGStride + i] * (-C[r * NN + n] * ctf2);
+            } else {
+                v += G[n * kGStride + ADL_NX];
+            }
+        }
+        if (e < nloc) Hb[e] = v;
+        else gp[e - nloc] = v;
+    }
+}
+
+// global-global entries: sum of the interval partials in a fixed order, plus the power cost over
+// the phase-fixed period and the time cost, which couple the t_f globals (objective.py,
+// ocp_outputs.py:118-140): with E = sum_k tf_k A_k, T = n0 tf0 + n1 tf1,
+//   f_p = -c_p E / T,  d2(E/T)/dtf_i dtf_j = -(A_i n_j + A_j n_i) / T^2 + 2 E n_i n_j / T^3
+__global__ __launch_bounds__(64) void dual_hess_finalize_kernel(HDArgs ha) {
+    const DArgs& a = ha.a;
+    const int b = blockIdx.x;
+    const int g = threadIdx.x;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* cost = a.P + (size_t)b * a.n_p + a.n_v + ADL_NW;
+    for (int q = g; q < ha.ng; q += 64) {
+        double v = 0.0;
+        for (int k = 0; k < a.n_k; ++k) v += ha.gpart[((size_t)b * a.n_k + k) * ha.ng + q];
+        const int col = ha.gcol[q], row = ha.grow[q];
+        const int ntf = a.single ? 2 : 1;
+        const bool tf_row = row >= 1 && row <= ntf;
+        const bool tf_col = col >= 1 && col <= ntf;
+        const bool psi_col = col == a.n_thv + kPhiPsi;
+        if (tf_row && (tf_col || psi_col)) {
+            double A[2] = {0.0, 0.0}, E = 0.0;
+            for (int k = 0; k < a.n_k; ++k) {
+                const int ph = (a.single && k >= a.nkr) ? 1 : 0;
+                const double Ak = ha.apart[(size_t)b * a.n_k + k];
+                A[ph] += Ak;
+                E += V[1 + ph] * Ak;
+            }
+            const double nn[2] = {a.single ? (double)a.nkr / a.n_k : 1.0,
+                                  a.single ? (double)(a.n_k - a.nkr) / a.n_k : 0.0};
+            const double T = time_period(V, a);
+            const double psi = V[a.n_thv + kPhiPsi];
+            const double cp = cost[kCostPower], ct = cost[kCostTf];
+            const double sigma = ha.sigma[b];
+            const int i = row - 1;
+            if (tf_col) {
+                const int j = col - 1;
+                const double d2 = -(A[i] * nn[j] + A[j] * nn[i]) / (T * T) + 2.0 * E * nn[i] * nn[j] / (T * T * T);
+                v += sigma * ((1.0 - psi) * (-cp) * d2 + 2.0 * ct * nn[i] * nn[j]);
+            } else {
+                v += sigma * cp * (A[i] / T - E * nn[i] / (T * T));
+            }
+        }
+        ha.H[(size_t)b * ha.hnnz + ha.gslot[q]] = v;
+    }
+}
+
+template <int D>
+int launch_hess(const HDArgs& ha, int batch, size_t dyn, hipStream_t s) {
+    // the LDS image (tangents + direction-pair Hessian) exceeds 64 KiB: raise the dynamic limit
+    ADL_TRY(hipFuncSetAttribute((const void*)dual_hess_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+    dual_hess_kernel<D><<<dim3((unsigned)(batch * ha.a.n_k)), kBlock, dyn, s>>>(ha);
+    return 0;
+}
+
 template <int D>
 int launch(const DArgs& a, int batch, size_t dyn, hipStream_t s) {
     dual_interval_kernel<D><<<dim3((unsigned)(batch * a.n_k)), kBlock, dyn, s>>>(a);
@@ -579,7 +943,115 @@ struct adl_handle_s {
     double *d_V = nullptr, *d_P = nullptr, *d_f = nullptr, *d_g = nullptr, *d_grad = nullptr, *d_jac = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool timed = false;
+    // Hessian (built on first use)
+    DualHessTables* ht = nullptr;
+    DHessTabs* d_ht = nullptr;
+    int *d_tasks = nullptr, *d_ent_off = nullptr, *d_term_off = nullptr, *d_slot0 = nullptr, *d_nslot = nullptr;
+    int *d_hgslot = nullptr, *d_gcol = nullptr, *d_grow = nullptr;
+    short* d_task_target = nullptr;
+    unsigned* d_terms = nullptr;
+    double *d_gpart = nullptr, *d_apart = nullptr;
+    double *d_hV = nullptr, *d_hP = nullptr, *d_sigma = nullptr, *d_lam = nullptr, *d_H = nullptr;   // host-entry scratch
+    int hd_total = 0;
+    size_t hess_dyn = 0;
+    hipEvent_t hev[2] = {nullptr, nullptr};
+    bool htimed = false;
 };
+
+static DArgs make_args(adl_handle h, const double* V, const double* P) {
+    const Tables& T = h->t;
+    const Layout& L = T.lay;
+    DArgs a{};
+    a.V = V; a.P = P; a.cst = h->d_cst;
+    for (int j = 0; j <= L.d; ++j) {
+        for (int r = 0; r <= L.d; ++r) a.coll.C[j * (L.d + 1) + r] = T.coll.C[j][r];
+        a.coll.D[j] = T.coll.D[j];
+    }
+    for (int j = 0; j < L.d; ++j) a.coll.w[j] = T.coll.w[j];
+    a.ct = h->d_ct; a.goff = h->d_goff; a.gslot = h->d_gslot; a.gcode = h->d_gcode;
+    for (size_t q = 0; q < T.kconst.size(); ++q) a.kconst[q] = T.kconst[q];
+    a.part = h->d_part;
+    a.n_k = L.n_k; a.d = L.d; a.n_v = L.n_v; a.n_g = L.n_g; a.n_p = L.n_p; a.nnz = (int)T.row.size();
+    a.stride = L.stride; a.v_int0 = L.v_int0; a.nkr = L.nk_reelout; a.single = L.single; a.n_thv = L.n_thv;
+    a.tang_total = T.tang_total;
+    return a;
+}
+
+static size_t hess_dyn_fixed(int d) {
+    switch (d) {
+        case 2: return hess_dyn_fixed_doubles<2>();
+        case 3: return hess_dyn_fixed_doubles<3>();
+        case 4: return hess_dyn_fixed_doubles<4>();
+        default: return hess_dyn_fixed_doubles<5>();
+    }
+}
+
+// builds and uploads the Hessian tables on first use
+static int ensure_hess(adl_handle h) {
+    if (h->ht) return AWE_OK;
+    auto* H = new DualHessTables();
+    std::string err;
+    if (build_dual_hess_tables(h->t, h->consts.data(), *H, err)) {
+        delete H;
+        return fail(AWE_ERR_ARG, err);
+    }
+    const Tables& T = h->t;
+    h->hd_total = H->ht.npairs[0] + T.lay.d * H->ht.npairs[1];
+    h->hess_dyn = sizeof(double) * ((size_t)T.tang_total + h->hd_total + hess_dyn_fixed(T.lay.d));
+    if (h->hess_dyn > 110 * 1024) {
+        delete H;
+        return fail(AWE_ERR_ARG, "internal: Hessian LDS image exceeds the workgroup budget");
+    }
+    h->ht = H;
+    const size_t nb = (size_t)h->batch, ng = H->gslot.size();
+#define ADL_UPLOAD(dst, src, n)                                                      \
+    ADL_TRY(hipMalloc((void**)&dst, sizeof(*dst) * (n)));                            \
+    ADL_TRY(hipMemcpy(dst, src, sizeof(*dst) * (n), hipMemcpyHostToDevice));
+    ADL_UPLOAD(h->d_ht, &H->ht, 1);
+    ADL_UPLOAD(h->d_tasks, H->tasks.data(), H->tasks.size());
+    ADL_UPLOAD(h->d_task_target, H->task_target.data(), H->task_target.size());
+    ADL_UPLOAD(h->d_ent_off, H->ent_off.data(), H->ent_off.size());
+    ADL_UPLOAD(h->d_term_off, H->term_off.data(), H->term_off.size());
+    ADL_UPLOAD(h->d_terms, H->terms.data(), H->terms.size());
+    ADL_UPLOAD(h->d_slot0, H->slot0.data(), H->slot0.size());
+    ADL_UPLOAD(h->d_nslot, H->nslot.data(), H->nslot.size());
+    ADL_UPLOAD(h->d_hgslot, H->gslot.data(), ng);
+    ADL_UPLOAD(h->d_gcol, H->gcol.data(), ng);
+    ADL_UPLOAD(h->d_grow, H->grow.data(), ng);
+#undef ADL_UPLOAD
+    ADL_TRY(hipMalloc((void**)&h->d_gpart, sizeof(double) * nb * T.lay.n_k * std::max<size_t>(ng, 1)));
+    ADL_TRY(hipMalloc((void**)&h->d_apart, sizeof(double) * nb * T.lay.n_k));
+    for (auto& e : h->hev) ADL_TRY(hipEventCreate(&e));
+    return AWE_OK;
+}
+
+static int launch_hess_all(adl_handle h, const double* V, const double* P, const double* sigma, const double* lam,
+                           double* Hv, hipStream_t s) {
+    const DualHessTables& H = *h->ht;
+    HDArgs ha{};
+    ha.a = make_args(h, V, P);
+    ha.ht = h->d_ht; ha.tasks = h->d_tasks; ha.task_target = h->d_task_target;
+    ha.ent_off = h->d_ent_off; ha.term_off = h->d_term_off; ha.terms = h->d_terms;
+    ha.slot0 = h->d_slot0; ha.nslot = h->d_nslot; ha.gslot = h->d_hgslot; ha.gcol = h->d_gcol; ha.grow = h->d_grow;
+    ha.sigma = sigma; ha.lam = lam; ha.H = Hv; ha.gpart = h->d_gpart; ha.apart = h->d_apart;
+    ha.hnnz = H.nnz; ha.ng = (int)H.gslot.size(); ha.hd_total = h->hd_total;
+    int rc = 0;
+    ADL_TRY(hipEventRecord(h->hev[0], s));
+    switch (h->t.lay.d) {
+        case 2: rc = launch_hess<2>(ha, h->batch, h->hess_dyn, s); break;
+        case 3: rc = launch_hess<3>(ha, h->batch, h->hess_dyn, s); break;
+        case 4: rc = launch_hess<4>(ha, h->batch, h->hess_dyn, s); break;
+        case 5: rc = launch_hess<5>(ha, h->batch, h->hess_dyn, s); break;
+        default: return fail(AWE_ERR_ARG, "unsupported d");
+    }
+    if (rc) return rc;
+    ADL_TRY(hipGetLastError());
+    dual_hess_finalize_kernel<<<dim3((unsigned)h->batch), 64, 0, s>>>(ha);
+    ADL_TRY(hipGetLastError());
+    ADL_TRY(hipEventRecord(h->hev[1], s));
+    h->htimed = true;
+    return AWE_OK;
+}
 
 extern "C" {
 
@@ -683,11 +1155,17 @@ int adl_create(int n_k, int d, const double* consts, int n_consts, int batch, ad
 int adl_destroy(adl_handle h) {
     if (!h) return AWE_OK;
     void* bufs[] = {h->d_cst, h->d_ct, h->d_goff, h->d_gslot, h->d_gcode, h->d_part,
-                    h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac};
+                    h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac,
+                    h->d_ht, h->d_tasks, h->d_ent_off, h->d_term_off, h->d_slot0, h->d_nslot, h->d_hgslot,
+                    h->d_gcol, h->d_grow, h->d_task_target, h->d_terms, h->d_gpart, h->d_apart,
+                    h->d_hV, h->d_hP, h->d_sigma, h->d_lam, h->d_H};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : h->hev)
+        if (e) (void)hipEventDestroy(e);
+    delete h->ht;
     delete h;
     return AWE_OK;
 }
@@ -714,19 +1192,8 @@ int adl_eval_nlp(adl_handle h, const double* V, const double* P, double* f, doub
     const Tables& T = h->t;
     const Layout& L = T.lay;
     hipStream_t s = (hipStream_t)stream;
-    DArgs a{};
-    a.V = V; a.P = P; a.cst = h->d_cst;
-    for (int j = 0; j <= L.d; ++j) {
-        for (int r = 0; r <= L.d; ++r) a.coll.C[j * (L.d + 1) + r] = T.coll.C[j][r];
-        a.coll.D[j] = T.coll.D[j];
-    }
-    for (int j = 0; j < L.d; ++j) a.coll.w[j] = T.coll.w[j];
-    a.ct = h->d_ct; a.goff = h->d_goff; a.gslot = h->d_gslot; a.gcode = h->d_gcode;
-    for (size_t q = 0; q < T.kconst.size(); ++q) a.kconst[q] = T.kconst[q];
-    a.f = f; a.g = g; a.grad = grad_f; a.jac = jac; a.part = h->d_part;
-    a.n_k = L.n_k; a.d = L.d; a.n_v = L.n_v; a.n_g = L.n_g; a.n_p = L.n_p; a.nnz = (int)T.row.size();
-    a.stride = L.stride; a.v_int0 = L.v_int0; a.nkr = L.nk_reelout; a.single = L.single; a.n_thv = L.n_thv;
-    a.tang_total = T.tang_total;
+    DArgs a = make_args(h, V, P);
+    a.f = f; a.g = g; a.grad = grad_f; a.jac = jac;
     const size_t dyn = sizeof(double) * (size_t)T.tang_total;
     ADL_TRY(hipEventRecord(h->ev[0], s));
     switch (L.d) {
@@ -782,6 +1249,82 @@ int adl_eval_nlp_host(adl_handle h, const double* V, const double* P, double* f,
     };
     if (!finite(f, nb) || !finite(g, nb * L.n_g) || !finite(grad_f, nb * L.n_v) || !finite(jac, nb * nnz))
         return fail(AWE_ERR_NONFINITE, "non-finite output");
+    return AWE_OK;
+}
+
+int adl_hess_nnz(adl_handle h, int* nnz_h) {
+    if (!h || !nnz_h) return fail(AWE_ERR_ARG, "null argument");
+    int rc = ensure_hess(h);
+    if (rc) return rc;
+    *nnz_h = h->ht->nnz;
+    return AWE_OK;
+}
+
+int adl_sparsity_hess(adl_handle h, int* colind, int* row) {
+    if (!h || !colind || !row) return fail(AWE_ERR_ARG, "null argument");
+    int rc = ensure_hess(h);
+    if (rc) return rc;
+    std::memcpy(colind, h->ht->colind.data(), sizeof(int) * h->ht->colind.size());
+    std::memcpy(row, h->ht->row.data(), sizeof(int) * h->ht->row.size());
+    return AWE_OK;
+}
+
+int adl_sparsity_hess_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind, int* row) {
+    if (!consts || !nnz) return fail(AWE_ERR_ARG, "null argument");
+    Tables T;
+    std::string err;
+    if (build_tables(n_k, d, consts, n_consts, T, err)) return fail(AWE_ERR_ARG, err);
+    auto* H = new DualHessTables();
+    if (build_dual_hess_tables(T, consts, *H, err)) {
+        delete H;
+        return fail(AWE_ERR_ARG, err);
+    }
+    *nnz = H->nnz;
+    if (colind) std::memcpy(colind, H->colind.data(), sizeof(int) * H->colind.size());
+    if (row) std::memcpy(row, H->row.data(), sizeof(int) * H->row.size());
+    delete H;
+    return AWE_OK;
+}
+
+int adl_eval_hess(adl_handle h, const double* V, const double* P, const double* sigma, const double* lam_g,
+                  double* H, void* stream) {
+    if (!h || !V || !P || !sigma || !lam_g || !H) return fail(AWE_ERR_ARG, "null argument");
+    int rc = ensure_hess(h);
+    if (rc) return rc;
+    return launch_hess_all(h, V, P, sigma, lam_g, H, (hipStream_t)stream);
+}
+
+int adl_eval_hess_host(adl_handle h, const double* V, const double* P, const double* sigma, const double* lam_g,
+                       double* H) {
+    if (!h || !V || !P || !sigma || !lam_g || !H) return fail(AWE_ERR_ARG, "null argument");
+    int rc = ensure_hess(h);
+    if (rc) return rc;
+    const Layout& L = h->t.lay;
+    const size_t nb = (size_t)h->batch, hn = (size_t)h->ht->nnz;
+    if (!h->d_H) {
+        ADL_TRY(hipMalloc((void**)&h->d_hV, sizeof(double) * nb * L.n_v));
+        ADL_TRY(hipMalloc((void**)&h->d_hP, sizeof(double) * nb * L.n_p));
+        ADL_TRY(hipMalloc((void**)&h->d_sigma, sizeof(double) * nb));
+        ADL_TRY(hipMalloc((void**)&h->d_lam, sizeof(double) * nb * L.n_g));
+        ADL_TRY(hipMalloc((void**)&h->d_H, sizeof(double) * nb * hn));
+    }
+    ADL_TRY(hipMemcpy(h->d_hV, V, sizeof(double) * nb * L.n_v, hipMemcpyHostToDevice));
+    ADL_TRY(hipMemcpy(h->d_hP, P, sizeof(double) * nb * L.n_p, hipMemcpyHostToDevice));
+    ADL_TRY(hipMemcpy(h->d_sigma, sigma, sizeof(double) * nb, hipMemcpyHostToDevice));
+    ADL_TRY(hipMemcpy(h->d_lam, lam_g, sizeof(double) * nb * L.n_g, hipMemcpyHostToDevice));
+    rc = launch_hess_all(h, h->d_hV, h->d_hP, h->d_sigma, h->d_lam, h->d_H, nullptr);
+    if (rc) return rc;
+    ADL_TRY(hipDeviceSynchronize());
+    ADL_TRY(hipMemcpy(H, h->d_H, sizeof(double) * nb * hn, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nb * hn; ++i)
+        if (!std::isfinite(H[i])) return fail(AWE_ERR_NONFINITE, "non-finite value in the Hessian");
+    return AWE_OK;
+}
+
+int adl_last_hess_ms(adl_handle h, float* ms) {
+    if (!h || !h->htimed || !ms) return fail(AWE_ERR_ARG, "no timed Hessian launch yet");
+    ADL_TRY(hipEventSynchronize(h->hev[1]));
+    ADL_TRY(hipEventElapsedTime(ms, h->hev[0], h->hev[1]));
     return AWE_OK;
 }
 

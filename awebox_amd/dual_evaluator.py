@@ -1,6 +1,6 @@
 """ctypes binding of ``libawedual.so`` (include/awedual.h): the multi-kite NLP oracle surface.
 
-``DualEvaluator`` serves ``nlp_f`` / ``nlp_g`` / ``nlp_grad_f`` / ``nlp_jac_g`` for the dual-kite
+``DualEvaluator`` serves ``nlp_f`` / ``nlp_g`` / ``nlp_grad_f`` / ``nlp_jac_g`` / ``nlp_hess_l`` for the dual-kite
 power-cycle NLP (config 3) with CasADi's argument meaning (x = V, p = P) and J_g in CCS
 (awebox/opti/preparation.py:366-400), plus the batched device-pointer path used by the sweep
 driver and ``bench.py``.  No CPU fallback: a missing library or device raises
@@ -21,7 +21,8 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libawedual
 
 EXPORTED_SYMBOLS = ["adl_create", "adl_destroy", "adl_last_error", "adl_sizes", "adl_sparsity_jac",
                     "adl_sparsity_jac_static", "adl_colour_counts", "adl_eval_nlp", "adl_eval_nlp_host",
-                    "adl_last_kernel_ms", "adl_node_eval_host"]
+                    "adl_last_kernel_ms", "adl_node_eval_host", "adl_hess_nnz", "adl_sparsity_hess",
+                    "adl_sparsity_hess_static", "adl_eval_hess", "adl_eval_hess_host", "adl_last_hess_ms"]
 
 
 def load_library(path: str = _LIB_PATH):
@@ -45,6 +46,12 @@ def load_library(path: str = _LIB_PATH):
     lib.adl_eval_nlp_host.argtypes = [h, dp, dp, dp, dp, dp, dp]
     lib.adl_last_kernel_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.adl_node_eval_host.argtypes = [dp, dp, dp, ctypes.c_int, dp, dp]
+    lib.adl_hess_nnz.argtypes = [h, ip]
+    lib.adl_sparsity_hess.argtypes = [h, ip, ip]
+    lib.adl_sparsity_hess_static.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip]
+    lib.adl_eval_hess.argtypes = [h] + [ctypes.c_void_p] * 6
+    lib.adl_eval_hess_host.argtypes = [h, dp, dp, dp, dp, dp]
+    lib.adl_last_hess_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float)]
     _LIB = lib
     return lib
 
@@ -67,6 +74,24 @@ def sparsity_jac_static(consts: du.MultiConstants):
     row = np.zeros(nnz.value, dtype=np.int32)
     if lib.adl_sparsity_jac_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
                                    colind.ctypes.data_as(ip), row.ctypes.data_as(ip)) != AWE_OK:
+        raise AwegpuError(_err(lib))
+    return colind, row
+
+
+def sparsity_hess_static(consts: du.MultiConstants):
+    """Upper-triangular CCS pattern (colind, row) of nlp_hess_l derived on the CPU."""
+    lib = load_library()
+    cfg = consts.cfg
+    c = np.ascontiguousarray(consts.consts, dtype=np.float64)
+    nnz = ctypes.c_int()
+    ip = ctypes.POINTER(ctypes.c_int)
+    if lib.adl_sparsity_hess_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz), None, None) != AWE_OK:
+        raise AwegpuError(_err(lib))
+    lay = du.layout_for(consts)
+    colind = np.zeros(lay.n_v + 1, dtype=np.int32)
+    row = np.zeros(nnz.value, dtype=np.int32)
+    if lib.adl_sparsity_hess_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
+                                    colind.ctypes.data_as(ip), row.ctypes.data_as(ip)) != AWE_OK:
         raise AwegpuError(_err(lib))
     return colind, row
 
@@ -189,3 +214,62 @@ class DualEvaluator:
     def nlp_jac_g(self, x, p):
         out = self._single(x, p)
         return out["g"][0], self.jac_csc(out["jac"][0])
+
+    # ---- Hessian of the Lagrangian (exact, dual_hess_kernel) ----------------------------
+    @property
+    def nnz_h(self):
+        if not hasattr(self, "_hrow"):
+            hn = ctypes.c_int()
+            self._check(self._lib.adl_hess_nnz(self._h, ctypes.byref(hn)))
+            self._hcolind = np.zeros(self.n_v + 1, dtype=np.int32)
+            self._hrow = np.zeros(hn.value, dtype=np.int32)
+            ip = ctypes.POINTER(ctypes.c_int)
+            self._check(self._lib.adl_sparsity_hess(self._h, self._hcolind.ctypes.data_as(ip),
+                                                    self._hrow.ctypes.data_as(ip)))
+        return len(self._hrow)
+
+    def sparsity_hess(self):
+        """Upper-triangular CCS pattern of nlp_hess_l: (colind[n_v+1], row[nnz_h])."""
+        self.nnz_h
+        return self._hcolind.copy(), self._hrow.copy()
+
+    def hess_csc(self, values, full=True):
+        """scipy CSC of the Hessian values (full symmetric matrix unless ``full`` is False)."""
+        import scipy.sparse as sp
+        colind, row = self.sparsity_hess()
+        U = sp.csc_matrix((np.asarray(values), row, colind), shape=(self.n_v, self.n_v))
+        if not full:
+            return U
+        return (U + U.T - sp.diags(U.diagonal())).tocsc()
+
+    def eval_hess_device(self, V, P, sigma, lam_g, H, stream=None):
+        """Upper-triangular CCS values of sigma f + lam_g^T g for every instance: contiguous float64
+        CUDA tensors V [B, n_v], P [B, n_p], sigma [B], lam_g [B, n_g], H [B, nnz_h]."""
+        import torch
+        for t, n in ((V, self.n_v), (P, self.n_p), (sigma, 1), (lam_g, self.n_g), (H, self.nnz_h)):
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
+                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.adl_eval_hess(self._h, V.data_ptr(), P.data_ptr(), sigma.data_ptr(),
+                                            lam_g.data_ptr(), H.data_ptr(), ctypes.c_void_p(s)))
+
+    def eval_hess(self, V, P, sigma, lam_g):
+        V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))
+        P = np.ascontiguousarray(np.asarray(P, dtype=np.float64).reshape(self.batch, self.n_p))
+        sig = np.ascontiguousarray(np.broadcast_to(np.asarray(sigma, dtype=np.float64), (self.batch,)))
+        lam = np.ascontiguousarray(np.asarray(lam_g, dtype=np.float64).reshape(self.batch, self.n_g))
+        H = np.zeros((self.batch, self.nnz_h))
+        self._check(self._lib.adl_eval_hess_host(self._h, _dptr(V), _dptr(P), _dptr(sig), _dptr(lam), _dptr(H)))
+        return H
+
+    def nlp_hess_l(self, x, p, lam_f, lam_g):
+        """CasADi nlp_hess_l: Hessian of lam_f f + lam_g^T g (upper triangle, CCS values)."""
+        if self.batch != 1:
+            raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
+        return self.eval_hess(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1), lam_f,
+                              np.asarray(lam_g).reshape(1, -1))[0]
+
+    def last_hess_ms(self):
+        a = ctypes.c_float()
+        self._check(self._lib.adl_last_hess_ms(self._h, ctypes.byref(a)))
+        return a.value

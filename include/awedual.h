@@ -12,6 +12,10 @@
  *
  *   adl_eval_nlp     <->  nlp_grad_f + nlp_jac_g fused (f, g, grad f, J_g values)
  *   adl_sparsity_jac <->  Sparsity of nlp_jac_g's output (CCS: colind[n_v+1], row[nnz])
+ *   adl_eval_hess     <->  nlp_hess_l  (exact Hessian of sigma f + lam_g^T g, upper triangle;
+ *                          IPOPT's hessian_approximation 'exact', opts/default.py:323,
+ *                          opti/preparation.py:272-273)
+ *   adl_sparsity_hess <->  Sparsity of nlp_hess_l's output (upper-triangular CCS)
  *
  * Memory: V[b*n_v + i], P[b*n_p + i], g[b*n_g + i], grad_f[b*n_v + i], jac[b*nnz + i], f[b] are
  * device pointers for adl_eval_nlp and host pointers for adl_eval_nlp_host.  Return codes as in
@@ -101,6 +105,23 @@ int adl_eval_nlp_host(adl_handle h, const double* V, const double* P, double* f,
                       double* jac);
 /* Kernel time of the last adl_eval_nlp (HIP events), milliseconds. */
 int adl_last_kernel_ms(adl_handle h, float* ms_main, float* ms_finalize);
+
+/* Hessian of the Lagrangian sigma f + lam_g^T g (nlp_hess_l): values of its upper triangle
+ * (row <= col) in the fixed CCS pattern of adl_sparsity_hess; sigma[b] and lam_g[b*n_g + i] per
+ * instance (device pointers for adl_eval_hess, host pointers for adl_eval_hess_host).  The
+ * structure and launch tables are derived on the first Hessian call. */
+int adl_hess_nnz(adl_handle h, int* nnz_h);
+int adl_sparsity_hess(adl_handle h, int* colind, int* row);
+int adl_sparsity_hess_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind, int* row);
+int adl_eval_hess(adl_handle h, const double* V, const double* P, const double* sigma, const double* lam_g,
+                  double* H, void* stream);
+int adl_eval_hess_host(adl_handle h, const double* V, const double* P, const double* sigma, const double* lam_g,
+                       double* H);
+/* Kernel time (interval + finalize kernels) of the last adl_eval_hess call, milliseconds. */
+int adl_last_hess_ms(adl_handle h, float* ms);
+/* Diagnostics (CPU): value [75] and Jacobian [75 x 127] of one node of the model source. */
+int adl_node_eval_host(const double* w, const double* th, const double* consts, int n_consts, double* val,
+                       double* jac);
 
 #ifdef __cplusplus
 }

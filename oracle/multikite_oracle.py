@@ -576,6 +576,30 @@ class MultiKiteOracle:
         V = torch.as_tensor(V)
         return grad(lambda v: self.nlp_f(v, P, lay, th, cost_names, phi_names))(V)
 
+    def nlp_hess_l(self, V, P, sigma, lam_g, lay, th, cost_names, phi_names):
+        """Hessian of sigma f + lam_g^T g (nlp_hess_l) as a full symmetric scipy CSC matrix (test
+        sizes only).  The continuity, periodicity and t_f rows are linear; every other g row lives
+        in one interval, so lam^T g contributes per-interval blocks (torch.func hessian of
+        lam_k^T interval_rows); the objective couples the intervals through the phase-fixed
+        period, so its Hessian is taken densely (forward over reverse of nlp_f)."""
+        import scipy.sparse as sp
+        from torch.func import hessian
+        V = torch.as_tensor(V)
+        lam_g = torch.as_tensor(lam_g)
+        idx = np.stack([lay.local_index(k) for k in range(self.n_k)])
+        R = lay.rows_per_interval
+        lam_k = lam_g[:self.n_k * R].reshape(self.n_k, R)
+        Hk = vmap(hessian(lambda wl, ph, lk: lk @ self.interval_rows(wl, ph, th)), in_dims=(0, 0, 0))(
+            V[torch.as_tensor(idx)], self._phases(), lam_k).numpy()
+        n = lay.n_v
+        rows = np.repeat(idx[:, :, None], idx.shape[1], axis=2)
+        cols = np.repeat(idx[:, None, :], idx.shape[1], axis=1)
+        H = sp.csc_matrix((Hk.ravel(), (rows.ravel(), cols.ravel())), shape=(n, n))
+        Hf = jacfwd(grad(lambda v: self.nlp_f(v, P, lay, th, cost_names, phi_names)))(V).numpy()
+        H = (H + sp.csc_matrix(float(sigma) * Hf)).tocsc()
+        H.eliminate_zeros()
+        return H
+
 
 def from_constants(mc, lay):
     """Build the oracle from an ``awebox_amd.dual.MultiConstants`` (inputs only)."""

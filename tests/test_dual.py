@@ -210,3 +210,21 @@ def test_cpu_port_matches_oracle(n_k, d, member):
     _close(out["g"][0], o.nlp_g(V, P, lay, th).numpy(), "g")
     _close(out["grad_f"][0], o.nlp_grad_f(V, P, lay, th, pb.COST_NAMES, pb.PHI_NAMES).numpy(), "grad_f")
     _close_jac(port.jac_csc(out["jac"][0]), o.nlp_jac_g(V, P, lay, th))
+
+
+def test_dual_hessian_pattern_covers_the_oracle():
+    """CPU (library tables only): the exact-Hessian CCS pattern of the dual-kite NLP contains every
+    nonzero of the oracle's Hessian in the committed fixture (tests/golden/dual_hess_n3_d2.npz)."""
+    import os
+    import scipy.sparse as sp
+    from awebox_amd import dual_evaluator as de
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "dual_hess_n3_d2.npz"))
+    mc = du.build_constants(du.MultiConfig(n_k=int(z["n_k"]), d=int(z["d"])))
+    lay = du.layout_for(mc)
+    ci, ri = de.sparsity_hess_static(mc)
+    assert ci[-1] == len(ri) and np.all(np.diff(ci) >= 0)
+    assert np.all(ri <= np.repeat(np.arange(lay.n_v), np.diff(ci)))          # upper triangle
+    pat = sp.csc_matrix((np.ones(len(ri)), ri, ci), shape=(lay.n_v, lay.n_v))
+    U = sp.csc_matrix((z["H_data"], z["H_indices"], z["H_indptr"]), shape=(lay.n_v, lay.n_v))
+    outside = abs(U) - abs(U).multiply(pat != 0)
+    assert outside.nnz == 0 or outside.max() <= 1e-12 * abs(U).max()
