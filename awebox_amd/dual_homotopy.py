@@ -194,12 +194,17 @@ def outputs(mc: du.MultiConstants, lay: du.MultiLayout, V: np.ndarray) -> dict:
     return {"avg_power_W": energy / T, "period_s": T, "energy_J": energy, "t_f": [t0, t1]}
 
 
-def make_evaluator(mc: du.MultiConstants, device="cuda", batch: int = 1):
-    """Dual-kite evaluator of `batch` instances with the coloured central-difference Hessian
-    (fd_hessian.py)."""
+def make_evaluator(mc: du.MultiConstants, device="cuda", batch: int = 1, hessian: str = "exact"):
+    """Dual-kite evaluator of `batch` instances.  ``hessian='exact'`` (IPOPT's default,
+    opts/default.py:323): nlp_hess_l from the hyper-dual kernel (awedual.hip, dual_hess_kernel);
+    ``'fd'``: coloured central differences of the exact HIP gradient (fd_hessian.py)."""
     from .dual_evaluator import DualEvaluator
-    from .fd_hessian import FdHessian
     ev = DualEvaluator(mc, batch=batch)
+    if hessian == "exact":
+        return ev
+    if hessian != "fd":
+        raise ValueError(f"unknown Hessian mode {hessian!r}")
+    from .fd_hessian import FdHessian
     return FdHessian(ev, lambda B: DualEvaluator(mc, batch=B), ev.layout, device=device)
 
 
