@@ -95,8 +95,15 @@ struct LaneIn {
     unsigned int seedXD;
     double cxx;                  // C[jj][jj] / (h tf) at a Radau node, 0 at the shooting node
     double tfs;                  // -1/tf for the t_f colour at a Radau node, else 0
+    // seed bit -> 0.0 / 1.0 by a bit-field extract and one conversion (i is a compile-time
+    // constant after inlining) instead of a 64-bit test and two selects per input read: -1 % kernel
+    // time at B = 2048 (tools/ap2_variants.py, profiles/r02/ap2_variants.log); the same form on the
+    // xdot seeds measured slower (register spills)
+    __device__ __forceinline__ static double bit(unsigned long long m, int i) {
+        return (double)(unsigned)((m >> i) & 1ull);
+    }
     __device__ __forceinline__ awe::Dual operator()(int i) const {
-        double t = ((seedA >> i) & 1ull) ? 1.0 : 0.0;
+        double t = bit(seedA, i);
         if (i >= AWE_NX && i < 2 * AWE_NX) {
             const int j = i - AWE_NX;
             if ((seedA >> j) & 1ull) t += cxx;

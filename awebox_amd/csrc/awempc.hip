@@ -61,15 +61,15 @@ struct MArgs {
 
 struct LaneIn {
     const double* w;     // node values (scaled), [32]
+    const double* nc;    // LDS: C[n][n] / (h tf) at a Radau node (0 at the shooting node), 1 / tf
     int lane;
-    bool radau;
-    double cnn_ihtf;     // C[n][n] / (h tf)
-    double inv_tf;
     __device__ __forceinline__ awe::Dual operator()(int i) const {
         double t = (i == lane) ? 1.0 : 0.0;
-        if (radau && i >= K3_NX && i < 2 * K3_NX) {
-            if (lane == i - K3_NX) t = cnn_ihtf;
-            if (lane == kDirTf) t = -w[i] * inv_tf;
+        if (i >= K3_NX && i < 2 * K3_NX) {
+            // re-read at each use (volatile): two fewer live doubles per lane in the model pass
+            const volatile double* vn = nc;
+            if (lane == i - K3_NX) t = vn[0];
+            if (lane == kDirTf) t = -w[i] * vn[1];
         }
         return awe::Dual(w[i], t);
     }
@@ -84,6 +84,23 @@ struct LaneSink {
         if (lane == 0) gval[r] = v.v;
     }
     __device__ __forceinline__ void ineq_row(int r, const awe::Dual& v) { eq_row(K3_N_EQ + r, v); }
+};
+
+// Main-tether drag preaccumulated per node (K3InlineDrag's element sum): values and partials
+// w.r.t. the scaled node variables q0..2, dq0..2, diam_t; pr = D[3] | dD/d(var j)[7][3].
+constexpr int kDragDirs = 7, kDragStride = 24;
+__device__ __forceinline__ int drag_var(int j) { return j < 6 ? j : awe::k3::TH_DIAM; }
+
+struct LdsDrag {
+    const double* pr;
+    int lane;
+    __device__ __forceinline__ void operator()(const awe::Dual*, const awe::Dual*, const awe::Dual&, double,
+                                               const double*, awe::Dual D[3]) const {
+        // lane = direction (uncompressed seeds): its tangent is the partial along its own variable
+        const int j = lane < 6 ? lane : (lane == awe::k3::TH_DIAM ? 6 : -1);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) D[i] = awe::Dual(pr[i], j >= 0 ? pr[3 + 3 * j + i] : 0.0);
+    }
 };
 
 template <int D>
@@ -104,6 +121,8 @@ __global__ __launch_bounds__(64 * waves_for<D>(), 3) void mpc_interval_kernel(MA
     __shared__ double tang[NN * kRowsPerNode * kLanes];
     __shared__ double gval[NN][16];
     __shared__ double fterm[STRIDE];
+    __shared__ double pre[NN][kDragStride];
+    __shared__ double nodec[NN][2];
 
     const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
     const int tid = threadIdx.x;
@@ -151,14 +170,39 @@ __global__ __launch_bounds__(64 * waves_for<D>(), 3) void mpc_interval_kernel(MA
     }
     __syncthreads();
 
+    if (tid < NN) {
+        nodec[tid][0] = tid > 0 ? C[tid * NN + tid] * inv_h_tf : 0.0;
+        nodec[tid][1] = tid > 0 ? 1.0 / tf : 0.0;     // the t_f direction acts at Radau nodes only
+    }
+    // ---- tether drag, one (node, direction) per thread: the element sum in the model's order --
+    for (int t = tid; t < NN * kDragDirs; t += NT) {
+        const int n = t / kDragDirs, j = t - n * kDragDirs, vj = drag_var(j);
+        const double* s = a.cst + K3_C_SCALING;
+        awe::Dual q[3], v[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            q[i] = awe::Dual(wn[n][awe::k3::Q + i], vj == awe::k3::Q + i ? 1.0 : 0.0) * s[awe::k3::Q + i];
+            v[i] = awe::Dual(wn[n][awe::k3::DQ + i], vj == awe::k3::DQ + i ? 1.0 : 0.0) * s[awe::k3::DQ + i];
+        }
+        const awe::Dual diam = awe::Dual(wn[n][awe::k3::TH_DIAM], vj == awe::k3::TH_DIAM ? 1.0 : 0.0) * s[awe::k3::TH_DIAM];
+        awe::Dual Dt[3];
+        awe::K3InlineDrag()(q, v, diam, u_ref, a.cst, Dt);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (j == 0) pre[n][i] = Dt[i].v;
+            pre[n][3 + 3 * j + i] = Dt[i].d;
+        }
+    }
+    __syncthreads();
+
     // ---- model pass: half-wave = node, lane = direction --------------------------------------
     {
         const int n = tid / kLanes, lane = tid % kLanes;
         if (n < NN) {
-            LaneIn in{wn[n], lane, n > 0, n > 0 ? C[n * NN + n] * inv_h_tf : 0.0, 1.0 / tf};
+            LaneIn in{wn[n], nodec[n], lane};
             LaneSink sink{tang + n * kRowsPerNode * kLanes, gval[n], lane};
             awe::Dual gamma(wn[n][kDirGamma], lane == kDirGamma ? 1.0 : 0.0);
-            awe::kite3_node<awe::Dual>(in, gamma, u_ref, a.cst, sink, n == 0);
+            awe::kite3_node<awe::Dual>(in, gamma, u_ref, a.cst, sink, n == 0, LdsDrag{pre[n], lane});
         }
     }
     // ---- tracking objective: per local column (pmpc.py:304-358) -----------------------------

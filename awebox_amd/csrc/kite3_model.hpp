@@ -83,8 +83,24 @@ AWE_HD void k3_tether_element(int e, int n_el, const T* q, const T* v, const T& 
     for (int i = 0; i < 3; ++i) out[i] = sg * (fac * ue[i]);
 }
 
-template <class T, class In, class Sink>
-AWE_HD void kite3_node(const In& in, const T& gamma, double u_ref, const double* c, Sink& out, bool want_ineq) {
+// the main tether's drag summed over its elements, evaluated inside the node model (host
+// structure, CPU paths); the GPU kernel substitutes values + partials preaccumulated per node
+struct K3InlineDrag {
+    template <class T>
+    AWE_HD void operator()(const T* q, const T* v, const T& diam, double u_ref, const double* c, T D[3]) const {
+        const int n_el = (int)c[K3_C_N_ELEMENTS];
+        for (int i = 0; i < 3; ++i) D[i] = T(0.0);
+        for (int e = 0; e < n_el; ++e) {
+            T ce[3];
+            k3_tether_element(e, n_el, q, v, diam, u_ref, c, ce);
+            for (int i = 0; i < 3; ++i) D[i] = D[i] + ce[i];
+        }
+    }
+};
+
+template <class T, class In, class Sink, class Drag = K3InlineDrag>
+AWE_HD void kite3_node(const In& in, const T& gamma, double u_ref, const double* c, Sink& out, bool want_ineq,
+                       const Drag& drag = Drag()) {
     using namespace k3;
     const double* s = c + K3_C_SCALING;
     auto SI = [&](int i) -> T { return in(i) * s[i]; };
@@ -151,15 +167,7 @@ AWE_HD void kite3_node(const In& in, const T& gamma, double u_ref, const double*
     const double g_grav = c[K3_C_G], m_k = c[K3_C_M_K], rho_t = c[K3_C_RHO_TETHER];
     T diam = SI(TH_DIAM);
     T D_tether[3];
-    {
-        const int n_el = (int)c[K3_C_N_ELEMENTS];
-        for (int i = 0; i < 3; ++i) D_tether[i] = T(0.0);
-        for (int e = 0; e < n_el; ++e) {
-            T ce[3];
-            k3_tether_element(e, n_el, q, v, diam, u_ref, c, ce);
-            for (int i = 0; i < 3; ++i) D_tether[i] = D_tether[i] + ce[i];
-        }
-    }
+    drag(q, v, diam, u_ref, c, D_tether);
     T qq = k3_dot(q, q);
     T nq = sqrt(qq);
     T mu = ((k3::kPi * 0.25) * diam * diam) * rho_t;              // m_t = mu |q|

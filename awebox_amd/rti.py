@@ -35,6 +35,7 @@ import torch
 
 from . import kite3 as k3
 from .collocation import coefficients
+from .ipm import _ScatterSum
 
 
 def orbit_states(orbit: k3.CircularOrbit, t: np.ndarray) -> np.ndarray:
@@ -183,6 +184,10 @@ class BatchedRti:
         valid = (r_idx < nS) & (c_idx < nS)                      # [nk, L, L]
         self.schur_src = t(np.where(valid.reshape(-1))[0])
         self.btd_schur = t(btd_index(r_idx[valid], c_idx[valid])[None, :] + bo * bT).reshape(-1)
+        # fixed-order sums over the duplicate destinations (the separators shared by neighbouring
+        # intervals): index_add_ would add them with run-dependent atomics on the GPU
+        self._schur_sum = _ScatterSum(self.btd_schur.cpu().numpy(), self.dev)
+        self._rs_sum = _ScatterSum(self.lsep.reshape(-1).cpu().numpy(), self.dev)
         T0 = np.zeros((nb, 3, m, m))
         for a in range(nb):
             for i in range(sizes[a], m):
@@ -442,11 +447,11 @@ class BatchedRti:
         Xz = self._solve(LU, piv, torch.cat([KIS, rI.view(B * nk, nI, 1)], dim=2))
         X, z = Xz[:, :, :L], Xz[:, :, L:]
         Tsch = (KIS.transpose(1, 2) @ X).view(B, nk * L * L)
-        Tb.index_add_(0, self.btd_schur, -Tsch[:, self.schur_src].reshape(-1))
+        self._schur_sum.add_into(Tb, -Tsch[:, self.schur_src].reshape(-1))
         upd = (KIS.transpose(1, 2) @ z).view(B, nk * L)
         rS = torch.zeros(B, nS + 1, **f64)
         rS[:, :nS] = rhs[:, self.sep_p]
-        rS.index_add_(1, self.lsep.reshape(-1), -upd)
+        self._rs_sum.add_into(rS, -upd)
         rb = torch.zeros(B, self.nb * self.m, **f64)
         rb[:, self.sep_btd] = rS[:, :nS]
         xb = self._btd(Tb.view(B, self.nb, 3, self.m, self.m), rb.view(B, self.nb, self.m, 1)).view(B, -1)

@@ -637,9 +637,39 @@ def hessian_block(ev, V, P, B, lay, dev, steps=10):
         kms.append(ev.last_hess_ms())
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    return {"metric": "nlp_hess_l evals/sec", "value": B / dt, "unit": "evals/s", "ms_per_step": dt * 1e3,
-            "kernel_ms": float(np.mean(kms)), "nnz_h": ev.nnz_h, "batch": B,
-            "finite": bool(torch.isfinite(H).all().item())}
+    out = {"metric": "nlp_hess_l evals/sec", "value": B / dt, "unit": "evals/s", "ms_per_step": dt * 1e3,
+           "kernel_ms": float(np.mean(kms)), "nnz_h": ev.nnz_h, "batch": B,
+           "finite": bool(torch.isfinite(H).all().item())}
+    rl = hess_roofline(B, float(np.mean(kms)))
+    if rl is not None:
+        out["roofline"] = rl
+    return out
+
+
+def hess_roofline(B, kernel_ms):
+    """FP64 issue roofline of ap2_hess_kernel from its committed PMC record (profiles/pmc_hess.json,
+    tools/gpu_pmc_all.sh at 256 instances): FP64 lane operations per instance (ADD + MUL + 2 FMA +
+    TRANS, x 64 lanes; they scale with the instance count) x B / the kernel time, against the
+    78.6 TFLOP/s FP64 vector peak; HBM bytes 2 x FETCH + WRITE likewise.  None if the record was
+    taken on other sources."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_hess.json")) as fh:
+            rec = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if rec.get("source_hash") != kernel_source_hash():
+        return None
+    per = rec["batch"]
+    ops = (rec["SQ_INSTS_VALU_ADD_F64"] + rec["SQ_INSTS_VALU_MUL_F64"] + 2.0 * rec["SQ_INSTS_VALU_FMA_F64"]
+           + rec["SQ_INSTS_VALU_TRANS_F64"]) * 64.0 / per
+    f64 = rec["SQ_INSTS_VALU_ADD_F64"] + rec["SQ_INSTS_VALU_MUL_F64"] + rec["SQ_INSTS_VALU_FMA_F64"] + \
+        rec["SQ_INSTS_VALU_TRANS_F64"]
+    achieved = ops * B / (kernel_ms * 1e-3) / 1e12
+    hbm = (2.0 * rec["FETCH_SIZE_kB"] + rec["WRITE_SIZE_kB"]) * 1024 / per * B / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "fp64", "achieved": achieved, "peak": 78.6, "unit": "TFLOP/s", "frac": achieved / 78.6,
+            "kernel": "ap2_hess_kernel<4>", "valu_f64_share": f64 / rec["SQ_INSTS_VALU"],
+            "wait_frac": rec["SQ_WAIT_ANY"] / rec["SQ_WAVE_CYCLES"], "occupancy_waves_per_simd": 1,
+            "hbm_GBps": hbm, "pmc_record": "profiles/pmc_hess.json"}
 
 
 def latency_block(consts, lay, v0, with_cpu=True, reps=50):

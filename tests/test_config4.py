@@ -7,7 +7,8 @@ HIP dual-kite evaluator and the interior-point solver.
   the shard's first point, one batched warm start for the rest) converges everywhere, with power
   rising with the wind speed;
 * sharding invariance: the same points split into two shards (as two ranks would hold them) give
-  the same powers as the single shard, to the solver tolerance.
+  the same powers as the single shard: bitwise for the shard's homotopy point, to 0.1 % for the
+  warm-started points (their anchor differs between the shardings).
 The example's own discretisation is N=20; the test runs N=12 to stay within a minute or two."""
 import numpy as np
 import pytest
@@ -43,4 +44,9 @@ def test_dual_fan_sweep_converges_and_is_shard_invariant(gpu):
     a, b = _sweep(u[:2]), _sweep(u[2:])
     assert all(a["ok"]) and all(b["ok"])
     sharded = np.asarray(a["avg_power_W"] + b["avg_power_W"])
-    assert np.allclose(sharded, p, rtol=1e-5), (sharded, p)
+    # the shard's first point follows the same homotopy path in both runs: identical result
+    assert sharded[0] == p[0]
+    # the other points are warm starts from a different anchor (the second shard starts its own
+    # homotopy at u[2]); with the exact Hessian the warm starts land on the same orbit family to
+    # ~1e-4 in power (measured 1.2e-4 at u[2], 1e-6 at u[3]), not on one bitwise-equal optimum
+    assert np.allclose(sharded, p, rtol=1e-3), (sharded, p)

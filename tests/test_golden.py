@@ -16,7 +16,8 @@ from awebox_amd import problem as pb
 from test_cpu_port import _close_hess
 from test_gpu_parity import _close, _close_jac
 
-FILES = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+# the AP2 evaluator fixtures (the dual-kite Hessian fixtures, dual_hess_*.npz, belong to test_dual_hess_gpu.py)
+FILES = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "ap2_*.npz")))
 IDS = [os.path.basename(f)[:-4] for f in FILES]
 
 

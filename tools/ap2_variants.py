@@ -1,0 +1,38 @@
+"""Time variants of libawegpu.so on the GPU, one subprocess each (the bench's AP2 block:
+B = 2048 instances of N=40 d=4, HIP-event kernel time, checksums of the outputs).
+
+usage: python tools/ap2_variants.py lib1.so lib2.so ...
+"""
+import json
+import subprocess
+import sys
+
+CHILD = r'''
+import sys, json, numpy as np, torch
+sys.path.insert(0, ".")
+from awebox_amd import evaluator as E, problem as pb
+from awebox_amd.initial_guess import batch_member, initial_guess
+E._LIB = None
+lib = E.load_library(sys.argv[1])
+B = 2048
+consts = pb.build_constants(); lay = pb.NlpLayout(40, 4); v0 = initial_guess(consts, lay)
+V = torch.tensor(np.stack([batch_member(v0, lay, b) for b in range(B)]), device="cuda")
+P = torch.tensor(np.stack([pb.pack_p(lay, consts, v0)] * B), device="cuda")
+ev = E.Ap2Evaluator(consts, batch=B)
+assert ev._lib is lib, "variant library not in use"
+f = torch.empty(B, dtype=torch.float64, device="cuda"); g = torch.empty(B, ev.n_g, dtype=torch.float64, device="cuda")
+gr = torch.empty(B, ev.n_v, dtype=torch.float64, device="cuda"); jac = torch.empty(B, ev.nnz, dtype=torch.float64, device="cuda")
+ks = []
+for i in range(25):
+    ev.eval_nlp_device(V, P, f, g, gr, jac)
+    if i >= 5: ks.append(ev.last_kernel_ms()[0])
+torch.cuda.synchronize()
+print(json.dumps({"lib": sys.argv[1], "kernel_ms": float(np.median(ks)), "evals_per_s": B / float(np.median(ks)) * 1e3,
+                  "jac_sum": float(jac.sum()), "g_sum": float(g.sum()), "grad_sum": float(gr.sum())}))
+'''
+
+if __name__ == "__main__":
+    for rep in range(2):
+        for lib in sys.argv[1:]:
+            r = subprocess.run([sys.executable, "-c", CHILD, lib], capture_output=True, text=True, timeout=240)
+            print(r.stdout.strip() or json.dumps({"lib": lib, "error": r.stderr[-800:]}), flush=True)

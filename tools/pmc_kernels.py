@@ -32,11 +32,38 @@ def ap2(B=2048):
     print("pmc ap2 done", flush=True)
 
 
+def hess(B=256):
+    """5 batched AP2 N=40 d=4 nlp_hess_l evaluations (sigma = 1, lam ~ N(0,1) seed 7, as the bench)."""
+    import numpy as np
+    import torch
+
+    from awebox_amd import problem as pb
+    from awebox_amd.evaluator import Ap2Evaluator
+    from awebox_amd.initial_guess import batch_member, initial_guess
+    dev = torch.device("cuda:0")
+    consts = pb.build_constants()
+    lay = pb.NlpLayout(40, 4)
+    v0 = initial_guess(consts, lay)
+    V = torch.tensor(np.stack([batch_member(v0, lay, b) for b in range(B)]), device=dev)
+    P = torch.tensor(np.stack([pb.pack_p(lay, consts, v0)] * B), device=dev)
+    ev = Ap2Evaluator(consts, batch=B)
+    g = torch.Generator().manual_seed(7)
+    lam = torch.randn(B, ev.n_g, generator=g, dtype=torch.float64).to(dev)
+    sig = torch.ones(B, dtype=torch.float64, device=dev)
+    H = torch.empty(B, ev.nnz_h, dtype=torch.float64, device=dev)
+    for _ in range(5):
+        ev.eval_hess_device(V, P, sig, lam, H)
+    torch.cuda.synchronize()
+    print("pmc hess done", float(ev.last_hess_ms()), flush=True)
+
+
 def main():
     import numpy as np
     import torch
     if "--ap2" in sys.argv:
         return ap2()
+    if "--hess" in sys.argv:
+        return hess()
 
     from awebox_amd import dual as du
     from awebox_amd import kite3 as k3

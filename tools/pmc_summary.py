@@ -23,8 +23,48 @@ def summarise(paths, kernel_substr="interval"):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
+def record_configs(fetch_dir, write_dir):
+    """profiles/pmc_traffic_configs.json: FETCH/WRITE_SIZE per dispatch of the config-3 (dual kites,
+    B = 128) and config-5 (tracking MPC, B = 256) interval kernels of tools/pmc_kernels.py."""
+    sys.path.insert(0, ROOT)
+    from bench import sources_hash
+    out = {}
+    for which, kern, batch in (("dual", "dual_interval_kernel", 128), ("mpc", "mpc_interval_kernel", 256)):
+        f = summarise(glob.glob(os.path.join(fetch_dir, "**", "*counter_collection.csv"), recursive=True), kern)
+        w = summarise(glob.glob(os.path.join(write_dir, "**", "*counter_collection.csv"), recursive=True), kern)
+        if "FETCH_SIZE" not in f or "WRITE_SIZE" not in w:
+            continue
+        out[which] = {"batch": batch, "kernel": kern + "<4>", "source_hash": sources_hash(which),
+                      "FETCH_SIZE_kB": f["FETCH_SIZE"], "WRITE_SIZE_kB": w["WRITE_SIZE"],
+                      "units": "kB per dispatch, mean over 5 dispatches (tools/pmc_kernels.py, tools/gpu_pmc_all.sh)"}
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic_configs.json"), "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+    print("wrote profiles/pmc_traffic_configs.json", sorted(out))
+
+
+def record_hess(dirs, batch=256):
+    """profiles/pmc_hess.json: counters per dispatch of ap2_hess_kernel<4> (tools/pmc_kernels.py --hess)."""
+    sys.path.insert(0, ROOT)
+    from bench import kernel_source_hash
+    paths = [p for d in dirs for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)]
+    summ = summarise(paths, "ap2_hess_kernel")
+    rec = {"batch": batch, "kernel": "ap2_hess_kernel<4>", "source_hash": kernel_source_hash(),
+           "units": "FETCH/WRITE_SIZE in kB per dispatch; SQ_* per dispatch"}
+    for k, v in summ.items():
+        rec[k + ("_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else "")] = v
+    with open(os.path.join(ROOT, "profiles", "pmc_hess.json"), "w") as fh:
+        json.dump(rec, fh, indent=1, sort_keys=True)
+    print("wrote profiles/pmc_hess.json")
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
+    if args and args[0] == "--record-configs":
+        record_configs(args[1], args[2])
+        sys.exit(0)
+    if args and args[0] == "--record-hess":
+        record_hess(args[1:])
+        sys.exit(0)
     batch = None
     if args and args[0] == "--record":
         batch = int(args[1])
