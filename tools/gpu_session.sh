@@ -1,4 +1,6 @@
 #!/bin/bash
+# Round-2 kernel session: AP2 seed-variant timings (tools/ap2_variants.py), PMC traffic of the
+# config-3/5 kernels, and the config-5 / config-4 GPU tests.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
