@@ -259,12 +259,28 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
         double* Dg = T + ((size_t)k * 3 + 1) * mm;
         double* Ug = T + ((size_t)k * 3 + 2) * mm;
         const bool last = k == nb - 1;
-        for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < m; j += 64) {
-                R0[i][j] = Dg[i * m + j];
-                R0[i][m + j] = last ? 0.0 : Ug[i * m + j];
-                R0[i][2 * m + j] = i == j ? 1.0 : 0.0;
-                if (k > 0) R1[i][j] = Lg[i * m + j];
+        {
+            // the stage's three blocks: every global load of a thread issued before its first LDS
+            // store, so the 3 x 12 row loads overlap instead of paying one memory latency each
+            constexpr int R = kBtdMaxM / kRG;
+            double vd[R], vu[R], vl[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = ti + r * kRG;
+                const bool in = i < m && tj < m;
+                vd[r] = in ? Dg[i * m + tj] : 0.0;
+                vu[r] = (in && !last) ? Ug[i * m + tj] : 0.0;
+                vl[r] = (in && k > 0) ? Lg[i * m + tj] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = ti + r * kRG;
+                if (i < m && tj < m) {
+                    R0[i][tj] = vd[r];
+                    R0[i][m + tj] = vu[r];
+                    R0[i][2 * m + tj] = i == tj ? 1.0 : 0.0;
+                    if (k > 0) R1[i][tj] = vl[r];
+                }
             }
         }
         __syncthreads();
@@ -423,6 +439,7 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
                                                             const double* __restrict__ Dinvs,
                                                             double* __restrict__ Xs) {
     __shared__ double A[kBtdMaxM][kBtdMaxM + 1];
+    __shared__ double Ai[kBtdMaxM][kBtdMaxM + 1];
     __shared__ double Dp[kBtdMaxM][kBtdMaxM + 1];
     __shared__ double Y[kBtdMaxM][kBtdMaxRhs + 1];
     __shared__ double Z[kBtdMaxM][kBtdMaxRhs + 1];
@@ -432,40 +449,65 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
     const double* T = Ts + (size_t)blockIdx.x * nb * 3 * mm;
     const double* Dinv = Dinvs + (size_t)blockIdx.x * nb * mm;
     double* X = Xs + (size_t)blockIdx.x * nb * m * ldx + j0;
+    // a stage's global loads (right-hand sides and up to three blocks, 12 rows each per thread,
+    // tj < 64 covers the m <= 48 and w <= 64 columns) are all issued before the first LDS store:
+    // one memory latency per stage instead of one per row and block (the chain is latency-bound)
+    constexpr int R = kBtdMaxM / kRG;
 
     for (int k = 0; k < nb; ++k) {                            // forward: Y_k
         double* Xk = X + (size_t)k * m * ldx;
-        for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < w; j += 64) Z[i][j] = Xk[(size_t)i * ldx + j];
-            if (k > 0)
-                for (int j = tj; j < m; j += 64) A[i][j] = T[((size_t)k * 3 + 0) * mm + i * m + j];
+        {
+            double vz[R], vl[R], vi[R], vp[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = ti + r * kRG;
+                const bool in = i < m && tj < m;
+                vz[r] = (i < m && tj < w) ? Xk[(size_t)i * ldx + tj] : 0.0;
+                vl[r] = (in && k > 0) ? T[((size_t)k * 3 + 0) * mm + i * m + tj] : 0.0;
+                vi[r] = in ? Dinv[(size_t)k * mm + i * m + tj] : 0.0;
+                vp[r] = in ? T[((size_t)k * 3 + 1) * mm + i * m + tj] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = ti + r * kRG;
+                if (i < m) {
+                    if (tj < w) Z[i][tj] = vz[r];
+                    if (tj < m) { A[i][tj] = vl[r]; Ai[i][tj] = vi[r]; Dp[i][tj] = vp[r]; }
+                }
+            }
         }
         __syncthreads();
         if (k > 0) {                                          // Z -= L_k Y_{k-1}
             btd_matmul<-1>(A, Y, Z, Z, m, w, ti, tj, false);
             __syncthreads();
         }
-        for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < m; j += 64) {
-                A[i][j] = Dinv[(size_t)k * mm + i * m + j];
-                Dp[i][j] = T[((size_t)k * 3 + 1) * mm + i * m + j];
-            }
-        }
-        __syncthreads();
-        btd_matmul<1>(A, Z, Z, Y, m, w, ti, tj, true);        // Y = D'^-1 Z
+        btd_matmul<1>(Ai, Z, Z, Y, m, w, ti, tj, true);       // Y = D'^-1 Z
         __syncthreads();
         btd_matmul<-1>(Dp, Y, Z, Q, m, w, ti, tj, false);     // one refinement step: Q = Z - D' Y
         __syncthreads();
-        btd_matmul<1>(A, Q, Y, Y, m, w, ti, tj, false);       // Y += D'^-1 Q
+        btd_matmul<1>(Ai, Q, Y, Y, m, w, ti, tj, false);      // Y += D'^-1 Q
         __syncthreads();
         for (int i = ti; i < m; i += kRG)
             for (int j = tj; j < w; j += 64) Xk[(size_t)i * ldx + j] = Y[i][j];
     }
     for (int k = nb - 2; k >= 0; --k) {                       // backward: x_k = Y_k - W_k x_{k+1}
         double* Xk = X + (size_t)k * m * ldx;
-        for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < m; j += 64) A[i][j] = T[((size_t)k * 3 + 2) * mm + i * m + j];
-            for (int j = tj; j < w; j += 64) Z[i][j] = Xk[(size_t)i * ldx + j];
+        {
+            double vu[R], vz[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = ti + r * kRG;
+                vu[r] = (i < m && tj < m) ? T[((size_t)k * 3 + 2) * mm + i * m + tj] : 0.0;
+                vz[r] = (i < m && tj < w) ? Xk[(size_t)i * ldx + tj] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = ti + r * kRG;
+                if (i < m) {
+                    if (tj < m) A[i][tj] = vu[r];
+                    if (tj < w) Z[i][tj] = vz[r];
+                }
+            }
         }
         __syncthreads();
         btd_matmul<-1>(A, Y, Z, Z, m, w, ti, tj, false);
