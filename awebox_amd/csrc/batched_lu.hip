@@ -408,20 +408,23 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
     }
 }
 
-// Z[i][j] (-)= sum_c M[i][c] Y[c][j] for i < m, j < w: with few right-hand sides one wave per
-// (i, j) and the lanes over c (wave-shuffle sum) -- the one-right-hand-side solves of the
-// interior-point refinement would otherwise leave 60 of 64 lanes idle; with many, one thread per
-// (row group, column).
+// Z[i][j] (-)= sum_c M[i][c] Y[c][j] for i < m, j < w: with few right-hand sides one thread per
+// (i, j) over the whole workgroup, the m products summed in order from LDS (independent loads,
+// they pipeline) -- the one-right-hand-side solves of the interior-point refinement would
+// otherwise leave 60 of 64 lanes idle.  (A wave per (i, j) with a shuffle-tree sum, the previous
+// form, paid six dependent cross-lane steps per row: ~4 us per product, 12 rows per wave.)  With
+// many right-hand sides, one thread per (row group, column).
 template <int SIGN>
 __device__ __forceinline__ void btd_matmul(double (*M)[kBtdMaxM + 1], double (*Yv)[kBtdMaxRhs + 1],
                                            double (*Zv)[kBtdMaxRhs + 1], double (*Out)[kBtdMaxRhs + 1],
                                            int m, int w, int ti, int tj, bool init_zero) {
     if (w <= 8) {
-        for (int p = ti; p < m * w; p += kRG) {
+        for (int p = ti * 64 + tj; p < m * w; p += kThreads) {
             const int i = p / w, j = p - i * w;
-            double v = tj < m ? M[i][tj] * Yv[tj][j] : 0.0;
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if (tj == 0) Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * v;
+            double acc = 0.0;
+#pragma unroll 8
+            for (int c = 0; c < m; ++c) acc += M[i][c] * Yv[c][j];
+            Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * acc;
         }
     } else {
         for (int i = ti; i < m; i += kRG) {

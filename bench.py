@@ -617,7 +617,7 @@ def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
             "period_s": [round(t, 2) for t in res["period_s"]], "scaling": "weak",
             "solver": "GPU interior point (awebox_amd/ipm.py): homotopy for the shard's first point, batched warm "
                       "start for the rest; structured KKT with the block-recursion separator sweep, exact KKT "
-                      "inertia; Hessian by coloured central differences of the HIP gradient (fd_hessian.py)"}
+                      "inertia; exact Hessian of the Lagrangian (dual_hess_kernel: colour-pair hyper-dual forward mode)"}
 
 
 def hessian_block(ev, V, P, B, lay, dev, steps=10):
