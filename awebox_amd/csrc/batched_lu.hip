@@ -408,32 +408,23 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
     }
 }
 
-// Z[i][j] (-)= sum_c M[i][c] Y[c][j] for i < m, j < w: with few right-hand sides one thread per
-// (i, j) over the whole workgroup, the m products summed in order from LDS (independent loads,
-// they pipeline) -- the one-right-hand-side solves of the interior-point refinement would
-// otherwise leave 60 of 64 lanes idle.  (A wave per (i, j) with a shuffle-tree sum, the previous
-// form, paid six dependent cross-lane steps per row: ~4 us per product, 12 rows per wave.)  With
-// many right-hand sides, one thread per (row group, column).
+// Z[i][j] (-)= sum_c M[i][c] Y[c][j] for i < m, j < w: one thread per (i, j) over the whole
+// workgroup (consecutive threads take consecutive columns of a row: M[i][c] is a broadcast,
+// Y[c][j] conflict-free), the m products summed in order from LDS (independent loads, they
+// pipeline).  The previous forms -- a wave per (i, j) with a shuffle-tree sum for few right-hand
+// sides (six dependent cross-lane steps per row), one thread per (row group, column) otherwise (12
+// rows serially per thread; 4 of 256 threads busy for one column) -- were latency-bound: the
+// 41-stage solve took 3.1 ms, 2.2 ms with this mapping for one column.
 template <int SIGN>
 __device__ __forceinline__ void btd_matmul(double (*M)[kBtdMaxM + 1], double (*Yv)[kBtdMaxRhs + 1],
                                            double (*Zv)[kBtdMaxRhs + 1], double (*Out)[kBtdMaxRhs + 1],
                                            int m, int w, int ti, int tj, bool init_zero) {
-    if (w <= 8) {
-        for (int p = ti * 64 + tj; p < m * w; p += kThreads) {
-            const int i = p / w, j = p - i * w;
-            double acc = 0.0;
+    for (int p = ti * 64 + tj; p < m * w; p += kThreads) {
+        const int i = p / w, j = p - i * w;
+        double acc = 0.0;
 #pragma unroll 8
-            for (int c = 0; c < m; ++c) acc += M[i][c] * Yv[c][j];
-            Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * acc;
-        }
-    } else {
-        for (int i = ti; i < m; i += kRG) {
-            for (int j = tj; j < w; j += 64) {
-                double acc = 0.0;
-                for (int c = 0; c < m; ++c) acc += M[i][c] * Yv[c][j];
-                Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * acc;
-            }
-        }
+        for (int c = 0; c < m; ++c) acc += M[i][c] * Yv[c][j];
+        Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * acc;
     }
 }
 
