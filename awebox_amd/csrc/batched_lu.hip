@@ -329,13 +329,16 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
                     a[r][q] = (i < m && j < na) ? R0[i][j] : 0.0;
                 }
         }
-        double* colbuf = &R1[0][0];                           // column c of the current matrix
-        double* rowbuf = &R1[1][0];                           // the pivot row (3 m entries)
-        int* used = reinterpret_cast<int*>(&R1[3][0]);        // row already a pivot
+        // column and pivot-row buffers alternate between columns (c & 1), so a column needs two
+        // barriers, not three: a wave can only write column c + 2's buffers after every wave has
+        // passed column c + 1's barriers, i.e. finished reading column c's.  Every wave finds the
+        // same pivot, so the set of used pivot rows is a per-wave register mask.
         int* pivrow = reinterpret_cast<int*>(&R1[4][0]);      // pivot row of column c
-        for (int i = tid; i < m; i += kThreads) used[i] = 0;
+        unsigned long long usedmask = 0ull;                   // rows already pivots (m <= 48)
         __syncthreads();
         for (int c = 0; c < m; ++c) {
+            double* colbuf = &R1[(c & 1) ? 2 : 0][0];         // column c of the current matrix
+            double* rowbuf = &R1[(c & 1) ? 3 : 1][0];         // the pivot row (3 m entries)
             if (owner && cg == c / kTC) {
 #pragma unroll
                 for (int r = 0; r < kTR; ++r) {
@@ -348,13 +351,14 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
             __syncthreads();
             double best = -1.0;                               // every wave finds the same pivot
             int bi = m;
-            if (tj < m && !used[tj]) { best = fabs(colbuf[tj]); bi = tj; }
+            if (tj < m && !((usedmask >> tj) & 1ull)) { best = fabs(colbuf[tj]); bi = tj; }
             for (int off = 32; off > 0; off >>= 1) {
                 const double ob = __shfl_xor(best, off);
                 const int oi = __shfl_xor(bi, off);
                 if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
             }
             const int p = bi;
+            usedmask |= 1ull << p;
             if (owner && rg == p / kTR) {
 #pragma unroll
                 for (int r = 0; r < kTR; ++r)
@@ -378,9 +382,9 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
                     }
                 }
             }
-            if (tid == 0) { used[p] = 1; pivrow[c] = p; }
-            __syncthreads();
+            if (tid == 0) pivrow[c] = p;
         }
+        __syncthreads();
         // row pivrow[c] holds row c of the result: scatter back to R0 in order
         if (owner) {
 #pragma unroll
