@@ -349,15 +349,15 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
                 }
             }
             __syncthreads();
-            double best = -1.0;                               // every wave finds the same pivot
-            int bi = m;
-            if (tj < m && !((usedmask >> tj) & 1ull)) { best = fabs(colbuf[tj]); bi = tj; }
-            for (int off = 32; off > 0; off >>= 1) {
-                const double ob = __shfl_xor(best, off);
-                const int oi = __shfl_xor(bi, off);
-                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-            }
-            const int p = bi;
+            // every wave finds the same pivot: the largest |entry| among unused rows by a max
+            // butterfly, then the smallest such row by one ballot (ties as before: lowest row)
+            const bool cand = tj < m && !((usedmask >> tj) & 1ull);
+            const double best = cand ? fabs(colbuf[tj]) : -1.0;
+            double mx = best;
+            for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+            unsigned long long hit = __ballot(cand && best == mx);
+            if (hit == 0ull) hit = ~usedmask & ((1ull << m) - 1ull);    // all-NaN column: any unused row
+            const int p = __ffsll((long long)hit) - 1;
             usedmask |= 1ull << p;
             if (owner && rg == p / kTR) {
 #pragma unroll
