@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per thread setting")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hessian", action="store_true", help="skip the nlp_hess_l timing block")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the batch-1 host round-trip block (its launches share the AP2 kernel's name)")
     ap.add_argument("--mpc-batch", type=int, default=256,
                     help="MPC instances for the config-5 block (3-DOF tracking MPC, N=20 d=4; 0: skip)")
     ap.add_argument("--pmpc-loops", type=int, default=64,
@@ -288,7 +290,7 @@ def main():
         line["dual_sweep"] = dual_sweep
     if not args.no_hessian:
         line["hessian"] = hessian_block(ev, V, P, B, lay, dev)
-    if world == 1:
+    if world == 1 and not args.no_latency:
         line["latency_batch1"] = latency_block(consts, lay, v0, with_cpu=not args.no_cpu_baseline)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(consts, lay, v0, args.cpu_seconds)

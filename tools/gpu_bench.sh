@@ -13,7 +13,7 @@ step() {  # step <limit> <log> <cmd...>
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
 step 600 bench.log python bench.py
-step 300 rocprof_ap2.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ap2 -o run --output-format csv -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --pmpc-loops 0 --sweep-points 0 --dual-sweep-points 0 --no-hessian
+step 300 rocprof_ap2.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ap2 -o run --output-format csv -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --pmpc-loops 0 --sweep-points 0 --dual-sweep-points 0 --no-hessian --no-latency
 find gpurun_out/prof_ap2 -name '*_trace.csv' -size +4M -delete
 step 400 rocprof_sweep.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sweep -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --pmpc-loops 0 --dual-sweep-points 0 --no-hessian
 find gpurun_out/prof_sweep -name '*_trace.csv' -size +4M -delete

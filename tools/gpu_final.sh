@@ -15,7 +15,7 @@ step() {  # step <limit> <log> <cmd...>
 step 900 pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 step 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
 step 600 bench.log python bench.py
-step 300 rocprof_ap2.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ap2 -o run --output-format csv -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --sweep-points 0 --dual-sweep-points 0 --no-hessian
+step 300 rocprof_ap2.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ap2 -o run --output-format csv -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --sweep-points 0 --dual-sweep-points 0 --no-hessian --no-latency
 find gpurun_out/prof_ap2 -name '*_trace.csv' -size +4M -delete
 # the AP2 sweep block alone (8 points per GPU, fan mode): GPU busy share = kernel time / wall
 step 400 rocprof_sweep.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sweep -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --pmpc-loops 0 --dual-sweep-points 0 --no-hessian
