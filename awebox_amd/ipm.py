@@ -464,7 +464,7 @@ class StructuredKKT:
     def matvec(self, x):
         return self._mv(self.vals, x)
 
-    def solve(self, rhs, refine=3, rtol=1e-12):
+    def solve(self, rhs, refine=None, rtol=1e-12):
         """Elimination solve with iterative refinement on the sparse residual, rhs [B, N] (or [N]).
         The interior pivots come from blocks that may be ill-conditioned even when K is not (an
         indefinite interior Hessian), so an instance's result is accepted once its backward error
@@ -472,6 +472,12 @@ class StructuredKKT:
         does not get there is solved once by a dense LU of its assembled K."""
         one = rhs.dim() == 1
         rhs = rhs.unsqueeze(0) if one else rhs
+        if refine is None:
+            # separators through the block recursion (blocks beyond the fused sweep kernels: the
+            # dual kites) leave larger backward errors than the fused sweep's refined block solves;
+            # they get up to IPOPT's max_refinement_steps (10) before an instance falls back to a
+            # dense LU of the whole K (~0.3 s each at N = 13,848), the fused path keeps 3
+            refine = 10 if (self.use_btd and not self.btd.fused) else 3
         self.n_solve += 1
         x = self._solve(rhs)
         b_norm = rhs.abs().amax(dim=1)
