@@ -70,8 +70,8 @@ class BorderedBtd:
         self.sep_g = t(border)
         self.sc = None
         if deterministic:                                  # fixed-order sums of duplicate entries
-            from .ipm import _ScatterSum
-            self.sc = [_ScatterSum(d.cpu().numpy(), dev) for d in (self.dst_tt, self.dst_tg, self.dst_gt, self.dst_gg)]
+            from .ipm import scatter_sum
+            self.sc = [scatter_sum(d.cpu().numpy(), dev) for d in (self.dst_tt, self.dst_tg, self.dst_gt, self.dst_gg)]
 
     # ---------------------------------------------------------------------------------------
     def factor(self, vals):

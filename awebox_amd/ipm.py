@@ -222,6 +222,25 @@ class _ScatterSum:
         return out
 
 
+_SCATTER_CACHE: dict = {}
+
+
+def scatter_sum(dst, dev) -> _ScatterSum:
+    """The _ScatterSum of a destination pattern, shared by every structure with the same pattern on
+    the same device: the homotopy builds a StructuredKKT per step (and per sweep shard), and the
+    host-side table construction was ~0.8 s of a 6-step AP2 homotopy (cProfile,
+    profiles/r02/solver_pstats_b8.txt).  The tables are read-only after construction."""
+    import hashlib
+    dst = np.ascontiguousarray(np.asarray(dst, dtype=np.int64).reshape(-1))
+    key = (hashlib.sha1(dst.tobytes()).hexdigest(), dst.size, str(torch.device(dev)))
+    sc = _SCATTER_CACHE.get(key)
+    if sc is None:
+        if len(_SCATTER_CACHE) >= 256:
+            _SCATTER_CACHE.clear()
+        sc = _SCATTER_CACHE[key] = _ScatterSum(dst, dev)
+    return sc
+
+
 class _GatherMv:
     """y = A(vals) x for a fixed COO pattern: products vals * x[cols], summed per row by a
     _ScatterSum (fixed order).  Replaces rocSPARSE's CSR SpMV, whose adaptive algorithm splits
@@ -229,7 +248,7 @@ class _GatherMv:
 
     def __init__(self, rows, cols, shape, dev):
         self.cols = torch.tensor(np.asarray(cols, dtype=np.int64), device=dev)
-        self.sum = _ScatterSum(rows, dev)
+        self.sum = scatter_sum(rows, dev)
         self.shape = shape
 
     def mv(self, vals, x):
@@ -349,10 +368,10 @@ class StructuredKKT:
         schur_flat = (lsep_arr[:, :, None] * (nS + 1) + lsep_arr[:, None, :]).reshape(-1)
         int_p = np.where(owner >= 0)[0]
         self.int_p = torch.tensor(int_p, device=dev)
-        self.sc = [_ScatterSum(t, dev) for t in (dst_ii, dst_is, dst_ss, schur_flat)]
-        self.sc_mv = _ScatterSum(P_, dev)
-        self.sc_dense = _ScatterSum(P_ * N + Q_, dev)
-        self.sc_rs = _ScatterSum(lsep_arr.reshape(-1), dev)
+        self.sc = [scatter_sum(t, dev) for t in (dst_ii, dst_is, dst_ss, schur_flat)]
+        self.sc_mv = scatter_sum(P_, dev)
+        self.sc_dense = scatter_sum(P_ * N + Q_, dev)
+        self.sc_rs = scatter_sum(lsep_arr.reshape(-1), dev)
         # separators in stages [c[k-1], x[k]] (block tridiagonal, globals as border): pairing each
         # shooting state with the multipliers of the continuity row that defines it keeps the block
         # sweep's pivot blocks regular -- the finer order x[0], c[0], x[1], ... meets near-singular

@@ -35,7 +35,7 @@ import torch
 
 from . import kite3 as k3
 from .collocation import coefficients
-from .ipm import _ScatterSum
+from .ipm import scatter_sum
 
 
 def orbit_states(orbit: k3.CircularOrbit, t: np.ndarray) -> np.ndarray:
@@ -186,8 +186,8 @@ class BatchedRti:
         self.btd_schur = t(btd_index(r_idx[valid], c_idx[valid])[None, :] + bo * bT).reshape(-1)
         # fixed-order sums over the duplicate destinations (the separators shared by neighbouring
         # intervals): index_add_ would add them with run-dependent atomics on the GPU
-        self._schur_sum = _ScatterSum(self.btd_schur.cpu().numpy(), self.dev)
-        self._rs_sum = _ScatterSum(self.lsep.reshape(-1).cpu().numpy(), self.dev)
+        self._schur_sum = scatter_sum(self.btd_schur.cpu().numpy(), self.dev)
+        self._rs_sum = scatter_sum(self.lsep.reshape(-1).cpu().numpy(), self.dev)
         T0 = np.zeros((nb, 3, m, m))
         for a in range(nb):
             for i in range(sizes[a], m):
