@@ -116,17 +116,18 @@ class BorderedBtd:
         Schur complement C' (Haynsworth additivity); the identity rows of unused block positions
         are taken out."""
         from .batched_lu import sym_inertia, sym_inertia_host
+        from .ipm import ZERO_PIVOT
         B, nb, m = self.B, self.nb, self.m
         f = sym_inertia if self.dev_is_cuda() else sym_inertia_host
         if self.fused:
             F, Dinv = self.Tf                              # F's diagonal slots hold the pivot blocks D'_k
-            c = f(F[:, :, 1].reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
+            c = f(F[:, :, 1].reshape(B * nb, m, m), ztol=ZERO_PIVOT).view(B, nb, 3).sum(1)
         else:
-            c = f(self.Dp.reshape(B * nb, m, m), ztol=1e-30).view(B, nb, 3).sum(1)
+            c = f(self.Dp.reshape(B * nb, m, m), ztol=ZERO_PIVOT).view(B, nb, 3).sum(1)
         c = c.to(torch.int64)
         c[:, 0] -= self.n_unused
         if self.nG:
-            cc = (sym_inertia if self.Cp.is_cuda else sym_inertia_host)(self.Cp.contiguous(), ztol=1e-30)
+            cc = (sym_inertia if self.Cp.is_cuda else sym_inertia_host)(self.Cp.contiguous(), ztol=ZERO_PIVOT)
             c = c + cc.to(torch.int64)
         return c
 

@@ -44,10 +44,20 @@ def _require():
         raise ImportError("casadi is not importable here; the bridge is only needed where IPOPT runs via CasADi")
 
 
+def p_packer_for(layout):
+    """The by-name reader of the reference's parameter struct for an evaluator's layout: the
+    periodic-OCP P (AP2 ``NlpLayout`` and multi-kite ``MultiLayout``: problem.pack_p_from_reference)
+    or Pmpc's p (``MpcLayout``: kite3.pack_p_from_reference)."""
+    from . import kite3 as k3
+    from . import problem as pb
+    if isinstance(layout, k3.MpcLayout):
+        return k3.pack_p_from_reference
+    return pb.pack_p_from_reference
+
+
 def reference_p_reader(P_struct):
     """A function turning the reference's numeric P (a DM of P_struct's size) into this library's
-    flat P, reading P_struct's entries by name (problem.pack_p_from_reference)."""
-    from . import problem as pb
+    flat P, reading P_struct's entries by name (p_packer_for the evaluator's layout)."""
 
     def convert(p_num, layout):
         s = P_struct(p_num)
@@ -57,7 +67,7 @@ def reference_p_reader(P_struct):
                 return np.asarray(s[path]).ravel()
             except Exception as exc:                           # missing entry name in the struct
                 raise KeyError(path) from exc
-        return pb.pack_p_from_reference(get, layout)
+        return p_packer_for(layout)(get, layout)
     return convert
 
 
@@ -76,15 +86,20 @@ def make_nlp(evaluator, P_struct=None):
     P = cas.MX.sym("P", n_p)
     F = _FCallback("awe_f", evaluator, convert, n_p)
     G = _GCallback("awe_g", evaluator, convert, n_p)
-    H = _HessCallback("awe_hess_l", evaluator, convert, n_p)
     nlp = {"x": V, "p": P, "f": F(V, P), "g": G(V, P)}
-    nlp["_callbacks"] = [F, G, H]  # callbacks must outlive the solver
-    nlp["_hess_lag"] = H
+    nlp["_callbacks"] = [F, G]  # callbacks must outlive the solver
+    if hasattr(evaluator, "eval_hess"):
+        H = _HessCallback("awe_hess_l", evaluator, convert, n_p)
+        nlp["_callbacks"].append(H)
+        nlp["_hess_lag"] = H
     return nlp
 
 
 def solver_options(nlp):
-    """nlpsol options that keep IPOPT's exact Hessian with the HIP Hessian kernel."""
+    """nlpsol options that keep IPOPT's exact Hessian with the HIP Hessian kernel (evaluators
+    without a Hessian kernel leave the Hessian to CasADi's default)."""
+    if "_hess_lag" not in nlp:
+        return {"expand": False}
     return {"hess_lag": nlp["_hess_lag"], "expand": False}
 
 

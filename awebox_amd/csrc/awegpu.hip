@@ -422,14 +422,10 @@ void ap2_interval_kernel(KArgs a) {
     // stage A, one (node, height) per thread: wind speed and density at the kite and at every
     // tether element midpoint, as functions of q_z; stage B, one (node, element, direction)
     // per thread: the element's drag along q0..2, dq0..2, diam_t
-#ifndef AWE_EXP_SKIP_PRE
     submodel_pass<D, NT>(a.cst, th, wn, pre, tang, tid);
-#endif
 
     // ---- phase 1: model, one node per half-wavefront, one colour per lane ------------------
-#ifndef AWE_EXP_SKIP_MODEL
     first_order_pass<D>(ct, wn, pre, tang, gval, dfl + tid, C, vt, th, a.cst, inv_h_tf, inv_tf, wave, lane);
-#endif
     __syncthreads();
 
     // ---- phase 2: objective directional derivatives (one lane per direction) -------------
@@ -441,7 +437,6 @@ void ap2_interval_kernel(KArgs a) {
     const double w_ureg = pcost[kCostURegularisation] / a.cst[AWE_C_NORM_U_REG];
     const double w_fict = pcost[kCostFictitious] / a.cst[AWE_C_NORM_FICTITIOUS];
     const double w_theta = pcost[kCostThetaRegularisation] / a.cst[AWE_C_NORM_THETA_REG];
-#ifndef AWE_EXP_SKIP_OBJ
     for (int n = 1 + wave; n < NN; n += W) {
         const int dir = lane;
         const double* tp = tang + toff(n);
@@ -494,7 +489,6 @@ void ap2_interval_kernel(KArgs a) {
             if (dir == 0) fnode[n] = wj * (psi * trk + xdr + oth) + cb * (bv * bv) + (1.0 - psi) * (cp * pv);
         }
     }
-#endif
     __syncthreads();
 
     // ---- phase 3: write-out ---------------------------------------------------------------
@@ -563,9 +557,6 @@ void ap2_interval_kernel(KArgs a) {
 #pragma unroll
     for (int s = 0; s < kSegs; ++s) {
         const int g0 = sg[3 * s], len = sg[3 * s + 1], lo = sg[3 * s + 2];
-#ifdef AWE_EXP_SKIP_GATHER
-        if (tid < 0)
-#endif
         for (int i = tid; i < len; i += NT) {
             const unsigned e = gl[lo + i];
             jac[g0 + i] = scl[e >> 16] * tang[e & 0xffffu];

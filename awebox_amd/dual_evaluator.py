@@ -195,6 +195,14 @@ class DualEvaluator:
                                                 _dptr(jac)))
         return {"f": f, "g": g, "grad_f": grad, "jac": jac}
 
+    def eval_f(self, V, P):
+        """Host arrays in: f [B] (the derivative kernel; there is no value-only kernel for this NLP)."""
+        return self.eval_nlp(V, P)["f"]
+
+    def eval_g(self, V, P):
+        """Host arrays in: g [B, n_g] (the derivative kernel)."""
+        return self.eval_nlp(V, P)["g"]
+
     # ---- CasADi nlpsol oracle names (one instance) -----------------------------------
     def _single(self, x, p):
         if self.batch != 1:

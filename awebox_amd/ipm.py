@@ -72,13 +72,27 @@ class IpmOptions:
     max_backtracks: int = 40
     max_soc: int = 4                 # second-order corrections per line search (IPOPT max_soc)
     kappa_soc: float = 0.99
-    kkt: str = "structured"          # "structured" (interval elimination + Schur) or "dense"
+    # IPOPT's bound relaxation: every finite bound of a free variable or an inequality row moves
+    # outward by min(constr_viol_tol, bound_relax_factor max(1, |b|)) before the solve
+    bound_relax_factor: float = 1e-8
+    kappa_d: float = 1e-5            # linear damping of variables bounded on one side only
+    constr_mult_init_max: float = 1e3  # cold start: least-square multipliers unless larger than this
+    # IPOPT's termination tests beyond the scaled error (unscaled quantities) and its
+    # "acceptable" termination after acceptable_iter consecutive acceptable iterations
+    constr_viol_tol: float = 1e-4
+    dual_inf_tol: float = 1.0
+    compl_inf_tol: float = 1e-4
+    acceptable_iter: int = 15
+    acceptable_constr_viol_tol: float = 1e-2
+    acceptable_dual_inf_tol: float = 1e10
+    acceptable_compl_inf_tol: float = 1e-2
     lu_backend: str = "awelu"        # interval-block LU: "awelu" (batched_lu.hip) or "torch" (rocSOLVER)
     separators: str = "btd"          # separator system: "dense" LU or "btd" (awebox_amd/btd.py block sweep)
     inertia: str = "exact"           # inertia correction: "curvature" test (Chiang & Zavala) or "exact" (IPOPT:
                                      # In(K) = In(K_II) + In(S) from symmetric eigenvalues of the blocks)
     profile: bool = False            # synchronise and time the solver's phases (IpmResult.timing)
     verbose: bool = False
+    callback: object = None          # callback(iteration, V [B, n_v] device tensor, stepped [B] bool)
 
 
 @dataclass
@@ -104,7 +118,7 @@ class DeviceNlp:
     B instances at once (the evaluator's batch): same structure (free set, inequality rows,
     bounds), per-instance P and scaling."""
 
-    def __init__(self, ev, P, lbx, ubx, lbg, ubg, device):
+    def __init__(self, ev, P, lbx, ubx, lbg, ubg, device, relax=0.0, relax_cap=1e-4):
         self.ev, self.dev = ev, device
         n_v, n_g = ev.n_v, ev.n_g
         P = np.atleast_2d(np.asarray(P, dtype=np.float64))
@@ -123,6 +137,13 @@ class DeviceNlp:
         # bounds of y = [x_free; s] (slack bounds are scaled per instance once c_scale is known)
         yl = np.concatenate([lbx[self.free], lbg[self.ineq]])
         yu = np.concatenate([ubx[self.free], ubg[self.ineq]])
+        # the original bounds (reported violations), then IPOPT's bound relaxation
+        # (TNLPAdapter: fixed variables and equality rows are not relaxed)
+        self.yl0, self.yu0 = yl.copy(), yu.copy()
+        if relax > 0.0:
+            with np.errstate(invalid="ignore"):
+                yl = np.where(np.isfinite(yl), yl - np.minimum(relax_cap, relax * np.maximum(1.0, np.abs(yl))), yl)
+                yu = np.where(np.isfinite(yu), yu + np.minimum(relax_cap, relax * np.maximum(1.0, np.abs(yu))), yu)
         self.yl = torch.tensor(np.tile(yl, (B, 1)), device=device)
         self.yu = torch.tensor(np.tile(yu, (B, 1)), device=device)
         self.has_l = torch.isfinite(self.yl)
@@ -266,10 +287,6 @@ def _dense_A(nlp, jv, N0, K):
     scol = n + torch.arange(mI, device=K.device)
     K[srow, scol] = -1.0
     K[scol, srow] = -1.0
-
-
-ZERO_PIVOT = 1e-30   # relative zero-pivot threshold of the inertia count: KKT pivots legitimately span
-                     # 1e-10 .. 1e10 at small mu, so only exactly singular columns count as zero
 
 
 ZERO_PIVOT = 1e-30   # relative zero-pivot threshold of the inertia count: KKT pivots legitimately span
@@ -483,12 +500,16 @@ class StructuredKKT:
     def matvec(self, x):
         return self._mv(self.vals, x)
 
-    def solve(self, rhs, refine=None, rtol=1e-12):
+    def solve(self, rhs, refine=None, rtol=1e-12, active=None):
         """Elimination solve with iterative refinement on the sparse residual, rhs [B, N] (or [N]).
         The interior pivots come from blocks that may be ill-conditioned even when K is not (an
         indefinite interior Hessian), so an instance's result is accepted once its backward error
         is small, ||K x - rhs|| <= rtol (||K|| ||x|| + ||rhs||) in the max norm; an instance that
-        does not get there is solved once by a dense LU of its assembled K."""
+        does not get there is solved once by a dense LU of its assembled K.  ``active`` ([B] bool,
+        numpy or torch) restricts refinement and the dense fallback to the instances whose result
+        the caller uses: the others (converged, failed, outside the current step) may hold a
+        near-singular K and are returned unrefined.  A singular fallback K yields non-finite
+        values for the caller's isfinite checks instead of an exception."""
         one = rhs.dim() == 1
         rhs = rhs.unsqueeze(0) if one else rhs
         if refine is None:
@@ -501,6 +522,9 @@ class StructuredKKT:
         x = self._solve(rhs)
         b_norm = rhs.abs().amax(dim=1)
         done = torch.zeros(rhs.shape[0], dtype=torch.bool, device=self.dev)
+        if active is not None:
+            done = ~torch.as_tensor(np.asarray(active) if not torch.is_tensor(active) else active,
+                                    dtype=torch.bool, device=self.dev).reshape(-1)
         for it in range(refine + 1):
             r = rhs - self.matvec(x)
             err = r.abs().amax(dim=1)
@@ -515,7 +539,8 @@ class StructuredKKT:
             self.n_dense += 1
             K = self.sc_dense.add_into(torch.zeros(self.N * self.N, dtype=torch.float64, device=self.dev),
                                        self.vals[b])
-            x[b] = torch.linalg.solve(K.view(self.N, self.N), rhs[b])
+            xb, info = torch.linalg.solve_ex(K.view(self.N, self.N), rhs[b])
+            x[b] = torch.where(info == 0, xb, torch.full_like(xb, float("nan")))
         return x[0] if one else x
 
     def _block_solve(self, B):
@@ -587,7 +612,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     dev = torch.device(device)
     P = np.atleast_2d(np.asarray(P, dtype=np.float64))
     B = P.shape[0]
-    nlp = DeviceNlp(ev, P, lbx, ubx, lbg, ubg, dev)
+    nlp = DeviceNlp(ev, P, lbx, ubx, lbg, ubg, dev, relax=opts.bound_relax_factor, relax_cap=opts.constr_viol_tol)
     n, mI, m, ny = nlp.n, nlp.mI, nlp.m, nlp.ny
     N = ny + m
     f64 = dict(dtype=torch.float64, device=dev)
@@ -647,7 +672,9 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
 
     # ---- per-instance state (host) ---------------------------------------------------------
     mu = np.full(B, opts.mu_init)
-    mu_floor = max(opts.mu_target, opts.tol / 10)
+    # IPOPT's MonotoneMuUpdate floor: max(mu_target, mu_min, min(tol, compl_inf_tol) / (barrier_tol_factor + 1))
+    mu_floor = max(opts.mu_target, 1e-11, min(opts.tol, opts.compl_inf_tol) / 11.0)
+    n_accept = np.zeros(B, dtype=np.int64)
     tau = np.maximum(opts.tau_min, 1.0 - mu)
     filt = [[] for _ in range(B)]
     c = nlp.constraints(g, y[:, n:])
@@ -666,6 +693,16 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     exact_inertia = opts.inertia == "exact" and (skkt.btd is not None or dev.type != "cuda")
     if skkt.btd is not None and dev.type == "cuda":
         skkt.force_btd = True
+    if not warm and opts.constr_mult_init_max > 0 and m:
+        # IPOPT's DefaultIterateInitializer: least-square constraint multipliers at the starting
+        # point, [I A^T; A 0] (w, lam) = (-(grad f - z_L + z_U), 0), kept only where
+        # max|lam| <= constr_mult_init_max (otherwise lam = 0)
+        skkt.factor(torch.zeros(B, len(nlp.h_keep), **f64), torch.ones(B, ny, **f64), jv, 0.0, mI)
+        sol = skkt.solve(torch.cat([-(torch.cat([grad, torch.zeros(B, mI, **f64)], 1) - zl + zu),
+                                    torch.zeros(B, m, **f64)], 1))
+        lam_ls = sol[:, ny:]
+        keep = torch.isfinite(lam_ls).all(1) & (lam_ls.abs().amax(1) <= opts.constr_mult_init_max)
+        lam = torch.where(keep[:, None], lam_ls, lam)
     timing = {}
 
     class _Phase:
@@ -690,11 +727,18 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         du = torch.where(hu, yu - yv, torch.ones_like(yv))
         return dl, du
 
+    # IPOPT's kappa_d damping: + kappa_d mu (y - y_L) for variables bounded below only, and
+    # + kappa_d mu (y_U - y) for those bounded above only, in the barrier function
+    lo_only = (hl & ~hu).to(torch.float64)
+    hi_only = (hu & ~hl).to(torch.float64)
+    damp_dir = lo_only - hi_only
+
     def barrier_phi(fv, yv, mu_t):
         dl, du = gaps(yv)
         lg = torch.where(hl, torch.log(dl), torch.zeros_like(dl)).sum(1) + \
             torch.where(hu, torch.log(du), torch.zeros_like(du)).sum(1)
-        return fv - mu_t * lg
+        dmp = (lo_only * dl).sum(1) + (hi_only * du).sum(1)
+        return fv - mu_t * lg + opts.kappa_d * mu_t * dmp
 
     def grad_y(gradv):
         return torch.cat([gradv, torch.zeros(B, mI, **f64)], 1)
@@ -712,11 +756,20 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
 
     nb = int(hl[0].sum().item() + hu[0].sum().item())
 
-    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_t):
+    cs_slack = nlp.c_scale[:, nlp.ineq_t]
+    gl0 = torch.tensor(nlp.yl0[n:], **f64)
+    gu0 = torch.tensor(nlp.yu0[n:], **f64)
+
+    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_t, damped=False, unscaled=False):
         """IPOPT's scaled optimality error per instance (host [B] arrays): total, dual, primal,
-        complementarity at barrier parameter mu_t ([B] tensor)."""
+        complementarity at barrier parameter mu_t ([B] tensor); ``damped`` adds the kappa_d term
+        (the barrier problem's error).  With ``unscaled`` also the unscaled dual infeasibility,
+        constraint violation (original bounds of the inequality rows) and complementarity that
+        IPOPT's termination tests compare with dual_inf_tol / constr_viol_tol / compl_inf_tol."""
         dl, du = gaps(yv)
         dual = grad_y(gradv) + A_T_lam(jvv, lamv) - zlv + zuv
+        if damped:
+            dual = dual + opts.kappa_d * mu_t[:, None] * damp_dir
         compl_l = torch.where(hl, dl * zlv - mu_t[:, None], torch.zeros_like(yv))
         compl_u = torch.where(hu, du * zuv - mu_t[:, None], torch.zeros_like(yv))
         zsum = zlv.abs().sum(1) + zuv.abs().sum(1)
@@ -724,9 +777,25 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         s_c = torch.clamp(zsum / max(1, nb), min=opts.s_max) / opts.s_max
         e_dual = dual.abs().amax(1) / s_d
         e_pr = cv.abs().amax(1) if m else torch.zeros(B, **f64)
-        e_c = torch.maximum(compl_l.abs().amax(1), compl_u.abs().amax(1)) / s_c
-        e = torch.stack([torch.maximum(torch.maximum(e_dual, e_pr), e_c), e_dual, e_pr, e_c]).cpu().numpy()
-        return e[0], e[1], e[2], e[3]
+        compl = torch.maximum(compl_l.abs().amax(1), compl_u.abs().amax(1))
+        e_c = compl / s_c
+        parts = [torch.maximum(torch.maximum(e_dual, e_pr), e_c), e_dual, e_pr, e_c]
+        if unscaled:
+            osc = nlp.obj_scale
+            u_dual = torch.maximum(dual[:, :n].abs().amax(1) if n else torch.zeros(B, **f64),
+                                   (dual[:, n:] * cs_slack).abs().amax(1) if mI else torch.zeros(B, **f64)) / osc
+            c_u = cv / nlp.c_scale
+            eq_mask = torch.ones(m, dtype=torch.bool, device=dev)
+            eq_mask[nlp.ineq_t] = False
+            u_pr = torch.where(eq_mask, c_u.abs(), torch.zeros_like(c_u)).amax(1) if m else torch.zeros(B, **f64)
+            if mI:
+                gI = (cv[:, nlp.ineq_t] + yv[:, n:]) / cs_slack         # g of the inequality rows, unscaled
+                vI = torch.maximum(torch.where(torch.isfinite(gu0), gI - gu0, torch.zeros_like(gI)),
+                                   torch.where(torch.isfinite(gl0), gl0 - gI, torch.zeros_like(gI)))
+                u_pr = torch.maximum(u_pr, torch.clamp(vI, min=0.0).amax(1))
+            parts += [u_dual, u_pr, compl / osc]
+        e = torch.stack(parts).cpu().numpy()
+        return tuple(e)
 
     def ftb(v, dv, mask_pos, tau_t):
         """Fraction-to-the-boundary step per instance: min(1, min_i -tau v_i / dv_i) (host [B])."""
@@ -771,7 +840,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 good = ~done
             if good.any():
                 with _Phase("kkt_solve"):
-                    sol = skkt.solve(rhs)
+                    sol = skkt.solve(rhs, active=good)
                 fin = torch.isfinite(sol).all(1).cpu().numpy()
                 if not exact_inertia:
                     dy = sol[:, :ny]
@@ -894,7 +963,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 c_soc = torch.where(st, dev_b(alpha)[:, None] * c_cur + ct,
                                     torch.where(ctn, dev_b(a_s)[:, None] * c_soc + ct, c_soc))
                 with _Phase("kkt_solve"):
-                    sol = skkt.solve(torch.cat([rhs_top, -c_soc], 1))
+                    sol = skkt.solve(torch.cat([rhs_top, -c_soc], 1), active=start_soc | cont_soc)
                 fin = torch.isfinite(sol).all(1).cpu().numpy()
                 upd = (start_soc | cont_soc) & fin
                 sel = dev_b(upd)[:, None] > 0
@@ -937,7 +1006,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             dlv, duv = gaps(yv)
             sig = torch.where(hl, 1.0 / dlv ** 2, torch.zeros_like(yv)) + torch.where(hu, 1.0 / duv ** 2, torch.zeros_like(yv))
             skkt.factor(hv_zero, sig + 1e-8, jv_c, 0.0, mI)
-            sol = skkt.solve(-torch.cat([torch.zeros(B, ny, **f64), cv], 1))
+            sol = skkt.solve(-torch.cat([torch.zeros(B, ny, **f64), cv], 1), active=live)
             fin = torch.isfinite(sol).all(1).cpu().numpy()
             live &= fin
             dyv = torch.where(torch.isfinite(sol[:, :ny]), sol[:, :ny], torch.zeros_like(sol[:, :ny]))
@@ -976,15 +1045,25 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     it = 0
     while it < opts.max_iter:
         c = nlp.constraints(g, y[:, n:])
-        kkt_err, e_d, e_p, e_c = errors(grad, jv, c, y, lam, zl, zu, torch.full((B,), opts.mu_target, **f64))
-        conv = active & (kkt_err <= opts.tol)
+        kkt_err, e_d, e_p, e_c, u_d, u_p, u_c = errors(grad, jv, c, y, lam, zl, zu,
+                                                       torch.full((B,), opts.mu_target, **f64), unscaled=True)
+        # IPOPT's OptimalityErrorConvergenceCheck: the scaled error and the unscaled tests
+        conv = active & (kkt_err <= opts.tol) & (u_d <= opts.dual_inf_tol) & (u_p <= opts.constr_viol_tol) & \
+            (u_c <= opts.compl_inf_tol)
         status[conv] = "solve_succeeded"
         active &= ~conv
+        acceptable = (kkt_err <= opts.acceptable_tol) & (u_d <= opts.acceptable_dual_inf_tol) & \
+            (u_p <= opts.acceptable_constr_viol_tol) & (u_c <= opts.acceptable_compl_inf_tol)
+        n_accept = np.where(active & acceptable, n_accept + 1, 0)
+        if opts.acceptable_iter > 0:
+            acc_stop = active & (n_accept >= opts.acceptable_iter)
+            status[acc_stop] = "solved_to_acceptable_level"
+            active &= ~acc_stop
         if not active.any():
             break
         # barrier update (monotone), per instance
         for _ in range(50):
-            e_mu = errors(grad, jv, c, y, lam, zl, zu, dev_b(mu))[0]
+            e_mu = errors(grad, jv, c, y, lam, zl, zu, dev_b(mu), damped=True)[0]
             upd = active & (e_mu <= opts.kappa_eps * mu) & (mu > mu_floor * 1.0000001)
             if not upd.any():
                 break
@@ -999,7 +1078,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         mu_d = dev_b(mu)
         sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
         grad_phi = grad_y(grad) - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
-            torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y))
+            torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y)) + opts.kappa_d * mu_d[:, None] * damp_dir
         theta = c.abs().sum(1).cpu().numpy()
         phi = barrier_phi(f, y, mu_d).cpu().numpy()
         rhs_top = -(grad_phi + A_T_lam(jv, lam))
@@ -1071,7 +1150,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             # IPOPT after restoration: constraint multipliers by least squares on the dual
             # infeasibility, [I A^T; A 0] (w, lam) = (-(grad f - z_L + z_U), 0)
             skkt.factor(hv_zero, torch.ones(B, ny, **f64), jv, 0.0, mI)
-            sol = skkt.solve(torch.cat([-(grad_y(grad) - zl + zu), torch.zeros(B, m, **f64)], 1))
+            sol = skkt.solve(torch.cat([-(grad_y(grad) - zl + zu), torch.zeros(B, m, **f64)], 1), active=rest_ok)
             fin = torch.isfinite(sol).all(1)
             sel = (dev_b(rest_ok)[:, None] > 0) & fin[:, None]
             lam = torch.where(sel, sol[:, ny:], lam)
@@ -1086,6 +1165,10 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                        delta_w=float(dw_rec[b]) if acc_all[b] else -1.0,
                        backtracks=int(nback[b]), soc=int(nsoc[b]))
             logs[b].append(rec)
+        if opts.callback is not None:
+            # IPOPT's intermediate callback (awebox's iteration_callback, opti/preparation.py:305-313):
+            # the full V of every instance after the iteration, and which instances stepped
+            opts.callback(it, nlp.full_x(y[:, :n]), stepped.copy())
         if opts.verbose:
             shown = np.where(active | (pending & ~rest_ok))[0]
             for b0 in (shown if B <= 4 else shown[:1]):

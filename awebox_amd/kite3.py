@@ -276,6 +276,46 @@ class MpcLayout:
         return lb, ub
 
 
+MPC_P_ENTRIES = ("x0", "ref", "u_ref", "Q", "R", "P")   # pmpc.py:166-186 (tracking cost), in order
+
+
+def pack_p_from_reference(get, lay: MpcLayout) -> np.ndarray:
+    """The MPC parameter vector in this library's flat layout from Pmpc's parameter struct, read
+    entry by entry by name: ``p = struct_symMX([x0 (nx), ref (the MPC trial's V struct), u_ref,
+    Q (nx), R (nu), P (nx)])`` (pmpc.py:166-186, cost_type 'tracking').  ``get((name,))`` returns
+    the entry; with a casadi.tools struct ``p_num``: ``get = lambda path: np.asarray(p_num[path])``.
+    A missing name raises KeyError; a wrong size raises ValueError."""
+    sizes = {"x0": (lay.p_x0, NX), "ref": (lay.p_ref, lay.n_v), "u_ref": (lay.p_u_ref, 1),
+             "Q": (lay.p_Q, NX), "R": (lay.p_R, NU), "P": (lay.p_P, NX)}
+    p = np.zeros(lay.n_p)
+    for name in MPC_P_ENTRIES:
+        off, size = sizes[name]
+        v = np.asarray(get((name,)), dtype=np.float64).ravel()
+        if v.size != size:
+            raise ValueError(f"MPC parameter {name} has {v.size} values, expected {size}")
+        p[off:off + size] = v
+    return p
+
+
+def p_fun(p: np.ndarray, lay: MpcLayout) -> dict:
+    """Restatement of ``Pmpc.__create_P_fun`` (pmpc.py:641-689): the parameter P of the MPC trial's
+    NLP that the MPC constraints ``g = nlp.g_fun(V, P_fun(p))`` (:190) are evaluated with, as
+    {entry: value} by the names the reference's loop fills:
+
+    * ``('p', 'ref')``: the trial's V shape, zero except x[0] = p.x0 and x[N] = p.ref's x[N]
+      (:660-671) -- x[0] feeds the initial-condition rows (operation.py:303-326);
+    * ``('theta0', 'wind', 'u_ref')``: p.u_ref (:675-676); every other theta0 entry is the model
+      parameter of p_fix_num (:677-682) -- constant here (``Kite3Constants.consts``);
+    * everything else (``('p', 'weights')``, ``('cost', *)``): 0 (:684-685).
+
+    The MPC kernel reads x0 and u_ref from p directly, which is this map composed with g_fun."""
+    p = np.asarray(p, dtype=np.float64).ravel()
+    ref = np.zeros(lay.n_v)
+    ref[lay.x(0)] = p[lay.p_x0:lay.p_x0 + NX]
+    ref[lay.x(lay.n_k)] = p[lay.p_ref + lay.x(lay.n_k)]
+    return {("p", "ref"): ref, ("p", "weights"): np.zeros(NW), ("theta0", "wind", "u_ref"): p[lay.p_u_ref:lay.p_u_ref + 1]}
+
+
 def fict_columns(lay: MpcLayout) -> np.ndarray:
     """V indices of the fictitious forces f_fict10 of every interval's zoh control."""
     o = W_OFF[("u", "f_fict10")][0] - NX - NX                      # offset inside u

@@ -8,9 +8,10 @@ solver sees:
 * variable bounds (kite3.variable_bounds: system bounds on x[1..N], u, z; x[0] released; f_fict,
   theta, phi, xi fixed) and the path inequalities (tether stress, acceleration; released at k = 0,
   pmpc.py:125-131) as inequality rows with slacks;
-* the exact Hessian of the Lagrangian (the reference's IPOPT default) from coloured central
-  differences of the HIP MPC evaluator's exact gradients (fd_hessian.FdHessian, terminal-cost
-  columns included), one batched launch per Hessian;
+* the Hessian of the Lagrangian -- IPOPT's default is the exact one (pmpc.py:193-217,
+  default.py:323) -- approximated by coloured central differences of the HIP MPC evaluator's
+  exact gradients (fd_hessian.FdHessian, terminal-cost columns included, agreement with the
+  oracle's autograd Hessian to 1e-6), one batched launch per Hessian;
 * ``homotopy_warmstart`` (mpc_closed_loop.py:69): a 2-iteration pre-solve at mu = 1e-3
   (``mu_init = mu_target = 1e-3``, ``tol = 1e-4``, ``max_iter = 2``, pmpc.py:206-212) whose
   primal point starts the main solve (``mu_init = 1e-3``, ``tol = 1e-6``, pmpc.py:199-207);

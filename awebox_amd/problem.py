@@ -490,7 +490,30 @@ def collocation(d: int = 4):
     return coefficients(d, "radau")
 
 
-def pack_p_from_reference(get, layout: NlpLayout) -> np.ndarray:
+def sd_path(coeff: str, inp: str) -> tuple:
+    """P path of a stability derivative: ``('theta0', 'aero', coeff, input)``.  model_funcs.py:
+    483-493 appends ('params', 'aero', deriv_name, input_name) for every derivative of the kite
+    data (all flagged 's', default.py:599), and stability_derivatives.py:241-243 reads them back
+    as ``parameters['theta0', 'aero', coeff_name, input_name]`` -- there is no 'stab_derivs' level."""
+    return ("theta0", "aero", coeff, inp)
+
+
+def stab_derivs_present(get) -> dict:
+    """{coeff: [inputs]} of the stability derivatives in the reference's P: the reference keeps only
+    the (coeff, input) pairs its kite data define (stability_derivatives.py:230-249 tests the
+    label); a pair is absent exactly when ``get`` raises KeyError."""
+    out = {}
+    for c in SD_COEFFS:
+        for i in SD_INPUTS:
+            try:
+                get(sd_path(c, i))
+            except KeyError:
+                continue
+            out.setdefault(c, []).append(i)
+    return out
+
+
+def pack_p_from_reference(get, layout, stab_derivs_absent: dict | None = None) -> np.ndarray:
     """P in this library's flat layout from the reference's P struct, read entry by entry by name.
 
     The reference hands IPOPT ``p = P(p_fix_num)`` with ``P = struct([p: [ref (the V struct),
@@ -498,13 +521,26 @@ def pack_p_from_reference(get, layout: NlpLayout) -> np.ndarray:
     (ocp/discretization.py:129-179; theta0 = struct_op.generate_nested_dict_struct(options['params']),
     mdl/system.py:417-432).  ``get(path)`` returns the entry at ``path`` as an array, e.g.
     ``get(('p', 'ref'))``, ``get(('cost', 'power'))``, ``get(('theta0', 'wind', 'u_ref'))`` or
-    ``get(('theta0', 'aero', 'stab_derivs', 'CX', 'alpha'))``; with a casadi.tools struct
-    ``P_num``: ``get = lambda path: np.asarray(P_num[path]).ravel()``.  The flat order of the
-    theta0 tree is never used, only the names of the entries the evaluator reads; a stability
-    derivative absent from the reference's tree (KeyError) is zero, as in its data file."""
+    ``get(('theta0', 'aero', 'CX', 'alpha'))`` (``sd_path``); with a casadi.tools struct ``P_num``:
+    ``get = lambda path: np.asarray(P_num[path]).ravel()``.  The flat order of the theta0 tree is
+    never used, only the names of the entries the evaluator reads.
+
+    ``layout`` is the AP2 ``NlpLayout`` or the multi-kite ``dual.MultiLayout`` (same P structure,
+    its own V and weight sizes).  Every entry is required: a missing name raises KeyError --
+    except the stability derivatives listed in ``stab_derivs_absent`` ({coeff: [inputs]}), which
+    the kite data does not define and which are zero in the model (stability_derivatives.py:
+    166-200 sums only the derivatives present).  By default that list is the complement of
+    ``AP2_STAB_DERIVS`` (ampyx_data.py:121-223)."""
+    if stab_derivs_absent is None:
+        stab_derivs_absent = {c: [i for i in SD_INPUTS if i not in AP2_STAB_DERIVS.get(c, {})]
+                              for c in SD_COEFFS}
+    nw = layout.p_cost - layout.p_weights
     p = np.zeros(layout.n_p)
     p[layout.p_ref:layout.p_ref + layout.n_v] = np.asarray(get(("p", "ref")), dtype=np.float64).ravel()
-    p[layout.p_weights:layout.p_weights + NW] = np.asarray(get(("p", "weights")), dtype=np.float64).ravel()
+    w = np.asarray(get(("p", "weights")), dtype=np.float64).ravel()
+    if w.size != nw:
+        raise ValueError(f"p.weights has {w.size} values, expected {nw}")
+    p[layout.p_weights:layout.p_weights + nw] = w
     for i, name in enumerate(COST_NAMES):
         p[layout.p_cost + i] = float(np.asarray(get(("cost", name))).ravel()[0])
     th = np.zeros(NTHETA0)
@@ -514,9 +550,12 @@ def pack_p_from_reference(get, layout: NlpLayout) -> np.ndarray:
             for ci, cname in enumerate(SD_COEFFS):
                 for ii, iname in enumerate(SD_INPUTS):
                     try:
-                        v = np.asarray(get(("theta0", "aero", "stab_derivs", cname, iname)), dtype=np.float64).ravel()
+                        v = np.asarray(get(sd_path(cname, iname)), dtype=np.float64).ravel()
                     except KeyError:
-                        continue
+                        if iname in stab_derivs_absent.get(cname, ()):
+                            continue
+                        raise KeyError(f"stability derivative {sd_path(cname, iname)} missing from the "
+                                       f"reference P (not listed as absent from the kite data)") from None
                     if len(v) > SD_MAXLEN:
                         raise ValueError(f"stability derivative {cname}.{iname} has {len(v)} > {SD_MAXLEN} terms")
                     b = o + (ci * len(SD_INPUTS) + ii) * SD_MAXLEN
@@ -530,12 +569,13 @@ def pack_p_from_reference(get, layout: NlpLayout) -> np.ndarray:
     return p
 
 
-def reference_p_entries(P: np.ndarray, layout: NlpLayout) -> dict:
+def reference_p_entries(P: np.ndarray, layout) -> dict:
     """The inverse view: {path: array} of a flat P under the reference's entry names (the paths
     pack_p_from_reference reads); stability derivatives with their used terms only."""
     P = np.asarray(P, dtype=np.float64)
+    nw = layout.p_cost - layout.p_weights
     out = {("p", "ref"): P[layout.p_ref:layout.p_ref + layout.n_v].copy(),
-           ("p", "weights"): P[layout.p_weights:layout.p_weights + NW].copy()}
+           ("p", "weights"): P[layout.p_weights:layout.p_weights + nw].copy()}
     for i, name in enumerate(COST_NAMES):
         out[("cost", name)] = np.array([P[layout.p_cost + i]])
     th = P[layout.p_theta0:layout.p_theta0 + NTHETA0]
@@ -547,7 +587,7 @@ def reference_p_entries(P: np.ndarray, layout: NlpLayout) -> dict:
                     vals = AP2_STAB_DERIVS.get(cname, {}).get(iname)
                     if vals:
                         b = o + (ci * len(SD_INPUTS) + ii) * SD_MAXLEN
-                        out[("theta0", "aero", "stab_derivs", cname, iname)] = th[b:b + len(vals)].copy()
+                        out[sd_path(cname, iname)] = th[b:b + len(vals)].copy()
         else:
             out[("theta0",) + tuple(name.split("."))] = th[o:o + size].copy()
     return out

@@ -163,69 +163,100 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     res_o = torch.full((per, N_OUT), float("nan"), dtype=torch.float64, device=coll_dev)
     prev = None
     t_rank = time.perf_counter()
-    if mode == "fan" and my_u:
-        # the reference's sweeping warm start, fanned out: the shard's first point runs the full
-        # homotopy, then every other point of the shard is warm-started from that solution (the
-        # final homotopy step's costs and bounds), all of them in one batched solve
-        done = ("solve_succeeded", "solved_to_acceptable_level")
+    done = ("solve_succeeded", "solved_to_acceptable_level")
+    failures = (RuntimeError, ValueError, FloatingPointError, ArithmeticError)
+
+    def fail(rows, us, exc):
+        # a failed solve must not leave the other ranks waiting in the gather below: its points
+        # are reported with ok = False and NaN outputs
+        print(f"[rank {rank}] u_ref={[round(float(u), 3) for u in us]} failed: {exc}", flush=True)
+        for i, u in zip(rows, us):
+            res_v[i] = torch.tensor(v0, device=coll_dev)
+            res_o[i] = torch.tensor([u, float("nan"), float("nan"), 0.0, 0.0, float("nan")], device=coll_dev)
+
+    def run_batch(rows, us):
+        """Independent trials side by side: the full homotopy for every point of ``us``."""
         t0 = time.perf_counter()
-        ev1 = make_evaluator(consts, 1)
-        V0, summary, out0, res0 = prob.optimize(ev1, opts, device, v0, my_u[0])
-        it0 = sum(r["iterations"] for r in summary)
-        ok0 = all(r["status"] in done for r in summary)
-        el0 = time.perf_counter() - t0
-        res_v[0] = torch.tensor(V0, device=coll_dev)
-        res_o[0] = torch.tensor([my_u[0], out0["avg_power_W"], out0["period_s"], it0, float(ok0), el0], device=coll_dev)
-        if verbose:
-            print(f"[rank {rank}] u_ref={my_u[0]:.3f} P={out0['avg_power_W']:.1f} W T={out0['period_s']:.2f} s "
-                  f"iters={it0} ok={ok0} {el0:.1f} s", flush=True)
-            if res0.timing:
-                print(f"[rank {rank}] first point, final step timing {res0.timing}", flush=True)
-        rest = my_u[1:]
-        if rest:
-            del ev1
-            t1 = time.perf_counter()
-            final = prob.final_step(v0)
-            lbg, ubg = lay.g_bounds()
-            evb = make_evaluator(consts, len(rest))
-            P = np.stack([prob.pack_p(v0, final.cost_step, u) for u in rest])
-            rb = len(rest)
-            res = solve_batch(evb, P, np.tile(res0.x, (rb, 1)), final.lbx, final.ubx, lbg, ubg,
-                              lam0=np.tile(res0.lam_g, (rb, 1)), zl0=np.tile(res0.zl, (rb, 1)),
-                              zu0=np.tile(res0.zu, (rb, 1)), opts=hippo_options("final", opts), device=device)
-            el1 = time.perf_counter() - t1
-            if verbose and res[0].timing:
-                print(f"[rank {rank}] batched warm start timing {res[0].timing}", flush=True)
-            for i, (u, r) in enumerate(zip(rest, res)):
-                out = prob.outputs(r.x)
-                res_v[1 + i] = torch.tensor(r.x, device=coll_dev)
-                res_o[1 + i] = torch.tensor([u, out["avg_power_W"], out["period_s"], r.iterations,
-                                             float(r.status in done), el1], device=coll_dev)
-                if verbose:
-                    print(f"[rank {rank}] u_ref={u:.3f} P={out['avg_power_W']:.1f} W T={out['period_s']:.2f} s "
-                          f"iters={r.iterations} ok={r.status in done} (batched warm start, {el1:.1f} s)", flush=True)
-        my_u = []
-    if mode == "batch" and my_u:
-        done = ("solve_succeeded", "solved_to_acceptable_level")
-        t0 = time.perf_counter()
-        evb = make_evaluator(consts, len(my_u))
-        Vb, summary, outs, _ = prob.optimize_batch(evb, opts, device, v0, my_u, verbose=verbose)
+        try:
+            evb = make_evaluator(consts, len(us))
+            Vb, summary, outs, _ = prob.optimize_batch(evb, opts, device, v0, us, verbose=verbose)
+        except failures as exc:
+            fail(rows, us, exc)
+            return
         el = time.perf_counter() - t0
-        for i, u in enumerate(my_u):
+        for i, (row, u) in enumerate(zip(rows, us)):
             iters = sum(r["iterations"][i] for r in summary)
             ok = all(r["status"][i] in done for r in summary)
-            res_v[i] = torch.tensor(Vb[i], device=coll_dev)
-            res_o[i] = torch.tensor([u, outs[i]["avg_power_W"], outs[i]["period_s"], iters, float(ok), el],
-                                    device=coll_dev)
+            res_v[row] = torch.tensor(Vb[i], device=coll_dev)
+            res_o[row] = torch.tensor([u, outs[i]["avg_power_W"], outs[i]["period_s"], iters, float(ok), el],
+                                      device=coll_dev)
             if verbose:
                 print(f"[rank {rank}] u_ref={u:.3f} P={outs[i]['avg_power_W']:.1f} W T={outs[i]['period_s']:.2f} s "
                       f"iters={iters} ok={ok}", flush=True)
+
+    if mode == "fan" and my_u:
+        # the reference's sweeping warm start, fanned out: the shard's first point runs the full
+        # homotopy, then every other point of the shard is warm-started from that solution (the
+        # final homotopy step's costs and bounds), all of them in one batched solve.  If the first
+        # point does not converge, the rest run as independent batched homotopies instead.
+        t0 = time.perf_counter()
+        res0, ok0 = None, False
+        try:
+            ev1 = make_evaluator(consts, 1)
+            V0, summary, out0, res0 = prob.optimize(ev1, opts, device, v0, my_u[0])
+            del ev1
+            it0 = sum(r["iterations"] for r in summary)
+            ok0 = all(r["status"] in done for r in summary)
+            el0 = time.perf_counter() - t0
+            res_v[0] = torch.tensor(V0, device=coll_dev)
+            res_o[0] = torch.tensor([my_u[0], out0["avg_power_W"], out0["period_s"], it0, float(ok0), el0],
+                                    device=coll_dev)
+            if verbose:
+                print(f"[rank {rank}] u_ref={my_u[0]:.3f} P={out0['avg_power_W']:.1f} W T={out0['period_s']:.2f} s "
+                      f"iters={it0} ok={ok0} {el0:.1f} s", flush=True)
+                if res0.timing:
+                    print(f"[rank {rank}] first point, final step timing {res0.timing}", flush=True)
+        except failures as exc:
+            fail([0], my_u[:1], exc)
+        rest = my_u[1:]
+        if rest and not ok0:
+            run_batch(list(range(1, len(my_u))), rest)
+        elif rest:
+            t1 = time.perf_counter()
+            final = prob.final_step(v0)
+            lbg, ubg = lay.g_bounds()
+            rb = len(rest)
+            try:
+                evb = make_evaluator(consts, rb)
+                P = np.stack([prob.pack_p(v0, final.cost_step, u) for u in rest])
+                res = solve_batch(evb, P, np.tile(res0.x, (rb, 1)), final.lbx, final.ubx, lbg, ubg,
+                                  lam0=np.tile(res0.lam_g, (rb, 1)), zl0=np.tile(res0.zl, (rb, 1)),
+                                  zu0=np.tile(res0.zu, (rb, 1)), opts=hippo_options("final", opts), device=device)
+            except failures as exc:
+                fail(list(range(1, len(my_u))), rest, exc)
+                res = None
+            el1 = time.perf_counter() - t1
+            if res is not None:
+                if verbose and res[0].timing:
+                    print(f"[rank {rank}] batched warm start timing {res[0].timing}", flush=True)
+                for i, (u, r) in enumerate(zip(rest, res)):
+                    out = prob.outputs(r.x)
+                    res_v[1 + i] = torch.tensor(r.x, device=coll_dev)
+                    res_o[1 + i] = torch.tensor([u, out["avg_power_W"], out["period_s"], r.iterations,
+                                                 float(r.status in done), el1], device=coll_dev)
+                    if verbose:
+                        print(f"[rank {rank}] u_ref={u:.3f} P={out['avg_power_W']:.1f} W T={out['period_s']:.2f} s "
+                              f"iters={r.iterations} ok={r.status in done} (batched warm start, {el1:.1f} s)",
+                              flush=True)
+        my_u = []
+    if mode == "batch" and my_u:
+        run_batch(list(range(len(my_u))), my_u)
         my_u = []
     for i, u in enumerate(my_u):
         t0 = time.perf_counter()
         try:
             V, out, iters, ok, prev = point_solver(u, prev)
-        except (RuntimeError, ValueError, FloatingPointError) as exc:
+        except failures as exc:
             # a failed point must not leave the other ranks waiting in the gather below
             print(f"[rank {rank}] u_ref={u:.3f} failed: {exc}", flush=True)
             V, out, iters, ok, prev = v0, {"avg_power_W": float("nan"), "period_s": float("nan")}, 0, False, None
@@ -276,9 +307,11 @@ def main():
     ap.add_argument("--profile", action="store_true", help="phase timings of the interior-point solver")
     ap.add_argument("--separators", choices=["dense", "btd"], default="btd",
                     help="separator solve of the structured KKT (awebox_amd/btd.py for btd)")
-    ap.add_argument("--mode", choices=["chain", "batch", "fan"], default="fan",
-                    help="chain: warm-start chain per shard (the reference's sweep); batch: the shard's points "
-                         "as one batched homotopy; fan: homotopy for the first point, batched warm start for the rest")
+    ap.add_argument("--mode", choices=["chain", "batch", "fan"], default="chain",
+                    help="chain (default): the reference's sweeping warm start (sweep.py:154-172) within each "
+                         "shard; batch: independent trials, the shard's points as one batched homotopy; fan "
+                         "(throughput, opt-in): homotopy for the first point, batched warm start for the rest -- "
+                         "results then depend on how the points are sharded")
     ap.add_argument("--grid", type=int, default=0,
                     help="take the points from linspace(u-min, u-max, GRID) (config 4: 64), the first --points of it")
     args = ap.parse_args()

@@ -20,14 +20,15 @@ def hippo_options(label: str, base: IpmOptions | None = None) -> IpmOptions:
     """awebox's hippo strategy (preparation.py:285-323, default.py:324-351): the initial and
     intermediate homotopy steps stop at the barrier parameter mu_target = 1e-2 with tol 1e-4
     (initial: mu_init 1, cold start; middle: mu_init 1e-2, warm start); the final step starts at
-    mu_init 1e-2 and converges to tol 1e-8 (mu_target 0)."""
+    mu_init 1e-2 and converges to tol 1e-8 (mu_target 0).  The hippo steps set IPOPT's
+    acceptable_iter to 5 (acceptable_iter_hippo); the final step keeps IPOPT's default 15."""
     import dataclasses
     base = base or IpmOptions()
     if label.startswith("initial"):
-        return dataclasses.replace(base, mu_init=1.0, mu_target=1e-2, tol=1e-4)
+        return dataclasses.replace(base, mu_init=1.0, mu_target=1e-2, tol=1e-4, acceptable_iter=5)
     if label.startswith("final"):
         return dataclasses.replace(base, mu_init=1e-2, mu_target=0.0, tol=1e-8)
-    return dataclasses.replace(base, mu_init=1e-2, mu_target=1e-2, tol=1e-4)
+    return dataclasses.replace(base, mu_init=1e-2, mu_target=1e-2, tol=1e-4, acceptable_iter=5)
 
 
 def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device="cuda",

@@ -540,7 +540,7 @@ def pmpc_block(c, B, dev, dist, world, steps=3, warmup=1):
             "tracking_error_max": float(out["tracking_error"].max()),
             "reference": REFERENCE_NOTE,
             "solver": "batched IPM (mu_init 1e-3, tol 1e-6, 2-iteration homotopy pre-solve), bounds and path "
-                      "inequalities, exact Hessian by coloured central differences of the HIP gradient"}
+                      "inequalities, Hessian of the Lagrangian by coloured central differences of the exact HIP gradient"}
 
 
 SWEEP_GRID = 64       # config 4: u_ref = linspace(5, 8, 64), 8 contiguous points per GPU
@@ -595,8 +595,8 @@ def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
     {1:0, 2:1, 3:1}, N=20 d=4 as in the example, single_reelout), each GPU's shard of
     u_ref = linspace(5, 8, 64): `per_gpu` contiguous points (weak scaling), template broadcast / seed
     scatter / solution gather over RCCL; per shard the homotopy for the first point and one batched
-    warm-started solve for the rest (the HIP dual-kite evaluator, coloured central-difference
-    Hessian, exact-inertia interior point).  Timed by run_sweep between barriers, max over ranks."""
+    warm-started solve for the rest (the HIP dual-kite evaluator, the exact Hessian kernel
+    dual_hess_kernel, exact-inertia interior point).  Timed by run_sweep between barriers, max over ranks."""
     import torch
 
     from awebox_amd.dual_homotopy import make_evaluator

@@ -234,3 +234,36 @@ def test_mpc_nonfinite_is_an_error(gpu):
     ev = MpcEvaluator(c, batch=1)
     with pytest.raises(AwegpuError):
         ev.eval_nlp(V, p)
+
+
+def test_mpc_p_from_reference_and_p_fun():
+    """The MPC boundary: Pmpc's parameter struct read by name (pmpc.py:166-186) packs to the flat p;
+    and the constraints depend on p only through the restated P_fun (pmpc.py:641-689): changing
+    the tracking reference (except x[N]), Q, R and P leaves g unchanged, the initial-condition rows
+    are x[0] - P_fun(p).p.ref.x[0], and u_ref enters through theta0.wind.u_ref."""
+    c, lay, orc = _setup(n_k=3, d=2)
+    V, p = k3.batch_instance(c, lay, 1, 4)
+    named = {("x0",): p[lay.p_x0:lay.p_x0 + k3.NX], ("ref",): p[lay.p_ref:lay.p_ref + lay.n_v],
+             ("u_ref",): p[lay.p_u_ref:lay.p_u_ref + 1], ("Q",): p[lay.p_Q:lay.p_Q + k3.NX],
+             ("R",): p[lay.p_R:lay.p_R + k3.NU], ("P",): p[lay.p_P:lay.p_P + k3.NX]}
+    assert np.array_equal(k3.pack_p_from_reference(named.__getitem__, lay), p)
+    with pytest.raises(KeyError):
+        k3.pack_p_from_reference({k: v for k, v in named.items() if k != ("Q",)}.__getitem__, lay)
+    Pf = k3.p_fun(p, lay)
+    assert np.array_equal(Pf[("p", "ref")][lay.x(0)], p[lay.p_x0:lay.p_x0 + k3.NX])
+    assert np.count_nonzero(Pf[("p", "ref")]) <= 2 * k3.NX
+    g = orc.nlp_g(V, p, lay).numpy()
+    np.testing.assert_array_equal(g[lay.g_init()], V[lay.x(0)] - Pf[("p", "ref")][lay.x(0)])
+    p2 = p.copy()
+    rng = np.random.default_rng(5)
+    keep = np.zeros(lay.n_v, dtype=bool)
+    keep[lay.x(lay.n_k)] = True
+    p2[lay.p_ref:lay.p_ref + lay.n_v] = np.where(keep, p2[lay.p_ref:lay.p_ref + lay.n_v], rng.standard_normal(lay.n_v))
+    p2[lay.p_Q:] = rng.uniform(0.5, 2.0, lay.n_p - lay.p_Q)
+    for key in Pf:
+        np.testing.assert_array_equal(k3.p_fun(p2, lay)[key], Pf[key])
+    np.testing.assert_array_equal(orc.nlp_g(V, p2, lay).numpy(), g)
+    p3 = p.copy()
+    p3[lay.p_u_ref] += 1.0
+    assert k3.p_fun(p3, lay)[("theta0", "wind", "u_ref")][0] == p[lay.p_u_ref] + 1.0
+    assert not np.allclose(orc.nlp_g(V, p3, lay).numpy(), g)

@@ -102,28 +102,88 @@ def test_initial_guess_is_a_closed_circular_orbit():
     assert vb[0] == v0[0] and not np.allclose(vb[20:], v0[20:])
 
 
+REF_PARAMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_params.json")
+
+
+def _reference_theta0():
+    """{theta0 path: value} of the reference's parameter tree for the AP2 example, as extracted from
+    the reference's sources by tests/golden/make_reference_params.py (names, values, file:line)."""
+    import json
+    rows = json.load(open(REF_PARAMS))["entries"]
+    return {tuple(r["path"]): (None if r["value"] is None else np.asarray(r["value"])) for r in rows}
+
+
+def _reference_getter(tree):
+    def get(path):
+        v = tree[tuple(path)]                       # KeyError for a name the reference does not have
+        if v is None:
+            raise AssertionError(f"adapter read {path}, whose value the fixture does not hold")
+        return v
+    return get
+
+
+def test_reference_param_values_match_constants():
+    """Every theta0 entry the evaluator reads has the reference's name and value: the tree comes
+    from the reference's option definitions (default.py, model_funcs.py, ampyx_data.py,
+    ampyx_ap2_settings.py, the example), not from this library's own paths."""
+    tree = _reference_theta0()
+    consts = pb.build_constants()
+    P = pb.pack_p(pb.NlpLayout(), consts, np.zeros(pb.NlpLayout().n_v), step="power1")
+    entries = pb.reference_p_entries(P, pb.NlpLayout())
+    n_theta = 0
+    for path, ours in entries.items():
+        if path[0] != "theta0":
+            continue
+        assert path in tree, f"{path} is not an entry of the reference's parameter tree"
+        np.testing.assert_allclose(ours, tree[path][:len(ours)], rtol=1e-15, atol=0, err_msg=str(path))
+        assert len(ours) == len(tree[path]), path
+        n_theta += 1
+    # every stability derivative of the kite data, at the path stability_derivatives.py:243 reads
+    sd = {p for p in tree if p[:2] == ("theta0", "aero") and p[2] in pb.SD_COEFFS}
+    assert sd == {pb.sd_path(c, i) for c, d in pb.AP2_STAB_DERIVS.items() for i in d}
+    assert n_theta == len(pb.THETA0_ENTRIES) - 1 + len(sd)
+
+
 def test_pack_p_from_reference_round_trips_by_name():
     """The boundary adapter from the reference's P struct (discretization.py:168-179), read by
-    entry name: a name-keyed view of a packed P packs back to the same vector, and a P assembled
-    from the reference's own named values (ampyx_data.py stability derivatives, the power cost,
-    u_ref by name) equals pack_p's."""
-    from awebox_amd.initial_guess import initial_guess
+    entry name from the reference's own tree: equal to pack_p's P for the AP2 NLP; a name-keyed view
+    of a packed P packs back to the same vector; a missing derivative raises."""
     consts = pb.build_constants()
     lay = pb.NlpLayout()
     v0 = initial_guess(consts, lay)
     P = pb.pack_p(lay, consts, v0, step="power1", u_ref=7.25)
+    tree = dict(_reference_theta0())
+    tree[("theta0", "wind", "u_ref")] = np.array([7.25])
+    tree[("p", "ref")] = v0
+    tree[("p", "weights")] = consts.weights
+    for i, name in enumerate(pb.COST_NAMES):
+        tree[("cost", name)] = np.array([consts.cost_steps["power1"][i]])
+    assert np.array_equal(pb.pack_p_from_reference(_reference_getter(tree), lay), P)
     entries = pb.reference_p_entries(P, lay)
     assert np.array_equal(pb.pack_p_from_reference(entries.__getitem__, lay), P)
-    # built from names only: nested dicts as the reference's struct holds them
-    tree = {("p", "ref"): v0, ("p", "weights"): consts.weights}
+    # the reference's stab-derivative level is ('theta0', 'aero', coeff, input): the old
+    # 'stab_derivs' path does not exist there, and a dropped derivative is an error, not a zero
+    assert ("theta0", "aero", "stab_derivs", "CX", "alpha") not in tree
+    del tree[("theta0", "aero", "CX", "alpha")]
+    with pytest.raises(KeyError):
+        pb.pack_p_from_reference(_reference_getter(tree), lay)
+
+
+def test_pack_p_from_reference_dual_kites():
+    """The same adapter on the dual-kite layout (126 weights, V with l_s / diam_s and two t_f)."""
+    from awebox_amd import dual
+    consts = dual.build_constants(dual.MultiConfig(n_k=4, d=3))
+    lay = dual.MultiLayout(consts.model, 4, 3)
+    v0 = dual.initial_guess(consts, lay)
+    P = dual.pack_p(lay, consts, v0, step="power1", u_ref=6.5)
+    tree = dict(_reference_theta0())
+    tree[("theta0", "wind", "u_ref")] = np.array([6.5])
+    tree[("theta0", "wind", "z_ref")] = np.array([10.0])       # dual_kites_power_curve.py:34
+    tree[("p", "ref")] = v0
+    tree[("p", "weights")] = consts.weights
     for i, name in enumerate(pb.COST_NAMES):
-        tree[("cost", name)] = consts.cost_steps["power1"][i]
-    for (name, size) in pb.THETA0_ENTRIES:
-        if name != "aero.stab_derivs":
-            o, _ = pb.THETA0_OFF[name]
-            tree[("theta0",) + tuple(name.split("."))] = consts.theta0[o:o + size]
-    tree[("theta0", "wind", "u_ref")] = 7.25
-    for c, d in pb.AP2_STAB_DERIVS.items():
-        for inp, vals in d.items():
-            tree[("theta0", "aero", "stab_derivs", c, inp)] = np.asarray(vals)
-    assert np.array_equal(pb.pack_p_from_reference(tree.__getitem__, lay), P)
+        tree[("cost", name)] = np.array([consts.cost_steps["power1"][i]])
+    assert np.array_equal(pb.pack_p_from_reference(_reference_getter(tree), lay), P)
+    tree[("p", "weights")] = consts.weights[:pb.NW]           # the AP2 weight vector: wrong size
+    with pytest.raises(ValueError):
+        pb.pack_p_from_reference(_reference_getter(tree), lay)

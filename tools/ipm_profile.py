@@ -15,7 +15,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-k", type=int, default=40)
     ap.add_argument("--iters", type=int, default=40)
-    ap.add_argument("--kkt", default="structured")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--separators", default="dense", help="separator solve of the structured KKT: dense | btd")
     args = ap.parse_args()
@@ -40,7 +39,7 @@ def main():
     st = hm.schedule(consts, lay, v0)[0]
     lbg, ubg = lay.g_bounds()
     P = pb.pack_p(lay, consts, v0, step=st.cost_step)
-    opts = hippo_options("initial", IpmOptions(max_iter=args.iters, kkt=args.kkt, profile=True,
+    opts = hippo_options("initial", IpmOptions(max_iter=args.iters, profile=True,
                                                       separators=args.separators))
     res = solve(ev, P, v0, st.lbx, st.ubx, lbg, ubg, opts=opts, device=args.device)
     out = {"iterations": res.iterations, "status": res.status, "seconds": res.seconds,
@@ -56,9 +55,11 @@ def main():
     rhs = torch.randn(sk.N, dtype=torch.float64, device=args.device)
     for _ in range(2):
         sk.factor(hv, diag, jv, 0.0, nlp.mI)
-        sk.solve(rhs)
+        sol = sk.solve(rhs)
+    bwd = float(((rhs - sk.matvec(sol.unsqueeze(0))[0]).abs().max()
+                 / (sk.k_norm[0] * sol.abs().max() + rhs.abs().max())).item())
     print(json.dumps({"separator_path": "btd" if getattr(sk, "use_btd", False) else "dense",
-                      "backward_errors": sk.backward, "n_dense": sk.n_dense}), flush=True)
+                      "backward_error": bwd, "n_dense": sk.n_dense}), flush=True)
     sync = torch.cuda.synchronize if args.device == "cuda" else (lambda: None)
     sync()
     t = time.perf_counter()
