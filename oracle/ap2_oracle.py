@@ -105,9 +105,13 @@ class Ap2Oracle:
     produced and ``tests/test_problem.py`` for their checks.
     """
 
-    def __init__(self, scaling, consts: dict, sd_len, n_k=40, d=4):
+    def __init__(self, scaling, consts: dict, sd_len, n_k=40, d=4, r_tether=None):
         self.s = torch.as_tensor(np.asarray(scaling, dtype=np.float64))
         self.c = dict(consts)
+        # tether attachment point in the body frame: geometry.r_tether of the kite data
+        # (ampyx_data.py:77, zeros = centre-of-mass attachment; tests/golden/reference_params.json)
+        self.r_tether = torch.zeros(3, dtype=torch.float64) if r_tether is None else \
+            torch.as_tensor(np.asarray(r_tether, dtype=np.float64))
         self.sd_len = np.asarray(sd_len, dtype=np.int64).reshape(6, 9)
         self.n_k, self.d = n_k, d
         self.tau, self.C, self.D, self.w = self._radau(d)
@@ -224,10 +228,20 @@ class Ap2Oracle:
 
     def holonomic(self, w_sc, th):
         # holonomics.get_tether_length_constraint (holonomics.py:204-264)
+        # with the attachment point q + R r_tether (exactly q for the AP2's zero r_tether)
         w = self.si(w_sc)
-        q = get(w, "x", "q10")
+        node = get(w, "x", "q10") + reshape33(get(w, "x", "r10")) @ self.r_tether
         l_t = get(w, "x", "l_t")[0]
-        return 0.5 * (torch.dot(q, q) - l_t ** 2.0)
+        return 0.5 * (torch.dot(node, node) - l_t ** 2.0)
+
+    def tether_moment(self, w_sc, th, R):
+        """forces.generate_tether_moments (forces.py:174-190): n = 2 jacobian_dcm(lambda c, R)^T,
+        jacobian_dcm(expr) = unskew(R^T reshape(d expr / d r)) (vector_operations.py:238-262) --
+        zero for a centre-of-mass attachment, lambda r_tether x (R^T q) for a stick
+        (test/units/test_model.py:255-318)."""
+        lam_c = lambda ww: self.si(ww)[IDX[("z", "lambda10")]][0] * self.holonomic(ww, th)  # noqa: E731
+        dW_dr = grad(lam_c)(w_sc)[IDX[("x", "r10")]]
+        return 2. * self.unskew(R.T @ reshape33(dW_dr))
 
     def element_drag(self, q_upper, q_lower, dq_upper, dq_lower, diam, th):
         # element.get_element_drag_fun (element.py:60-104); cd 'constant'
@@ -273,7 +287,7 @@ class Ap2Oracle:
         beta = torch.dot(u, e2) / smooth_abs(torch.dot(u, e1))
         airspeed = norm(u)
         # stability_derivatives.collect_inputs / get_p_q_r, frame 'control'
-        om_c = omega * torch.tensor([-1., 1., -1.])
+        om_c = from_body_to_control(omega)                      # stability_derivatives.py:202-206
         om_hat = om_c / (2. * airspeed)
         b, cr = th["geometry.b_ref"], th["geometry.c_ref"]
         p, qq, r = om_hat[0] * b, om_hat[1] * cr, om_hat[2] * b
@@ -296,9 +310,8 @@ class Ap2Oracle:
         s_ref = th["geometry.s_ref"]
         F_ctrl = CF * dyn * s_ref
         M_ctrl = dyn * s_ref * (torch.stack([b, cr, b]) * CM)
-        flip = torch.tensor([-1., 1., -1.])
-        F_earth = R @ (flip * F_ctrl)                            # frames.from_control_to_earth
-        M_body = flip * M_ctrl                                   # frames.from_control_to_body
+        F_earth = from_control_to_earth(R, F_ctrl)              # six_dof_kite.py:109 (frame 'control')
+        M_body = from_control_to_body(M_ctrl)                   # six_dof_kite.py:118
         return dict(u=u, rho=rho, alpha=alpha, beta=beta, airspeed=airspeed, F_earth=F_earth,
                     M_body=M_body, R=R)
 
@@ -352,9 +365,7 @@ class Ap2Oracle:
         R = aero["R"]
         dR = reshape33(get(w, "xdot", "dr10"))
         J = reshape33(th["geometry.j"])
-        lam_c = lambda ww: self.si(ww)[IDX[("z", "lambda10")]][0] * self.holonomic(ww, th)  # noqa: E731
-        dW_dr = grad(lam_c)(w_sc)[IDX[("x", "r10")]]
-        n_tether = 2. * self.unskew(R.T @ reshape33(dW_dr))  # jacobian_dcm(...).T
+        n_tether = self.tether_moment(w_sc, th, R)
         M = gamma * get(w, "u", "m_fict10") + aero["M_body"]
         omega_derivative = M - (J @ domega + cross(omega, J @ omega) + n_tether)
         rot = omega_derivative / c["m_aero_scaling"]
@@ -722,8 +733,27 @@ def wind_dcm(vec_u, kite_dcm):
     return torch.stack([d_hat, s_hat, l_hat], dim=1)
 
 
+# frames.py:39-120.  The aero path uses the control-frame conversions (force and moment frames
+# 'control', omega to the control frame); the reference runs its frame self-tests
+# (frames.test_conversions, frames.py:206-417) on every stability-derivative model build
+# (stability_derivatives.py:43) -- tests/test_reference_units.py restates them on these functions.
+_CONTROL = torch.tensor([-1., 1., -1.], dtype=torch.float64)
+
+
+def from_body_to_control(v):
+    return _CONTROL * v
+
+
+def from_control_to_body(v):
+    return _CONTROL * v
+
+
 def from_body_to_earth(kite_dcm, v):
     return kite_dcm @ v
+
+
+def from_control_to_earth(kite_dcm, v):
+    return from_body_to_earth(kite_dcm, from_control_to_body(v))
 
 
 def from_earth_to_body(kite_dcm, v):
@@ -738,21 +768,6 @@ def from_wind_to_body(vec_u, kite_dcm, v):
     return from_earth_to_body(kite_dcm, wind_dcm(vec_u, kite_dcm) @ v)
 
 
-def tether_moment_stick(q, r_flat, lam, r_tether, l_t):
-    """forces.generate_tether_moments for a 6-DOF kite on tether node 1 with the stick attachment:
-    n = 2 jacobian_dcm(lam c, R)^T with c = 1/2 (|q + R r_tether|^2 - l_t^2) (holonomics.py:
-    205-265) and jacobian_dcm(expr) = unskew(R^T reshape(d expr / d r)) (vector_operations.py:
-    238-262); r_flat is the DCM in CasADi's column-major flat order."""
-    r_flat = r_flat.detach().clone().requires_grad_(True)
-    R = reshape33(r_flat)
-    node = q + R @ r_tether
-    W = lam * 0.5 * (torch.dot(node, node) - l_t ** 2)
-    (dW_dr,) = torch.autograd.grad(W, r_flat)
-    Rn = reshape33(r_flat.detach())
-    A = Rn.T @ reshape33(dW_dr)
-    return 2. * 0.5 * torch.stack([A[2, 1] - A[1, 2], A[0, 2] - A[2, 0], A[1, 0] - A[0, 1]])
-
-
 def _periodic_order():
     off, pos = {}, 0
     for n, s in _X:
@@ -765,10 +780,11 @@ def _periodic_order():
     return np.array(out)
 
 
-def from_problem(consts, n_k=40, d=4):
-    """Build the oracle from an ``awebox_amd.problem.Ap2Constants`` (inputs only)."""
+def from_problem(consts, n_k=40, d=4, r_tether=None):
+    """Build the oracle from an ``awebox_amd.problem.Ap2Constants`` (inputs only); ``r_tether``
+    overrides the kite data's attachment point (zeros for the AP2)."""
     from awebox_amd import problem as pb
     names = pb.CONST_NAMES
     import re
     cd = {n: float(consts.consts[i]) for i, n in enumerate(names) if not re.match(r"(scaling|sd_len)\d+$", n)}
-    return Ap2Oracle(consts.scaling, cd, consts.sd_len, n_k=n_k, d=d)
+    return Ap2Oracle(consts.scaling, cd, consts.sd_len, n_k=n_k, d=d, r_tether=r_tether)

@@ -1,12 +1,15 @@
 """The reference's unit-level known answers that the AP2 path touches, restated without CasADi
 (VERDICT r01 item 10):
 
-* frame self-tests (awebox/mdl/aero/kite_dir/frames.py:206-417): body <-> earth for a horizontal
-  and a vertical kite, body <-> wind for level and right-angle apparent wind, squared residual
-  below 1e-10, on the oracle's restated frame conversions;
+* frame self-tests (awebox/mdl/aero/kite_dir/frames.py:206-417, which the reference runs on every
+  stability-derivative model build, stability_derivatives.py:43): body <-> earth for a
+  horizontal and a vertical kite, body <-> wind for level and right-angle apparent wind, squared
+  residual below 1e-10, on the oracle's frame conversions (the aero path uses from_body_to_earth
+  through from_control_to_earth);
 * the tether moment of a stick attachment (test/units/test_model.py:255-318): the oracle's
-  jacobian_dcm route equals the analytic lambda r x (R^T q) at the reference's numeric state
-  to 1e-8;
+  tether-moment method (the one its rotational dynamics call, jacobian_dcm route) equals the
+  analytic lambda r x (R^T q) at the reference's numeric state to 1e-8, and is 0 for the AP2's
+  centre-of-mass attachment;
 * the shooting-node equality subset (ocp/constraints.py:170-207): a model equality row is kept at
   the shooting nodes only if its Jacobian w.r.t. the non-x variables (xdot, u, z, theta) is
   structurally nonzero -- checked on the CCS pattern the evaluator derives from dependency masks;
@@ -56,15 +59,29 @@ def test_frames_level_and_right_body_wind():
 
 
 def test_tether_moment_stick_attachment_golden():
+    """The oracle's own tether-moment path (Ap2Oracle.tether_moment, used by its rotational
+    dynamics) with the reference's stick attachment r_tether = [0, 0, -0.1] and numeric state
+    (test_model.py:255-318) equals lambda r x (R^T q) to 1e-8; with the AP2's r_tether = 0 it is 0."""
+    from awebox_amd import problem as pb
+    consts = pb.build_constants(pb.Ap2Config(n_k=2, d=2))
     t = lambda a: torch.tensor(a, dtype=torch.float64)  # noqa: E731
     r_tether = t([0.0, 0.0, -0.1])
     q = t([130.644, 24.5223, 74.2863])
     r10 = t([0.271805, 0.334641, -0.902295, 0.0595685, 0.929945, 0.362839, 0.960506, -0.15237, 0.23283])
-    lam = 45.024
-    n = ao.tether_moment_stick(q, r10, lam, r_tether, l_t=152.184)
+    lam, l_t = 45.024, 152.184
+    w = torch.zeros(ao.NW, dtype=torch.float64)
+    w[ao.IDX[("x", "q10")]] = q
+    w[ao.IDX[("x", "r10")]] = r10
+    w[ao.IDX[("x", "l_t")]] = l_t
+    w[ao.IDX[("z", "lambda10")]] = lam
+    w_sc = w / torch.as_tensor(consts.scaling)
     R = ao.reshape33(r10)
+    orc = ao.from_problem(consts, n_k=2, d=2, r_tether=r_tether)
+    n = orc.tether_moment(w_sc, None, R)
     n_true = lam * ao.cross(r_tether, R.T @ q)
     assert float(torch.linalg.norm(n_true - n) / torch.linalg.norm(n_true)) < 1e-8
+    n0 = ao.from_problem(consts, n_k=2, d=2).tether_moment(w_sc, None, R)
+    assert float(torch.linalg.norm(n0)) == 0.0
 
 
 def test_shooting_node_equality_subset_keeps_all_24_rows():
