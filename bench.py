@@ -14,8 +14,10 @@ Also reported:
                   on the launch stream, against 8 TB/s.  `traffic` is the HBM byte rate from the
                   rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE passes recorded in
                   profiles/pmc_traffic.json, used only when that record was taken for the same
-                  kernel sources and batch size (else null); the same record carries the FP64
-                  VALU instruction counts behind `fp64`.
+                  kernel sources and batch size (else null).
+  fp64         -- algorithmic FP64 rate (the op-counting count of profiles/r03/flops_ap2.json /
+                  kernel time) and the issued FP64 lane rate of the PMC record, both against the
+                  FP64 vector peak; their ratio is the work the SIMT forward mode repeats.
   sweep        -- the metric's second half: wind-speed sweep trials/s, --sweep-points per GPU of
                   config 4's grid linspace(5, 8, 64) (first point: full homotopy; the rest: one
                   batched warm-started solve), collectives over RCCL; dual_sweep: the same for the
@@ -38,6 +40,19 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0     # MI355X spec (MI355X_MICROARCH.md); 6.3 TB/s measured float4 copy
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector spec
 PMC_RECORD = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+FLOPS_RECORD = os.path.join(ROOT, "profiles", "r03", "flops_ap2.json")
+
+
+def flops_record():
+    """The algorithmic flop count per evaluation (tools/count_flops.py) for these model sources."""
+    try:
+        with open(FLOPS_RECORD) as fh:
+            rec = json.load(fh)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from count_flops import source_hash
+    except (OSError, ValueError, ImportError):
+        return None
+    return rec if rec.get("source_hash") == source_hash() else None
 
 
 def kernel_source_hash() -> str:
@@ -249,37 +264,39 @@ def main():
         "outputs_finite": finite,
     }
     rec = pmc_record(B)
+    fp64 = {}
+    alg = flops_record()
+    if alg is not None:
+        # useful work: the op-counting restatement's flops per evaluation (tools/count_flops.py)
+        tf_alg = alg["flops_per_eval"] * B / (kernel_ms * 1e-3) / 1e12
+        fp64["algorithmic"] = {"achieved": tf_alg, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": tf_alg / FP64_PEAK_TFLOPS, "flops_per_eval": alg["flops_per_eval"],
+                               "record": os.path.relpath(FLOPS_RECORD, ROOT),
+                               "note": "value ops once per node + forward-mode tangent ops per structurally "
+                                       "nonzero colour + assembly (tools/flops/ap2_flops.cpp)"}
     if rec is not None:
         hbm_bytes = 2.0 * rec["FETCH_SIZE_kB"] * 1024 + rec["WRITE_SIZE_kB"] * 1024
         line["roofline"]["traffic"] = hbm_bytes / (kernel_ms * 1e-3) / 1e9
         line["roofline"]["traffic_bytes_per_launch"] = hbm_bytes
+        line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
         f64 = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"]
         if all(k in rec for k in f64):
             flops = 64.0 * (rec[f64[0]] + rec[f64[1]] + 2.0 * rec[f64[2]] + rec[f64[3]])
             tf = flops / (kernel_ms * 1e-3) / 1e12
-            fp64 = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                    "flops_per_launch": flops,
-                    "note": "FP64 VALU instructions x 64 lanes (FMA = 2) from the PMC record (idle lanes of issued "
-                            "instructions count); peak = MI355X FP64 vector spec"}
+            issued = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                      "flops_per_launch": flops,
+                      "note": "FP64 VALU instructions x 64 lanes (FMA = 2) from the PMC record: issued lane "
+                              "operations, idle and redundant lanes included -- an upper bound on useful work"}
             for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
                 if k in rec:
-                    fp64[k] = rec[k]
+                    issued[k] = rec[k]
             if "SQ_INSTS_VALU" in rec:
-                fp64["valu_f64_share"] = sum(rec[k] for k in f64) / rec["SQ_INSTS_VALU"]
-            line["fp64"] = fp64
-            if fp64["frac"] >= line["roofline"]["frac"]:
-                # the counters say the kernel is bound by FP64 issue, not HBM: the compute roofline
-                # is the headline one, the HBM figures stay beside it
-                hbm = dict(line["roofline"])
-                line["roofline"] = {"bound": "fp64", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                    "frac": tf / FP64_PEAK_TFLOPS, "traffic": hbm["traffic"],
-                                    "traffic_unit": "GB/s (HBM, PMC)", "kernel": hbm["kernel"],
-                                    "kernel_ms": kernel_ms, "finalize_ms": hbm["finalize_ms"],
-                                    "flops_per_launch": flops, "flops_source": fp64["note"],
-                                    "hbm": {"achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                            "frac": hbm["frac"], "bytes_per_eval": hbm["bytes_per_eval"],
-                                            "traffic_bytes_per_launch": hbm_bytes}}
-        line["roofline"]["pmc_record"] = os.path.relpath(PMC_RECORD, ROOT)
+                issued["valu_f64_share"] = sum(rec[k] for k in f64) / rec["SQ_INSTS_VALU"]
+            fp64["issued"] = issued
+            if "algorithmic" in fp64:
+                fp64["issued_over_algorithmic"] = flops / (fp64["algorithmic"]["flops_per_eval"] * B)
+    if fp64:
+        line["fp64"] = fp64
     if dual is not None:
         line["dual"] = dual
     if mpc is not None:

@@ -9,7 +9,13 @@ HIP dual-kite evaluator and the interior-point solver.
 * sharding invariance: the same points split into two shards (as two ranks would hold them) give
   the same powers as the single shard: bitwise for the shard's homotopy point, to 0.1 % for the
   warm-started points (their anchor differs between the shardings).
-The example's own discretisation is N=20; the test runs N=12 to stay within a minute or two."""
+* config 4 at its stated shape: rank 0's shard of linspace(5, 8, 64) -- 8 points -- at the
+  example's N=20 d=4 (examples/dual_kites_power_curve.py:41,48), in fan mode and in chain mode
+  (the reference's sweeping warm start, awebox/sweep.py:154-172): every point converges, power
+  rises with u_ref, the shared homotopy point is bitwise identical, and the two modes' powers
+  agree to 1e-3 relative (warm starts from different anchors reach neighbouring KKT points of the
+  same orbit family; measured differences ~1e-4).
+The shard-invariance test runs N=12 to stay within a minute or two."""
 import numpy as np
 import pytest
 
@@ -26,12 +32,12 @@ def gpu():
     return torch
 
 
-def _sweep(points):
+def _sweep(points, n_k=N_K, mode="fan"):
     from awebox_amd.dual_homotopy import make_evaluator
     from awebox_amd.ipm import IpmOptions
     from awebox_amd.sweep import run_sweep
-    return run_sweep(points, n_k=N_K, d=4, make_evaluator=lambda c, b=1: make_evaluator(c, batch=b),
-                     device="cuda", opts=IpmOptions(max_iter=3000), arch="dual", mode="fan")
+    return run_sweep(points, n_k=n_k, d=4, make_evaluator=lambda c, b=1: make_evaluator(c, batch=b),
+                     device="cuda", opts=IpmOptions(max_iter=3000), arch="dual", mode=mode)
 
 
 def test_dual_fan_sweep_converges_and_is_shard_invariant(gpu):
@@ -50,3 +56,20 @@ def test_dual_fan_sweep_converges_and_is_shard_invariant(gpu):
     # homotopy at u[2]); with the exact Hessian the warm starts land on the same orbit family to
     # ~1e-4 in power (measured 1.2e-4 at u[2], 1e-6 at u[3]), not on one bitwise-equal optimum
     assert np.allclose(sharded, p, rtol=1e-3), (sharded, p)
+
+
+def test_config4_shard_at_stated_shape_fan_vs_chain(gpu):
+    u = np.linspace(5.0, 8.0, 64)[:8]                          # rank 0's shard of 8 GPUs
+    fan = _sweep(u, n_k=20, mode="fan")
+    chain = _sweep(u, n_k=20, mode="chain")
+    print("fan", fan["avg_power_W"], fan["iterations"], fan["wall_s"])
+    print("chain", chain["avg_power_W"], chain["iterations"], chain["wall_s"])
+    for res in (fan, chain):
+        assert all(res["ok"]), res
+        p = np.asarray(res["avg_power_W"])
+        assert p[0] > 1000.0 and np.all(np.diff(p) > 0), p
+        assert np.allclose(res["u_ref"], u)
+    pf, pc = np.asarray(fan["avg_power_W"]), np.asarray(chain["avg_power_W"])
+    assert pf[0] == pc[0]                                       # the same homotopy for point 0
+    assert np.allclose(pf, pc, rtol=1e-3), (pf, pc)
+    assert np.allclose(fan["period_s"], chain["period_s"], rtol=1e-2)

@@ -12,6 +12,6 @@ step() {  # step <limit> <log> <cmd...>
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
 if [ $# -eq 0 ]; then set -- tests -m gpu; fi
-step 1000 pytest_gpu.log python -u -m pytest -x -v --timeout 400 --timeout-method thread "$@"
+step 1100 pytest_gpu.log python -u -m pytest -x -v --durations=25 --timeout 600 --timeout-method thread "$@"
 step 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
 echo CHECK_DONE
