@@ -101,8 +101,22 @@ def config_traffic(which: str, batch: int, kernel_ms: float):
     if not rec or rec.get("source_hash") != sources_hash(which) or rec.get("batch") != batch:
         return None
     b = (2.0 * rec["FETCH_SIZE_kB"] + rec["WRITE_SIZE_kB"]) * 1024
-    return {"traffic": b / (kernel_ms * 1e-3) / 1e9, "traffic_bytes_per_launch": b,
-            "pmc_record": os.path.relpath(PMC_RECORD_CONFIGS, ROOT)}
+    out = {"traffic": b / (kernel_ms * 1e-3) / 1e9, "traffic_bytes_per_launch": b,
+           "pmc_record": os.path.relpath(PMC_RECORD_CONFIGS, ROOT)}
+    f64 = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"]
+    if all(k in rec for k in f64 + ["SQ_INSTS_VALU", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"]):
+        flops = 64.0 * (rec[f64[0]] + rec[f64[1]] + 2.0 * rec[f64[2]] + rec[f64[3]])
+        tf = flops / (kernel_ms * 1e-3) / 1e12
+        out["fp64_issued"] = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                              "valu_f64_share": sum(rec[k] for k in f64) / rec["SQ_INSTS_VALU"],
+                              "wait_frac": rec["SQ_WAIT_ANY"] / rec["SQ_WAVE_CYCLES"],
+                              "note": "FP64 VALU instructions x 64 lanes (FMA = 2) from the PMC record"}
+        # the counters decide what limits the kernel: FP64 issue + latency when its issued FP64 rate
+        # is well above its HBM fraction
+        hbm_frac = out["traffic"] / HBM_PEAK_GBS
+        out["measured_limiter"] = ("fp64 VALU issue + latency (SQ_WAIT_ANY {:.0%} of wave cycles)".format(
+            out["fp64_issued"]["wait_frac"]) if tf / FP64_PEAK_TFLOPS > hbm_frac else "hbm")
+    return out
 
 
 def pmc_record(batch: int):
@@ -297,6 +311,12 @@ def main():
                 fp64["issued_over_algorithmic"] = flops / (fp64["algorithmic"]["flops_per_eval"] * B)
     if fp64:
         line["fp64"] = fp64
+        if "issued" in fp64 and rec is not None:
+            wait = rec.get("SQ_WAIT_ANY", 0.0) / max(rec.get("SQ_WAVE_CYCLES", 1.0), 1.0)
+            line["roofline"]["measured_limiter"] = (
+                f"fp64 VALU issue + latency (issued FP64 {fp64['issued']['frac']:.1%} of peak, SQ_WAIT_ANY "
+                f"{wait:.0%} of wave cycles); HBM at {line['roofline']['frac']:.1%}"
+                if fp64["issued"]["frac"] > line["roofline"]["frac"] else "hbm")
     if dual is not None:
         line["dual"] = dual
     if mpc is not None:
@@ -563,6 +583,28 @@ def pmpc_block(c, B, dev, dist, world, steps=3, warmup=1):
 SWEEP_GRID = 64       # config 4: u_ref = linspace(5, 8, 64), 8 contiguous points per GPU
 
 
+def sweep_profile(arch: str):
+    """GPU utilisation of the sweep block from its committed rocprofv3 record (tools/sweep_record.py):
+    busy fraction and the dominant solver kernels, or None when the solver / evaluator sources
+    changed since the record was taken."""
+    path = os.path.join(ROOT, "profiles", "r03", f"sweep_profile_{arch}.json")
+    try:
+        with open(path) as fh:
+            rec = json.load(fh)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from sweep_record import sources_hash
+    except (OSError, ValueError, ImportError):
+        return None
+    if rec.get("source_hash") != sources_hash(arch):
+        return None
+    return {"record": os.path.relpath(path, ROOT), "gpu_busy_frac": rec["gpu_busy_frac"],
+            "gpu_kernel_s": rec["gpu_kernel_s"], "wall_s_profiled": rec["wall_s"],
+            "dominant_kernel": rec["top_kernels"][0]["kernel"],
+            "dominant_share_of_gpu_time": rec["top_kernels"][0]["share_of_gpu_time"],
+            "top_kernels": [{k: t[k] for k in ("kernel", "share_of_gpu_time", "avg_ms", "calls")}
+                            for t in rec["top_kernels"][:4]]}
+
+
 def _grid_points(per_gpu, world):
     """The points of the sweep: the first per_gpu x world of linspace(5, 8, 64) (config 4's grid;
     rank r gets the contiguous block [r per_gpu, (r + 1) per_gpu)), or an even spread over 5..8 m/s
@@ -604,7 +646,8 @@ def sweep_block(per_gpu, world, dist, dev, consts):
             "solver": "GPU interior point (awebox_amd/ipm.py): homotopy for the shard's first point, batched "
                       "warm start (solve_batch) for the rest; structured KKT (batched interval LU + "
                       "block-tridiagonal separators), exact Hessian, IPOPT inertia correction from exact KKT "
-                      "inertia, second-order corrections"}
+                      "inertia, second-order corrections",
+            "utilisation": sweep_profile("ap2")}
 
 
 def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
@@ -636,7 +679,8 @@ def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
             "period_s": [round(t, 2) for t in res["period_s"]], "scaling": "weak",
             "solver": "GPU interior point (awebox_amd/ipm.py): homotopy for the shard's first point, batched warm "
                       "start for the rest; structured KKT with the block-recursion separator sweep, exact KKT "
-                      "inertia; exact Hessian of the Lagrangian (dual_hess_kernel: colour-pair hyper-dual forward mode)"}
+                      "inertia; exact Hessian of the Lagrangian (dual_hess_kernel: colour-pair hyper-dual forward mode)",
+            "utilisation": sweep_profile("dual")}
 
 
 def hessian_block(ev, V, P, B, lay, dev, steps=10):

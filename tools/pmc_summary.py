@@ -23,21 +23,36 @@ def summarise(paths, kernel_substr="interval"):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
-def record_configs(fetch_dir, write_dir):
-    """profiles/pmc_traffic_configs.json: FETCH/WRITE_SIZE per dispatch of the config-3 (dual kites,
-    B = 128) and config-5 (tracking MPC, B = 256) interval kernels of tools/pmc_kernels.py."""
+def record_configs(fetch_dir, write_dir, *sq_dirs, only=None, hashes=None):
+    """profiles/pmc_traffic_configs.json: FETCH/WRITE_SIZE (and, from further counter directories,
+    the SQ_* FP64 / VALU / wave-state counters) per dispatch of the config-3 (dual kites, B = 128)
+    and config-5 (tracking MPC, B = 256) interval kernels of tools/pmc_kernels.py.  ``only`` limits
+    the update to some kernels (the others keep their entries); ``hashes`` overrides the source
+    hash of a kernel (records taken on committed sources that have changed in the tree since)."""
     sys.path.insert(0, ROOT)
     from bench import sources_hash
-    out = {}
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_configs.json")
+    try:
+        out = json.load(open(path))
+    except (OSError, ValueError):
+        out = {}
     for which, kern, batch in (("dual", "dual_interval_kernel", 128), ("mpc", "mpc_interval_kernel", 256)):
+        if only is not None and which not in only:
+            continue
         f = summarise(glob.glob(os.path.join(fetch_dir, "**", "*counter_collection.csv"), recursive=True), kern)
         w = summarise(glob.glob(os.path.join(write_dir, "**", "*counter_collection.csv"), recursive=True), kern)
         if "FETCH_SIZE" not in f or "WRITE_SIZE" not in w:
             continue
-        out[which] = {"batch": batch, "kernel": kern + "<4>", "source_hash": sources_hash(which),
-                      "FETCH_SIZE_kB": f["FETCH_SIZE"], "WRITE_SIZE_kB": w["WRITE_SIZE"],
-                      "units": "kB per dispatch, mean over 5 dispatches (tools/pmc_kernels.py, tools/gpu_pmc_all.sh)"}
-    with open(os.path.join(ROOT, "profiles", "pmc_traffic_configs.json"), "w") as fh:
+        rec = {"batch": batch, "kernel": kern + "<4>",
+               "source_hash": (hashes or {}).get(which) or sources_hash(which),
+               "FETCH_SIZE_kB": f["FETCH_SIZE"], "WRITE_SIZE_kB": w["WRITE_SIZE"],
+               "units": "FETCH/WRITE_SIZE in kB per dispatch, SQ_* per dispatch; mean over 5 dispatches "
+                        "(tools/pmc_kernels.py, tools/gpu_records.sh)"}
+        for d in sq_dirs:
+            for k, v in summarise(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True), kern).items():
+                rec[k] = v
+        out[which] = rec
+    with open(path, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     print("wrote profiles/pmc_traffic_configs.json", sorted(out))
 
@@ -60,7 +75,7 @@ def record_hess(dirs, batch=256):
 if __name__ == "__main__":
     args = sys.argv[1:]
     if args and args[0] == "--record-configs":
-        record_configs(args[1], args[2])
+        record_configs(*args[1:])
         sys.exit(0)
     if args and args[0] == "--record-hess":
         record_hess(args[1:])
