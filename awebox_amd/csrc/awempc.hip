@@ -300,6 +300,182 @@ __global__ __launch_bounds__(64) void mpc_finalize_kernel(MArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// nlp_hess_l: sigma f + lam^T g (kite3_tables.hpp, build_hess_tables)
+// ---------------------------------------------------------------------------------------------
+struct HArgs {
+    MArgs a;
+    const double* sigma;     // [B]
+    const double* lam;       // [B][n_g]
+    double* H;               // [B][hnnz]
+    double* gpart;           // [B][n_k][ng]
+    const int* task;         // p | q << 8
+    int ntask0, ntask1, npair1, hnnz, ng, hd_total;
+    const int* slot0;
+    const int* nslot;
+    const int* ent_off;
+    const int* term_off;
+    const unsigned* terms;
+    const int* gslot;
+    const int* xnslot;
+};
+
+constexpr int kHessThreads = 256;
+
+// hyper-dual node variable i: e1 along direction p, e2 along direction q (the first-order seeds)
+struct LaneHIn {
+    const double* w;
+    int p, q;
+    double cxx, inv_tf;      // C[n][n] / (h tf) and 1 / tf at a Radau node, 0 at the shooting node
+    __device__ __forceinline__ double seed(int dir, int i) const {
+        double t = (i == dir) ? 1.0 : 0.0;
+        if (i >= K3_NX && i < 2 * K3_NX) {
+            if (dir == i - K3_NX) t += cxx;
+            if (dir == kDirTf) t += -w[i] * inv_tf;
+        }
+        return t;
+    }
+    __device__ __forceinline__ awe::HDual operator()(int i) const {
+        return awe::HDual(w[i], seed(p, i), q == kGTask ? 0.0 : seed(q, i), 0.0);
+    }
+};
+
+// sum_r mu_r d2F_r / de1 de2 (pair task) or sum_r mu_r dF_r / de1 (first-order task)
+struct LaneHSink {
+    const double* mu;
+    bool first;
+    double acc;
+    __device__ __forceinline__ void eq_row(int r, const awe::HDual& v) { acc += mu[r] * (first ? v.a : v.ab); }
+    __device__ __forceinline__ void ineq_row(int r, const awe::HDual& v) { eq_row(K3_N_EQ + r, v); }
+};
+
+template <int D>
+__global__ __launch_bounds__(kHessThreads) void mpc_hess_kernel(HArgs ha) {
+    const MArgs& a = ha.a;
+    constexpr int NN = D + 1;
+    constexpr int NT = kHessThreads;
+    constexpr int STRIDE = K3_NX + K3_NU + K3_NX + K3_NZ + D * (K3_NX + K3_NZ);
+    constexpr int NLOC = 9 + STRIDE + K3_NX;
+    __shared__ double vloc[NLOC];
+    __shared__ double wn[NN][kLanes];
+    __shared__ double mu[NN][kRowsPerNode];
+    __shared__ double wq[K3_NX + K3_NU];                  // Q, R tracking weights
+    __shared__ double scl[1 + NN * NN];
+    extern __shared__ double hd[];                        // [hd_total]: per node, its tasks' values
+
+    const int b = blockIdx.x / a.n_k, k = blockIdx.x % a.n_k;
+    const int tid = threadIdx.x;
+    const double* V = a.V + (size_t)b * a.n_v;
+    const double* P = a.P + (size_t)b * a.n_p;
+    const double* lam = ha.lam + (size_t)b * a.n_g;
+    const double sigma = ha.sigma[b];
+    const int base = 9 + 2 + k * STRIDE;
+    for (int i = tid; i < NLOC; i += NT) vloc[i] = i < 9 ? V[i] : V[base + (i - 9)];
+    const double* pQ = P + K3_NX + a.n_v + 1;
+    for (int i = tid; i < K3_NX + K3_NU; i += NT) wq[i] = pQ[i];
+    const double u_ref = P[K3_NX + a.n_v];
+    const int row0 = K3_NX + k * (K3_N_EQ + K3_N_INEQ + D * K3_N_EQ + K3_NX);
+    for (int t = tid; t < NN * kRowsPerNode; t += NT) {
+        const int n = t / kRowsPerNode, r = t % kRowsPerNode;
+        double m = 0.0;
+        if (n == 0) m = lam[row0 + r];
+        else if (r < K3_N_EQ) m = lam[row0 + K3_N_EQ + K3_N_INEQ + (n - 1) * K3_N_EQ + r];
+        mu[n][r] = m;
+    }
+    __syncthreads();
+    const double tf = vloc[1];
+    const double inv_h_tf = (double)a.n_k / tf, inv_tf = 1.0 / tf;
+    const double* C = a.coll->C;
+    for (int i = tid; i < 1 + NN * NN; i += NT) scl[i] = i == 0 ? 1.0 : C[i - 1] * inv_h_tf;
+    const double* xk = vloc + 9;
+    const double* uk = xk + K3_NX;
+    const double* xdk = uk + K3_NU;
+    const double* zk = xdk + K3_NX;
+    const double* coll = zk + K3_NZ;
+    auto Xv = [&](int r, int i) -> double { return r == 0 ? xk[i] : coll[(r - 1) * (K3_NX + K3_NZ) + i]; };
+    for (int t = tid; t < NN * kLanes; t += NT) {
+        const int n = t / kLanes, i = t % kLanes;
+        double val;
+        if (i < K3_NX) val = Xv(n, i);
+        else if (i < 2 * K3_NX) {
+            if (n == 0) val = xdk[i - K3_NX];
+            else {
+                double s = 0.0;
+                for (int r = 0; r < NN; ++r) s += C[r * NN + n] * Xv(r, i - K3_NX);
+                val = s * inv_h_tf;
+            }
+        } else if (i < 2 * K3_NX + K3_NU) val = uk[i - 2 * K3_NX];
+        else if (i == 2 * K3_NX + K3_NU) val = n == 0 ? zk[0] : coll[(n - 1) * (K3_NX + K3_NZ) + K3_NX];
+        else if (i < K3_NW) val = vloc[i - (2 * K3_NX + K3_NU + K3_NZ)];
+        else val = vloc[2];                               // phi.gamma
+        wn[n][i] = val;
+    }
+    __syncthreads();
+
+    // ---- second-order pass: one (node, direction pair) per thread --------------------------------
+    const int nt0 = ha.ntask0, nt1 = ha.ntask1;
+    for (int t = tid; t < nt0 + D * nt1; t += NT) {
+        const int n = t < nt0 ? 0 : 1 + (t - nt0) / nt1;
+        const int ti = n == 0 ? t : (t - nt0) % nt1;
+        const int pq = ha.task[(n == 0 ? 0 : nt0) + ti];
+        LaneHIn in{wn[n], pq & 0xff, pq >> 8, n > 0 ? C[n * NN + n] * inv_h_tf : 0.0, n > 0 ? inv_tf : 0.0};
+        LaneHSink sink{mu[n], in.q == kGTask, 0.0};
+        const awe::HDual gamma(wn[n][kDirGamma], in.p == kDirGamma ? 1.0 : 0.0,
+                               in.q == kDirGamma ? 1.0 : 0.0, 0.0);
+        awe::kite3_node<awe::HDual>(in, gamma, u_ref, a.cst, sink, n == 0);
+        hd[(n == 0 ? 0 : nt0 + (n - 1) * nt1) + ti] = sink.acc;
+    }
+    __syncthreads();
+
+    // ---- V-space entries: the interval's contiguous local slots, then its global partials ---------
+    const int nloc = ha.nslot[k];
+    const int e0 = ha.ent_off[k];
+    const double* w = a.coll->w;
+    const double invN = 1.0 / a.n_k;
+    double sw = 0.0;
+    for (int j = 0; j < D; ++j) sw += w[j];
+    double* Hb = ha.H + (size_t)b * ha.hnnz + ha.slot0[k];
+    double* gp = ha.gpart + ((size_t)b * a.n_k + k) * ha.ng;
+    auto hoff = [&](int n) { return n == 0 ? 0 : nt0 + (n - 1) * nt1; };
+    for (int e = tid; e < nloc + ha.ng; e += NT) {
+        double v = 0.0;
+        for (int t = ha.term_off[e0 + e]; t < ha.term_off[e0 + e + 1]; ++t) {
+            const unsigned term = ha.terms[t];
+            const int type = term >> 30, n = (term >> 27) & 7;
+            if (type == kHTA) {
+                v += scl[(term >> 7) & 127] * scl[term & 127] * hd[hoff(n) + ((term >> 14) & 8191)];
+            } else if (type == kHTB) {
+                const int i = (term >> 22) & 31, r = (term >> 19) & 7;
+                v += hd[hoff(n) + ha.npair1 + i] * (-C[r * NN + n] * inv_h_tf * inv_tf);
+            } else if (type == kHTC) {
+                const int i = (term >> 22) & 31;
+                v += hd[hoff(n) + ha.npair1 + i] * (2.0 * wn[n][K3_NX + i] * inv_tf * inv_tf);
+            } else {
+                const int sub = (term >> 22) & 3, i = (term >> 17) & 31;
+                const double wt = sub == 0 ? w[n - 1] * wq[i] : (sub == 1 ? w[n - 1] : sw * wq[K3_NX + i]);
+                v += sigma * 2.0 * wt * invN;
+            }
+        }
+        if (e < nloc) Hb[e] = v;
+        else gp[e - nloc] = v;
+    }
+}
+
+// global-global entries (sums of the interval partials, fixed order) and the terminal cost
+__global__ __launch_bounds__(64) void mpc_hess_finalize_kernel(HArgs ha) {
+    const MArgs& a = ha.a;
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (lane < ha.ng) {
+        double v = 0.0;
+        for (int k = 0; k < a.n_k; ++k) v += ha.gpart[((size_t)b * a.n_k + k) * ha.ng + lane];
+        ha.H[(size_t)b * ha.hnnz + ha.gslot[lane]] = v;
+    }
+    if (lane < K3_NX) {
+        const double* pP = a.P + (size_t)b * a.n_p + K3_NX + a.n_v + 1 + K3_NX + K3_NU;
+        ha.H[(size_t)b * ha.hnnz + ha.xnslot[lane]] = ha.sigma[b] * 2.0 * pP[lane];
+    }
+}
+
 }  // namespace
 
 struct awempc_handle_s {
@@ -315,6 +491,17 @@ struct awempc_handle_s {
     double *d_V = nullptr, *d_P = nullptr, *d_f = nullptr, *d_g = nullptr, *d_grad = nullptr, *d_jac = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool timed = false;
+    // Hessian (built on first use: awempc_hess_init)
+    HessTables ht;
+    bool hess_ready = false;
+    int hd_total = 0;
+    int *d_task = nullptr, *d_slot0 = nullptr, *d_nslot = nullptr, *d_ent_off = nullptr, *d_term_off = nullptr;
+    int *d_hgslot = nullptr, *d_xnslot = nullptr;
+    unsigned* d_terms = nullptr;
+    double* d_gpart = nullptr;
+    double *d_hsig = nullptr, *d_hlam = nullptr, *d_H = nullptr;
+    hipEvent_t hev[2] = {nullptr, nullptr};
+    bool htimed = false;
 };
 
 extern "C" {
@@ -375,10 +562,14 @@ int awempc_create(int n_k, int d, const double* consts, int n_consts, int batch,
 int awempc_destroy(awempc_handle h) {
     if (!h) return AWE_OK;
     void* bufs[] = {h->d_cst, h->d_coll, h->d_goff, h->d_gslot, h->d_gcode, h->d_fpart,
-                    h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac};
+                    h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac,
+                    h->d_task, h->d_slot0, h->d_nslot, h->d_ent_off, h->d_term_off, h->d_hgslot, h->d_xnslot,
+                    h->d_terms, h->d_gpart, h->d_hsig, h->d_hlam, h->d_H};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : h->hev)
         if (e) (void)hipEventDestroy(e);
     delete h;
     return AWE_OK;
@@ -462,6 +653,125 @@ int awempc_eval_nlp_host(awempc_handle h, const double* V, const double* p, doub
     };
     if (!finite(f, nb) || !finite(g, nb * T.lay.n_g) || !finite(grad_f, nb * T.lay.n_v) || !finite(jac, nb * nnz))
         return fail(AWE_ERR_NONFINITE, "non-finite output");
+    return AWE_OK;
+}
+
+// ---- nlp_hess_l ------------------------------------------------------------------------------
+int awempc_sparsity_hess_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind, int* row) {
+    if (!consts || !nnz) return fail(AWE_ERR_ARG, "null argument");
+    Tables T;
+    HessTables H;
+    std::string err;
+    if (build_tables(n_k, d, consts, n_consts, T, err) || build_hess_tables(T, consts, H, err))
+        return fail(AWE_ERR_ARG, err);
+    *nnz = H.nnz;
+    if (colind) std::memcpy(colind, H.colind.data(), sizeof(int) * H.colind.size());
+    if (row) std::memcpy(row, H.row.data(), sizeof(int) * H.row.size());
+    return AWE_OK;
+}
+
+int awempc_hess_init(awempc_handle h, int* nnz) {
+    if (!h) return fail(AWE_ERR_ARG, "null handle");
+    if (!h->hess_ready) {
+        std::string err;
+        if (build_hess_tables(h->t, h->consts.data(), h->ht, err)) return fail(AWE_ERR_ARG, err);
+        const HessTables& H = h->ht;
+        h->hd_total = H.ntask[0] + h->t.lay.d * H.ntask[1];
+        if ((size_t)h->hd_total * sizeof(double) > 60 * 1024) return fail(AWE_ERR_ARG, "Hessian tasks exceed the LDS budget");
+        if ((int)H.gslot.size() > 64) return fail(AWE_ERR_ARG, "too many global Hessian entries");
+#define MPC_UPLOAD(dst, vec)                                                               \
+        MPC_TRY(hipMalloc((void**)&dst, sizeof(*dst) * (vec).size()));                      \
+        MPC_TRY(hipMemcpy(dst, (vec).data(), sizeof(*dst) * (vec).size(), hipMemcpyHostToDevice));
+        MPC_UPLOAD(h->d_task, H.task);
+        MPC_UPLOAD(h->d_slot0, H.slot0);
+        MPC_UPLOAD(h->d_nslot, H.nslot);
+        MPC_UPLOAD(h->d_ent_off, H.ent_off);
+        MPC_UPLOAD(h->d_term_off, H.term_off);
+        MPC_UPLOAD(h->d_terms, H.terms);
+        MPC_UPLOAD(h->d_hgslot, H.gslot);
+        MPC_UPLOAD(h->d_xnslot, H.xnslot);
+#undef MPC_UPLOAD
+        MPC_TRY(hipMalloc((void**)&h->d_gpart, sizeof(double) * (size_t)h->batch * h->t.lay.n_k * std::max<size_t>(1, H.gslot.size())));
+        for (auto& e : h->hev) MPC_TRY(hipEventCreate(&e));
+        h->hess_ready = true;
+    }
+    if (nnz) *nnz = h->ht.nnz;
+    return AWE_OK;
+}
+
+int awempc_sparsity_hess(awempc_handle h, int* colind, int* row) {
+    if (!h || !colind || !row) return fail(AWE_ERR_ARG, "null argument");
+    int rc = awempc_hess_init(h, nullptr);
+    if (rc) return rc;
+    std::memcpy(colind, h->ht.colind.data(), sizeof(int) * h->ht.colind.size());
+    std::memcpy(row, h->ht.row.data(), sizeof(int) * h->ht.row.size());
+    return AWE_OK;
+}
+
+int awempc_eval_hess(awempc_handle h, const double* V, const double* p, const double* sigma, const double* lam_g,
+                     double* H, void* stream) {
+    if (!h || !V || !p || !sigma || !lam_g || !H) return fail(AWE_ERR_ARG, "null argument");
+    int rc = awempc_hess_init(h, nullptr);
+    if (rc) return rc;
+    const Tables& T = h->t;
+    const HessTables& HT = h->ht;
+    hipStream_t s = (hipStream_t)stream;
+    MArgs a{T.lay.n_k, T.lay.d, T.lay.n_v, T.lay.n_g, T.lay.n_p, (int)T.row.size(), T.lay.stride,
+            V, p, nullptr, nullptr, nullptr, nullptr, h->d_cst, h->d_coll, h->d_goff, h->d_gslot, h->d_gcode, h->d_fpart};
+    HArgs ha{a, sigma, lam_g, H, h->d_gpart, h->d_task, HT.ntask[0], HT.ntask[1], HT.npair1, HT.nnz,
+             (int)HT.gslot.size(), h->hd_total, h->d_slot0, h->d_nslot, h->d_ent_off, h->d_term_off, h->d_terms,
+             h->d_hgslot, h->d_xnslot};
+    const dim3 grid((unsigned)(h->batch * T.lay.n_k));
+    const size_t lds = sizeof(double) * (size_t)h->hd_total;
+    MPC_TRY(hipEventRecord(h->hev[0], s));
+    switch (T.lay.d) {
+        case 2: mpc_hess_kernel<2><<<grid, kHessThreads, lds, s>>>(ha); break;
+        case 3: mpc_hess_kernel<3><<<grid, kHessThreads, lds, s>>>(ha); break;
+        case 4: mpc_hess_kernel<4><<<grid, kHessThreads, lds, s>>>(ha); break;
+        case 5: mpc_hess_kernel<5><<<grid, kHessThreads, lds, s>>>(ha); break;
+        default: return fail(AWE_ERR_ARG, "unsupported d");
+    }
+    MPC_TRY(hipGetLastError());
+    mpc_hess_finalize_kernel<<<dim3((unsigned)h->batch), 64, 0, s>>>(ha);
+    MPC_TRY(hipGetLastError());
+    MPC_TRY(hipEventRecord(h->hev[1], s));
+    h->htimed = true;
+    return AWE_OK;
+}
+
+int awempc_last_hess_ms(awempc_handle h, float* ms) {
+    if (!h || !h->htimed) return fail(AWE_ERR_ARG, "no timed Hessian evaluation yet");
+    MPC_TRY(hipEventSynchronize(h->hev[1]));
+    if (ms) MPC_TRY(hipEventElapsedTime(ms, h->hev[0], h->hev[1]));
+    return AWE_OK;
+}
+
+int awempc_eval_hess_host(awempc_handle h, const double* V, const double* p, const double* sigma, const double* lam_g,
+                          double* H) {
+    if (!h || !V || !p || !sigma || !lam_g || !H) return fail(AWE_ERR_ARG, "null argument");
+    int rc = awempc_hess_init(h, nullptr);
+    if (rc) return rc;
+    const Tables& T = h->t;
+    const size_t nb = (size_t)h->batch, hnnz = h->ht.nnz;
+    if (!h->d_V) {
+        MPC_TRY(hipMalloc((void**)&h->d_V, sizeof(double) * nb * T.lay.n_v));
+        MPC_TRY(hipMalloc((void**)&h->d_P, sizeof(double) * nb * T.lay.n_p));
+    }
+    if (!h->d_H) {
+        MPC_TRY(hipMalloc((void**)&h->d_hsig, sizeof(double) * nb));
+        MPC_TRY(hipMalloc((void**)&h->d_hlam, sizeof(double) * nb * T.lay.n_g));
+        MPC_TRY(hipMalloc((void**)&h->d_H, sizeof(double) * nb * hnnz));
+    }
+    MPC_TRY(hipMemcpy(h->d_V, V, sizeof(double) * nb * T.lay.n_v, hipMemcpyHostToDevice));
+    MPC_TRY(hipMemcpy(h->d_P, p, sizeof(double) * nb * T.lay.n_p, hipMemcpyHostToDevice));
+    MPC_TRY(hipMemcpy(h->d_hsig, sigma, sizeof(double) * nb, hipMemcpyHostToDevice));
+    MPC_TRY(hipMemcpy(h->d_hlam, lam_g, sizeof(double) * nb * T.lay.n_g, hipMemcpyHostToDevice));
+    rc = awempc_eval_hess(h, h->d_V, h->d_P, h->d_hsig, h->d_hlam, h->d_H, nullptr);
+    if (rc) return rc;
+    MPC_TRY(hipDeviceSynchronize());
+    MPC_TRY(hipMemcpy(H, h->d_H, sizeof(double) * nb * hnnz, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nb * hnnz; ++i)
+        if (!std::isfinite(H[i])) return fail(AWE_ERR_NONFINITE, "non-finite Hessian");
     return AWE_OK;
 }
 

@@ -30,6 +30,17 @@ constexpr int U_FFICT = 22, U_DCOEFF = 25, U_DDDLT = 27, Z_LAMBDA = 28, TH_DIAM 
 constexpr double kPi = 3.14159265358979323846;
 }  // namespace k3
 
+// the roll angle enters through sin / cos: their hyper-dual forms (the first- and second-order
+// kernels instantiate the model on Dual and HDual, scalar.hpp)
+AWE_HD HDual sin(HDual x) {
+    const double s = ::sin(x.v), c = ::cos(x.v);
+    return hd_apply(x, s, c, -s);
+}
+AWE_HD HDual cos(HDual x) {
+    const double s = ::sin(x.v), c = ::cos(x.v);
+    return hd_apply(x, c, -s, -c);
+}
+
 template <class T>
 struct Kite3Result {
     T eq[K3_N_EQ];

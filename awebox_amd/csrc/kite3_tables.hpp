@@ -183,4 +183,212 @@ inline int build_tables(int n_k, int d, const double* consts, int n_consts, Tabl
     return 0;
 }
 
+// =========================================================================================
+// Hessian of the Lagrangian (nlp_hess_l of the MPC NLP, pmpc.py:193-217 with IPOPT's exact
+// Hessian, default.py:323).  The constraints' second derivatives come from the node model in
+// hyper-dual arithmetic, one task per direction pair (p, q) that is structurally nonzero (HDep over
+// the 32 directions of the first-order pass, kite3 needs no colouring); the initial-condition and
+// continuity rows are linear.  Directions map to V columns exactly as in the first-order gather
+// list, so the V-space entry (a, b) of node n is s_a s_b Hdir_n(p_a, p_b) with s = 1 or the
+// polynomial scale C[r][n] / (h tf); xdot's second-order dependence on t_f adds
+// G_n,i d2 xdot_i / dV dV with G_n,i = sum_r mu_r dF_r / dxdot_i (first-order tasks, e2 = 0).
+// The tracking cost (pmpc.py:304-358) is a diagonal quadratic in V.
+// =========================================================================================
+constexpr int kHTA = 0, kHTB = 1, kHTC = 2, kHTD = 3;   // term types (bits 31..30)
+constexpr int kGTask = 255;                            // q of a first-order task
+// A: scl[sa] scl[sb] hd_n[t]        n 27..29, t 14..26, sa 7..13, sb 0..6
+// B: G_n,i (-C[r][n] / (h tf^2))     n, i 22..26, r 19..21        (t_f, X_{r,i})
+// C: G_n,i 2 xdot_i / tf^2           n, i 22..26                   (t_f, t_f)
+// D: sigma 2 (tracking weight)       n, sub 22..23 (0 coll x, 1 coll z, 2 u), i 17..21
+inline unsigned hta(int n, int t, int sa, int sb) {
+    return ((unsigned)kHTA << 30) | ((unsigned)n << 27) | ((unsigned)t << 14) | ((unsigned)sa << 7) | (unsigned)sb;
+}
+inline unsigned htb(int n, int i, int r) {
+    return ((unsigned)kHTB << 30) | ((unsigned)n << 27) | ((unsigned)i << 22) | ((unsigned)r << 19);
+}
+inline unsigned htc(int n, int i) { return ((unsigned)kHTC << 30) | ((unsigned)n << 27) | ((unsigned)i << 22); }
+inline unsigned htd(int n, int sub, int i) {
+    return ((unsigned)kHTD << 30) | ((unsigned)n << 27) | ((unsigned)sub << 22) | ((unsigned)i << 17);
+}
+
+struct HessTables {
+    int ntask[2] = {0, 0}, task_off[2] = {0, 0}, npair1 = 0;   // kind 1: npair1 pair tasks, then K3_NX G tasks
+    std::vector<int> task;              // p | q << 8, per kind
+    std::vector<int> colind, row;       // upper-triangular CCS of the V-space Hessian
+    int nnz = 0;
+    std::vector<int> slot0, nslot;      // [n_k] contiguous local slots of interval k
+    std::vector<int> gslot;             // slots of the global-global entries (theta, phi)
+    std::vector<int> xnslot;            // slots of the terminal (x[N], x[N]) diagonal
+    std::vector<int> ent_off;           // [n_k + 1]: entries of interval k = nslot[k] local + globals
+    std::vector<int> term_off;
+    std::vector<unsigned> terms;
+};
+
+// node variables each direction seeds (shooting node: itself; Radau node: a state direction
+// also moves its xdot, the t_f direction moves every xdot)
+inline uint32_t hdir_vars(int kind, int dir) {
+    if (dir == kGTask) return 0u;
+    if (kind == 0) return 1u << dir;
+    if (dir < K3_NX) return (1u << dir) | (1u << (K3_NX + dir));
+    if (dir == kDirTf) return ((1u << K3_NX) - 1u) << K3_NX;
+    return 1u << dir;
+}
+
+// V columns (with scale index: 0 -> 1, 1 + r NN + n -> C[r][n] / (h tf)) direction `dir` of node
+// `n` of interval k feeds (the first-order gather list's columns)
+inline void hdir_columns(const Layout& L, int k, int n, int dir, std::vector<std::pair<int, int>>& cols) {
+    const int NN = L.d + 1;
+    cols.clear();
+    if (dir == kDirGamma) { cols.emplace_back(K3_NTH + 0, 0); return; }
+    if (dir >= 2 * K3_NX + K3_NU + K3_NZ) { cols.emplace_back(dir - (2 * K3_NX + K3_NU + K3_NZ), 0); return; }
+    if (dir >= 2 * K3_NX && dir < 2 * K3_NX + K3_NU) { cols.emplace_back(L.u(k, dir - 2 * K3_NX), 0); return; }
+    if (n == 0) {
+        if (dir < K3_NX) cols.emplace_back(L.x(k, dir), 0);
+        else if (dir < 2 * K3_NX) cols.emplace_back(L.xdot(k, dir - K3_NX), 0);
+        else cols.emplace_back(L.z(k), 0);
+        return;
+    }
+    if (dir < K3_NX) { cols.emplace_back(L.coll_x(k, n - 1, dir), 0); return; }
+    if (dir < 2 * K3_NX) {
+        for (int r = 0; r < NN; ++r)
+            if (r != n) cols.emplace_back(L.X(k, r, dir - K3_NX), 1 + r * NN + n);
+        return;
+    }
+    cols.emplace_back(L.coll_z(k, n - 1), 0);
+}
+
+}  // namespace k3t
+
+namespace awt {
+inline HDep sin(const HDep& x) { return hdep_nl(x); }
+inline HDep cos(const HDep& x) { return hdep_nl(x); }
+}  // namespace awt
+
+namespace k3t {
+
+inline int build_hess_tables(const Tables& T, const double* consts, HessTables& H, std::string& err) {
+    const Layout& L = T.lay;
+    const int n_k = L.n_k, d = L.d, NN = d + 1;
+    struct HSink {
+        awt::HDep rows[kRowsPerNode];
+        void eq_row(int r, const awt::HDep& v) { rows[r] = v; }
+        void ineq_row(int r, const awt::HDep& v) { rows[K3_N_EQ + r] = v; }
+    };
+    struct HIn { awt::HDep operator()(int i) const { return awt::HDep::var(i); } };
+    HSink hs;
+    awe::kite3_node<awt::HDep>(HIn{}, awt::HDep::var(kDirGamma), 5.0, consts, hs, true);
+    auto interacts = [&](int r, uint32_t va, uint32_t vb) {
+        for (int u = 0; u < 32; ++u)
+            if (((va >> u) & 1u) && (hs.rows[r].h[u] & (unsigned long long)vb)) return true;
+        return false;
+    };
+    H.task.clear();
+    for (int kind = 0; kind < 2; ++kind) {
+        H.task_off[kind] = (int)H.task.size();
+        const int nrows = kind == 0 ? kRowsPerNode : K3_N_EQ;
+        for (int p = 0; p < kLanes; ++p)
+            for (int q = p; q < kLanes; ++q) {
+                const uint32_t vp = hdir_vars(kind, p), vq = hdir_vars(kind, q);
+                bool nz = false;
+                for (int r = 0; r < nrows && !nz; ++r) nz = interacts(r, vp, vq);
+                if (nz) H.task.push_back(p | (q << 8));
+            }
+        if (kind == 1) {
+            H.npair1 = (int)H.task.size() - H.task_off[1];
+            for (int i = 0; i < K3_NX; ++i) H.task.push_back((K3_NX + i) | (kGTask << 8));
+        }
+        H.ntask[kind] = (int)H.task.size() - H.task_off[kind];
+    }
+    if (H.ntask[0] >= 8192 || H.ntask[1] >= 8192) { err = "internal: too many Hessian tasks"; return 1; }
+
+    // ---- V-space entries and their terms -------------------------------------------------------
+    const int itf = 1;                                  // V index of theta.t_f
+    std::vector<std::pair<long long, unsigned>> ent;    // (key = col n_v + row, term)
+    std::vector<int> ent_k;
+    std::vector<std::pair<int, int>> ca, cb;
+    auto add = [&](int k, int r0, int c0, unsigned term) {
+        if (r0 > c0) std::swap(r0, c0);
+        ent.emplace_back((long long)c0 * L.n_v + r0, term);
+        ent_k.push_back(k);
+    };
+    for (int k = 0; k < n_k; ++k) {
+        for (int n = 0; n < NN; ++n) {
+            const int kind = n > 0;
+            const int np = kind == 0 ? H.ntask[0] : H.npair1;
+            for (int t = 0; t < np; ++t) {
+                const int pq = H.task[H.task_off[kind] + t], p = pq & 0xff, q = pq >> 8;
+                hdir_columns(L, k, n, p, ca);
+                hdir_columns(L, k, n, q, cb);
+                for (size_t a = 0; a < ca.size(); ++a)
+                    for (size_t b = (p == q ? a : 0); b < cb.size(); ++b) {
+                        int r0 = ca[a].first, c0 = cb[b].first, sa = ca[a].second, sb = cb[b].second;
+                        if (r0 > c0) { std::swap(r0, c0); std::swap(sa, sb); }
+                        add(k, r0, c0, hta(n, t, sa, sb));
+                    }
+            }
+            if (n == 0) continue;
+            for (int i = 0; i < K3_NX; ++i) {
+                for (int r = 0; r < NN; ++r) add(k, itf, L.X(k, r, i), htb(n, i, r));
+                add(k, itf, itf, htc(n, i));
+                add(k, L.coll_x(k, n - 1, i), L.coll_x(k, n - 1, i), htd(n, 0, i));
+            }
+            add(k, L.coll_z(k, n - 1), L.coll_z(k, n - 1), htd(n, 1, 0));
+        }
+        for (int i = 0; i < K3_NU; ++i) add(k, L.u(k, i), L.u(k, i), htd(0, 2, i));
+    }
+    std::vector<long long> keys;
+    keys.reserve(ent.size() + K3_NX);
+    for (auto& e : ent) keys.push_back(e.first);
+    for (int i = 0; i < K3_NX; ++i) keys.push_back((long long)L.x(n_k, i) * L.n_v + L.x(n_k, i));   // terminal cost
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    H.nnz = (int)keys.size();
+    H.colind.assign(L.n_v + 1, 0);
+    H.row.resize(H.nnz);
+    for (int i = 0; i < H.nnz; ++i) {
+        H.colind[keys[i] / L.n_v + 1]++;
+        H.row[i] = (int)(keys[i] % L.n_v);
+    }
+    for (int c = 0; c < L.n_v; ++c) H.colind[c + 1] += H.colind[c];
+    auto slot_of = [&](long long key) { return (int)(std::lower_bound(keys.begin(), keys.end(), key) - keys.begin()); };
+    H.gslot.clear();
+    for (int c = 0; c < L.v_int0; ++c)
+        for (int s = H.colind[c]; s < H.colind[c + 1]; ++s) H.gslot.push_back(s);
+    H.xnslot.clear();
+    for (int i = 0; i < K3_NX; ++i) H.xnslot.push_back(slot_of((long long)L.x(n_k, i) * L.n_v + L.x(n_k, i)));
+    const int ng = (int)H.gslot.size();
+    H.slot0.resize(n_k);
+    H.nslot.resize(n_k);
+    for (int k = 0; k < n_k; ++k) {
+        H.slot0[k] = H.colind[L.x(k, 0)];
+        H.nslot[k] = H.colind[L.x(k + 1, 0)] - H.slot0[k];
+    }
+    // every x[N] slot is a terminal diagonal entry (finalize kernel)
+    if (H.colind[L.n_v] - H.colind[L.x(n_k, 0)] != K3_NX) { err = "internal: x[N] Hessian columns"; return 1; }
+    std::vector<std::vector<unsigned>> bucket;
+    H.ent_off.assign(n_k + 1, 0);
+    for (int k = 0; k < n_k; ++k) H.ent_off[k + 1] = H.ent_off[k] + H.nslot[k] + ng;
+    bucket.resize(H.ent_off[n_k]);
+    for (size_t e = 0; e < ent.size(); ++e) {
+        const int k = ent_k[e];
+        const int slot = slot_of(ent[e].first);
+        const int col = (int)(ent[e].first / L.n_v);
+        int idx;
+        if (col < L.v_int0) {
+            idx = (int)(std::find(H.gslot.begin(), H.gslot.end(), slot) - H.gslot.begin()) + H.nslot[k];
+        } else {
+            idx = slot - H.slot0[k];
+            if (idx < 0 || idx >= H.nslot[k]) { err = "internal: Hessian entry outside its interval"; return 1; }
+        }
+        bucket[H.ent_off[k] + idx].push_back(ent[e].second);
+    }
+    H.term_off.assign(bucket.size() + 1, 0);
+    H.terms.clear();
+    for (size_t i = 0; i < bucket.size(); ++i) {
+        H.term_off[i + 1] = H.term_off[i] + (int)bucket[i].size();
+        H.terms.insert(H.terms.end(), bucket[i].begin(), bucket[i].end());
+    }
+    return 0;
+}
+
 }  // namespace k3t

@@ -22,7 +22,8 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libawempc.
 
 EXPORTED_SYMBOLS = ["awempc_create", "awempc_destroy", "awempc_last_error", "awempc_sizes",
                     "awempc_sparsity_jac", "awempc_sparsity_jac_static", "awempc_eval_nlp",
-                    "awempc_eval_nlp_host", "awempc_last_kernel_ms"]
+                    "awempc_eval_nlp_host", "awempc_last_kernel_ms", "awempc_hess_init", "awempc_sparsity_hess",
+                    "awempc_sparsity_hess_static", "awempc_eval_hess", "awempc_eval_hess_host", "awempc_last_hess_ms"]
 
 
 def load_library(path: str = _LIB_PATH):
@@ -44,6 +45,12 @@ def load_library(path: str = _LIB_PATH):
     lib.awempc_eval_nlp.argtypes = [h] + [ctypes.c_void_p] * 7
     lib.awempc_eval_nlp_host.argtypes = [h, dp, dp, dp, dp, dp, dp]
     lib.awempc_last_kernel_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.awempc_hess_init.argtypes = [h, ip]
+    lib.awempc_sparsity_hess.argtypes = [h, ip, ip]
+    lib.awempc_sparsity_hess_static.argtypes = [ctypes.c_int, ctypes.c_int, dp, ctypes.c_int, ip, ip, ip]
+    lib.awempc_eval_hess.argtypes = [h] + [ctypes.c_void_p] * 6
+    lib.awempc_eval_hess_host.argtypes = [h, dp, dp, dp, dp, dp]
+    lib.awempc_last_hess_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float)]
     _LIB = lib
     return lib
 
@@ -62,6 +69,24 @@ def sparsity_jac_static(consts: k3.Kite3Constants):
     row = np.zeros(nnz.value, dtype=np.int32)
     if lib.awempc_sparsity_jac_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
                                       colind.ctypes.data_as(ip), row.ctypes.data_as(ip)) != AWE_OK:
+        raise AwegpuError(lib.awempc_last_error().decode())
+    return colind, row
+
+
+def sparsity_hess_static(consts: k3.Kite3Constants):
+    """Upper-triangular CCS pattern (colind, row) of the MPC nlp_hess_l, derived on the CPU."""
+    lib = load_library()
+    cfg = consts.cfg
+    c = np.ascontiguousarray(consts.consts, dtype=np.float64)
+    nnz = ctypes.c_int()
+    ip = ctypes.POINTER(ctypes.c_int)
+    if lib.awempc_sparsity_hess_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz), None, None) != AWE_OK:
+        raise AwegpuError(lib.awempc_last_error().decode())
+    lay = k3.MpcLayout(cfg.n_k, cfg.d)
+    colind = np.zeros(lay.n_v + 1, dtype=np.int32)
+    row = np.zeros(nnz.value, dtype=np.int32)
+    if lib.awempc_sparsity_hess_static(cfg.n_k, cfg.d, _dptr(c), c.size, ctypes.byref(nnz),
+                                       colind.ctypes.data_as(ip), row.ctypes.data_as(ip)) != AWE_OK:
         raise AwegpuError(lib.awempc_last_error().decode())
     return colind, row
 
@@ -131,6 +156,65 @@ class MpcEvaluator:
         a, b = ctypes.c_float(), ctypes.c_float()
         self._check(self._lib.awempc_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    # ---------------------------------------------- nlp_hess_l ---------------------------
+    @property
+    def nnz_h(self):
+        if getattr(self, "_hcolind", None) is None:
+            n = ctypes.c_int()
+            self._check(self._lib.awempc_hess_init(self._h, ctypes.byref(n)))
+            self._hcolind = np.zeros(self.n_v + 1, dtype=np.int32)
+            self._hrow = np.zeros(n.value, dtype=np.int32)
+            ip = ctypes.POINTER(ctypes.c_int)
+            self._check(self._lib.awempc_sparsity_hess(self._h, self._hcolind.ctypes.data_as(ip),
+                                                       self._hrow.ctypes.data_as(ip)))
+        return len(self._hrow)
+
+    def sparsity_hess(self):
+        """Upper-triangular CCS pattern of nlp_hess_l: (colind[n_v+1], row[nnz_h])."""
+        _ = self.nnz_h
+        return self._hcolind.copy(), self._hrow.copy()
+
+    def hess_csc(self, values, full=True):
+        import scipy.sparse as sp
+        _ = self.nnz_h
+        U = sp.csc_matrix((np.asarray(values), self._hrow, self._hcolind), shape=(self.n_v, self.n_v))
+        return (U + sp.triu(U, 1).T).tocsc() if full else U
+
+    def eval_hess_device(self, V, p, sigma, lam_g, H, stream=None):
+        """Upper-triangular values of the Hessian of sigma f + lam^T g for all instances; contiguous
+        float64 CUDA tensors [B, n_v], [B, n_p], [B], [B, n_g], [B, nnz_h]."""
+        import torch
+        nh = self.nnz_h
+        for t, n in ((V, self.n_v), (p, self.n_p), (sigma, 1), (lam_g, self.n_g), (H, nh)):
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
+                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.awempc_eval_hess(self._h, V.data_ptr(), p.data_ptr(), sigma.data_ptr(),
+                                               lam_g.data_ptr(), H.data_ptr(), ctypes.c_void_p(s)))
+
+    def eval_hess(self, V, p, sigma, lam_g):
+        """Host arrays in, host array out: H [B, nnz_h] (upper triangle, CCS)."""
+        nh = self.nnz_h
+        V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))
+        p = np.ascontiguousarray(np.asarray(p, dtype=np.float64).reshape(self.batch, self.n_p))
+        sig = np.ascontiguousarray(np.broadcast_to(np.asarray(sigma, dtype=np.float64), (self.batch,)))
+        lam = np.ascontiguousarray(np.asarray(lam_g, dtype=np.float64).reshape(self.batch, self.n_g))
+        H = np.zeros((self.batch, nh))
+        self._check(self._lib.awempc_eval_hess_host(self._h, _dptr(V), _dptr(p), _dptr(sig), _dptr(lam), _dptr(H)))
+        return H
+
+    def nlp_hess_l(self, x, p, lam_f, lam_g):
+        """CasADi nlp_hess_l: Hessian of lam_f f + lam_g^T g (upper triangle, CCS values)."""
+        if self.batch != 1:
+            raise ValueError("the oracle-named entry points evaluate one instance (batch=1)")
+        return self.eval_hess(np.asarray(x).reshape(1, -1), np.asarray(p).reshape(1, -1), lam_f,
+                              np.asarray(lam_g).reshape(1, -1))[0]
+
+    def last_hess_ms(self):
+        a = ctypes.c_float()
+        self._check(self._lib.awempc_last_hess_ms(self._h, ctypes.byref(a)))
+        return a.value
 
     # ---------------------------------------------- host path --------------------------
     def eval_nlp(self, V, p):

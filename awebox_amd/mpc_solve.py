@@ -8,10 +8,11 @@ solver sees:
 * variable bounds (kite3.variable_bounds: system bounds on x[1..N], u, z; x[0] released; f_fict,
   theta, phi, xi fixed) and the path inequalities (tether stress, acceleration; released at k = 0,
   pmpc.py:125-131) as inequality rows with slacks;
-* the Hessian of the Lagrangian -- IPOPT's default is the exact one (pmpc.py:193-217,
-  default.py:323) -- approximated by coloured central differences of the HIP MPC evaluator's
-  exact gradients (fd_hessian.FdHessian, terminal-cost columns included, agreement with the
-  oracle's autograd Hessian to 1e-6), one batched launch per Hessian;
+* the exact Hessian of the Lagrangian (IPOPT's default, pmpc.py:193-217, default.py:323) from the
+  HIP MPC evaluator's hyper-dual Hessian kernel (awempc_eval_hess: one thread per structurally
+  nonzero direction pair of a node, tracking cost added in closed form), one batched launch per
+  Hessian; coloured central differences of the exact gradient (fd_hessian.FdHessian) remain as
+  ``hessian="fd"`` for evaluators without a Hessian;
 * ``homotopy_warmstart`` (mpc_closed_loop.py:69): a 2-iteration pre-solve at mu = 1e-3
   (``mu_init = mu_target = 1e-3``, ``tol = 1e-4``, ``max_iter = 2``, pmpc.py:206-212) whose
   primal point starts the main solve (``mu_init = 1e-3``, ``tol = 1e-6``, pmpc.py:199-207);
@@ -90,17 +91,23 @@ class BatchedPmpc(BatchedRti):
 
     def __init__(self, consts: k3.Kite3Constants, batch: int, device="cuda", evaluator=None,
                  make_batched=None, plant="collocation", n_fe=20, homotopy_warmstart=True,
-                 opts: IpmOptions | None = None):
-        """``make_batched(b)``: an evaluator of the same NLP for b instances (the Hessian's
-        perturbed evaluations); default = the HIP MPC evaluator."""
+                 opts: IpmOptions | None = None, hessian="exact"):
+        """``hessian``: "exact" -- the evaluator's own nlp_hess_l (the HIP hyper-dual Hessian kernel,
+        IPOPT's default exact Hessian); "fd" -- coloured central differences of the exact gradient
+        (fd_hessian.FdHessian, ``make_batched(b)``: an evaluator of the same NLP for b instances, by
+        default the HIP MPC evaluator), for evaluators without a Hessian."""
         super().__init__(consts, batch, device=device, evaluator=evaluator, plant=plant, n_fe=n_fe,
                          fix_fict=True)
-        if make_batched is None:
-            from .mpc import MpcEvaluator
+        if hessian == "exact" and hasattr(self.ev, "eval_hess_device"):
+            self.nlp_ev = self.ev
+        else:
+            if make_batched is None:
+                from .mpc import MpcEvaluator
 
-            def make_batched(b):
-                return MpcEvaluator(consts, batch=b)
-        self.nlp_ev = FdHessian(self.ev, make_batched, self.lay, device=self.dev, tail=True)
+                def make_batched(b):
+                    return MpcEvaluator(consts, batch=b)
+            self.nlp_ev = FdHessian(self.ev, make_batched, self.lay, device=self.dev, tail=True)
+        self.hessian = "exact" if self.nlp_ev is self.ev else "fd"
         self.lbx, self.ubx = k3.variable_bounds(consts, self.lay)
         self.lbg, self.ubg = self.lay.g_bounds()
         self.homotopy_warmstart = homotopy_warmstart

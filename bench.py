@@ -577,7 +577,9 @@ def pmpc_block(c, B, dev, dist, world, steps=3, warmup=1):
             "tracking_error_max": float(out["tracking_error"].max()),
             "reference": REFERENCE_NOTE,
             "solver": "batched IPM (mu_init 1e-3, tol 1e-6, 2-iteration homotopy pre-solve), bounds and path "
-                      "inequalities, Hessian of the Lagrangian by coloured central differences of the exact HIP gradient"}
+                      "inequalities, exact Hessian of the Lagrangian (awempc_eval_hess: hyper-dual direction-pair kernel)"
+                      if r.hessian == "exact" else "batched IPM, Hessian by coloured central differences",
+            "hessian_ms_last": r.ev.last_hess_ms() if r.hessian == "exact" else None}
 
 
 SWEEP_GRID = 64       # config 4: u_ref = linspace(5, 8, 64), 8 contiguous points per GPU

@@ -9,8 +9,11 @@
  *              awebox/pmpc.py:193-217, called per MPC step at pmpc.py:252-270 with
  *              p = [x0, ref, u_ref, Q, R, P] (pmpc.py:166-186)
  *
- *   awempc_eval_nlp     <->  nlp_grad_f + nlp_jac_g fused (f, g, grad f, J_g values)
- *   awempc_sparsity_jac <->  Sparsity of nlp_jac_g's output (CCS: colind[n_v+1], row[nnz])
+ *   awempc_eval_nlp      <->  nlp_grad_f + nlp_jac_g fused (f, g, grad f, J_g values)
+ *   awempc_sparsity_jac  <->  Sparsity of nlp_jac_g's output (CCS: colind[n_v+1], row[nnz])
+ *   awempc_eval_hess     <->  nlp_hess_l: sigma f + lam^T g, upper triangle in a fixed CCS pattern
+ *                             (IPOPT's exact Hessian, awebox/opts/default.py:323, pmpc.py:193-217)
+ *   awempc_sparsity_hess <->  Sparsity of nlp_hess_l's output
  *
  * Memory: V[b*n_v + i], p[b*n_p + i], g[b*n_g + i], grad_f[b*n_v + i], jac[b*nnz + i], f[b] are
  * device pointers for awempc_eval_nlp, host pointers for awempc_eval_nlp_host.  Return codes as in
@@ -89,6 +92,24 @@ int awempc_eval_nlp_host(awempc_handle h, const double* V, const double* p, doub
                          double* grad_f, double* jac);
 /* kernel time of the last awempc_eval_nlp (HIP events on its stream), ms */
 int awempc_last_kernel_ms(awempc_handle h, float* ms_main, float* ms_finalize);
+
+/* ---- nlp_hess_l ----------------------------------------------------------------------------------
+ * Hessian of sigma f + lam^T g w.r.t. V, upper triangle (row <= col), CCS over the n_v columns:
+ * H[b*nnz_h + i].  sigma[b], lam[b*n_g + i].  The structure is derived on the host from the node
+ * model's second-order dependencies (built on the first call). */
+int awempc_hess_init(awempc_handle h, int* nnz_h);
+int awempc_sparsity_hess(awempc_handle h, int* colind, int* row);
+/* the same pattern without a device; colind = row = NULL returns *nnz */
+int awempc_sparsity_hess_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind,
+                                int* row);
+/* device pointers, asynchronous on `stream` */
+int awempc_eval_hess(awempc_handle h, const double* V, const double* p, const double* sigma, const double* lam_g,
+                     double* H, void* stream);
+/* host pointers: copy in, evaluate, copy out, synchronise, check finiteness */
+int awempc_eval_hess_host(awempc_handle h, const double* V, const double* p, const double* sigma,
+                          const double* lam_g, double* H);
+/* kernel time (Hessian + finalize) of the last awempc_eval_hess, ms */
+int awempc_last_hess_ms(awempc_handle h, float* ms);
 
 #ifdef __cplusplus
 }

@@ -36,7 +36,7 @@ import math
 
 import numpy as np
 import torch
-from torch.func import grad, jacfwd, jvp, vmap
+from torch.func import grad, hessian, jacfwd, jvp, vmap
 
 from oracle.ap2_oracle import Ap2Oracle, cross, norm, smooth_abs, smooth_norm, smooth_sqrt
 
@@ -303,6 +303,26 @@ class Kite3Oracle:
     def nlp_grad_f(self, V, p, lay):
         V = torch.as_tensor(V)
         return grad(lambda vv: self.nlp_f(vv, p, lay))(V)
+
+    def nlp_hess_l(self, V, p, sigma, lam, lay):
+        """Dense Hessian of sigma f + lam^T g (nlp_hess_l): per interval the Hessian of
+        lam_k^T rows_k(wloc) by torch.func (the initial-condition rows are linear), scattered into
+        V space; plus sigma times the Hessian of the tracking cost."""
+        V, p = torch.as_tensor(V), torch.as_tensor(p)
+        lam = torch.as_tensor(np.asarray(lam, dtype=np.float64))
+        u_ref = p[lay.p_u_ref]
+        idx = np.stack([self.local_index(lay, k) for k in range(self.n_k)])
+        lk = torch.stack([lam[NX + k * lay.rows_per_interval:NX + (k + 1) * lay.rows_per_interval]
+                          for k in range(self.n_k)])
+
+        def lag(wloc, mu):
+            return torch.dot(mu, self.interval_rows(wloc, u_ref))
+        Hk = vmap(hessian(lag), in_dims=(0, 0))(V[torch.as_tensor(idx)], lk).numpy()
+        H = np.zeros((lay.n_v, lay.n_v))
+        for k in range(self.n_k):
+            H[np.ix_(idx[k], idx[k])] += Hk[k]
+        Hf = hessian(lambda vv: self.nlp_f(vv, p, lay))(V).numpy()
+        return H + float(sigma) * Hf
 
 
 def from_constants(k3, lay):

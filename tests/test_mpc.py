@@ -267,3 +267,48 @@ def test_mpc_p_from_reference_and_p_fun():
     p3[lay.p_u_ref] += 1.0
     assert k3.p_fun(p3, lay)[("theta0", "wind", "u_ref")][0] == p[lay.p_u_ref] + 1.0
     assert not np.allclose(orc.nlp_g(V, p3, lay).numpy(), g)
+
+
+# ---- nlp_hess_l (exact Hessian of the MPC NLP, pmpc.py:193-217 with IPOPT's default) ------------
+def _hess_inputs(c, lay, B=1, seed=3):
+    rng = np.random.default_rng(seed)
+    Vs, ps = zip(*(k3.batch_instance(c, lay, i, max(B, 4)) for i in range(B)))
+    lam = rng.standard_normal((B, lay.n_g))
+    sig = 1.0 + rng.random(B)
+    return np.stack(Vs), np.stack(ps), sig, lam
+
+
+def test_hessian_pattern_covers_oracle():
+    """The host-derived nlp_hess_l pattern (second-order dependency analysis of kite3_node) is a
+    superset of the oracle's structural non-zeros at a generic point (N=3 d=2 and N=4 d=4)."""
+    from awebox_amd.mpc import sparsity_hess_static
+    for n_k, d in ((3, 2), (4, 4)):
+        c, lay, orc = _setup(n_k=n_k, d=d)
+        V, p, sig, lam = _hess_inputs(c, lay)
+        Ho = orc.nlp_hess_l(V[0], p[0], sig[0], lam[0], lay)
+        colind, row = sparsity_hess_static(c)
+        pat = sp.csc_matrix((np.ones(len(row)), row, colind), shape=(lay.n_v, lay.n_v)).toarray() > 0
+        upper = np.triu(np.abs(Ho) > 0)
+        missing = upper & ~pat
+        assert not missing.any(), np.argwhere(missing)[:10]
+        assert np.all(np.diff(colind) >= 0) and np.all(row <= np.repeat(np.arange(lay.n_v), np.diff(colind)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_k,d,B", [(3, 2, 2), (20, 4, 3)])
+def test_hessian_matches_oracle_gpu(n_k, d, B):
+    """HIP nlp_hess_l (hyper-dual direction-pair kernel) against the oracle's automatic Hessian:
+    per column |a - b| <= 1e-9 |b| + 1e-11 max|b| (fp64, evaluation order only), for B instances
+    with different sigma and lambda; bitwise repeatable."""
+    from awebox_amd.mpc import MpcEvaluator
+    c, lay, orc = _setup(n_k=n_k, d=d)
+    V, p, sig, lam = _hess_inputs(c, lay, B=B)
+    ev = MpcEvaluator(c, batch=B)
+    H = ev.eval_hess(V, p, sig, lam)
+    assert np.array_equal(H, ev.eval_hess(V, p, sig, lam))
+    for b in range(B):
+        Ho = np.triu(orc.nlp_hess_l(V[b], p[b], sig[b], lam[b], lay))
+        Hk = ev.hess_csc(H[b], full=False).toarray()
+        scale = np.abs(Ho).max()
+        err = np.abs(Hk - Ho)
+        assert np.all(err <= RTOL * np.abs(Ho) + ATOL_REL * scale), (err.max(), np.unravel_index(err.argmax(), err.shape))
