@@ -29,23 +29,46 @@ constexpr int kMaxN = 1024;
 
 thread_local std::string g_err;
 
+// dst(t) = src(t) for t = tid, tid + kThreads, ... < total with U global loads of a thread in flight
+// before its first store: a plain loop waits one memory latency per element (the compiler cannot
+// move the next load above a store it cannot disambiguate), which made the LDS staging of the
+// factor panels and right-hand sides latency-bound.
+template <int U, class Ld, class St>
+__device__ __forceinline__ void copy_batched(int total, int tid, int nthreads, Ld ld, St st) {
+    for (int t0 = tid; t0 < total; t0 += U * nthreads) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = t0 + u * nthreads;
+            v[u] = t < total ? ld(t) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = t0 + u * nthreads;
+            if (t < total) st(t, v[u]);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __restrict__ As, int* __restrict__ pivs) {
     extern __shared__ double panel[];                   // [n][kNB], row-major
     __shared__ double red_v[kThreads / 64];
     __shared__ int red_i[kThreads / 64];
     __shared__ int piv_loc[kNB];
+    __shared__ int orgmap[kMaxN];                       // row -> original row under the panel's swaps
+    __shared__ int perm_pos[2 * kNB], perm_org[2 * kNB]; // the panel's interchanges as one permutation
     double* A = As + (size_t)blockIdx.x * n * n;
     int* piv = pivs + (size_t)blockIdx.x * n;
     const int tid = threadIdx.x;
+    for (int i = tid; i < n; i += kThreads) orgmap[i] = i;
 
     for (int k0 = 0; k0 < n; k0 += kNB) {
         const int kb = min(kNB, n - k0);
         const int rows = n - k0;
         // ---- stage the panel A[k0:n, k0:k0+kb] ----------------------------------------------
-        for (int t = tid; t < rows * kb; t += kThreads) {
-            const int r = t / kb, c = t % kb;
-            panel[r * kNB + c] = A[(size_t)(k0 + r) * n + k0 + c];
-        }
+        copy_batched<8>(rows * kb, tid, kThreads,
+                        [&](int t) { return A[(size_t)(k0 + t / kb) * n + k0 + t % kb]; },
+                        [&](int t, double v) { panel[(t / kb) * kNB + t % kb] = v; });
         __syncthreads();
         // ---- factorise the panel with partial pivoting ----------------------------------------
         for (int c = 0; c < kb; ++c) {
@@ -71,7 +94,12 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
                 if (red_v[w] > best || (red_v[w] == best && red_i[w] < bi)) { best = red_v[w]; bi = red_i[w]; }
             }
             const int p = bi;
-            if (tid == 0) piv_loc[c] = p;
+            if (tid == 0) {
+                piv_loc[c] = p;
+                const int o = orgmap[k0 + c];                // the same interchange on the row map
+                orgmap[k0 + c] = orgmap[k0 + p];
+                orgmap[k0 + p] = o;
+            }
             if (p != c && tid < kb) {                        // swap panel rows c and p
                 const double a = panel[c * kNB + tid];
                 panel[c * kNB + tid] = panel[p * kNB + tid];
@@ -87,43 +115,70 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
             }
             __syncthreads();
         }
-        // ---- write the panel back, record pivots, apply the swaps outside the panel ----------------
+        // ---- write the panel back, record pivots; the kb sequential interchanges as one permutation
+        //      of the rows they touch (positions k0 + c and k0 + piv_loc[c]; a position listed twice
+        //      moves the same value twice), applied with all loads of a column before its stores --
         for (int t = tid; t < rows * kb; t += kThreads) {
             const int r = t / kb, c = t % kb;
             A[(size_t)(k0 + r) * n + k0 + c] = panel[r * kNB + c];
         }
         if (tid < kb) piv[k0 + tid] = k0 + piv_loc[tid] + 1;
-        for (int j = tid; j < n; j += kThreads) {            // interchanges outside the panel: each
-            if (j >= k0 && j < k0 + kb) continue;            // thread owns its columns, no barriers
-            for (int c = 0; c < kb; ++c) {
-                const int p = piv_loc[c];
-                if (p == c) continue;
-                const size_t ra = (size_t)(k0 + c) * n, rb = (size_t)(k0 + p) * n;
-                const double a = A[ra + j];
-                A[ra + j] = A[rb + j];
-                A[rb + j] = a;
-            }
+        if (tid < 2 * kNB) {
+            const int pos = tid < kb ? k0 + tid : (tid - kNB < kb && tid >= kNB ? k0 + piv_loc[tid - kNB] : k0);
+            perm_pos[tid] = pos;
+            perm_org[tid] = orgmap[pos];
         }
         __syncthreads();
-        // ---- U12 (forward substitution with L11) and the trailing update, one column per thread --
+        if (tid < 2 * kNB) orgmap[perm_pos[tid]] = perm_pos[tid];   // back to the identity
+        for (int j = tid; j < n; j += kThreads) {            // interchanges outside the panel: each
+            if (j >= k0 && j < k0 + kb) continue;            // thread owns its columns
+            double v[2 * kNB];
+#pragma unroll
+            for (int e = 0; e < 2 * kNB; ++e) v[e] = A[(size_t)perm_org[e] * n + j];
+#pragma unroll
+            for (int e = 0; e < 2 * kNB; ++e) A[(size_t)perm_pos[e] * n + j] = v[e];
+        }
+        __syncthreads();
+        // ---- U12 (forward substitution with L11) and the trailing update, one column per thread:
+        //      the column's kb U12 rows loaded together, then the trailing rows in groups of kRowU
+        //      whose loads are issued one group ahead (a memory latency per group, not per row) --
+        constexpr int kRowU = 8;
         for (int j = k0 + kb + tid; j < n; j += kThreads) {
             double u[kNB];
 #pragma unroll
+            for (int r = 0; r < kNB; ++r) u[r] = r < kb ? A[(size_t)(k0 + r) * n + j] : 0.0;
+#pragma unroll
             for (int r = 0; r < kNB; ++r) {
                 if (r < kb) {
-                    double v = A[(size_t)(k0 + r) * n + j];
+                    double v = u[r];
                     for (int c = 0; c < r; ++c) v -= panel[r * kNB + c] * u[c];
                     u[r] = v;
-                    A[(size_t)(k0 + r) * n + j] = v;
-                } else {
-                    u[r] = 0.0;
                 }
             }
-            for (int i = kb; i < rows; ++i) {
-                double acc = A[(size_t)(k0 + i) * n + j];
 #pragma unroll
-                for (int c = 0; c < kNB; ++c) acc -= panel[i * kNB + c] * u[c];
-                A[(size_t)(k0 + i) * n + j] = acc;
+            for (int r = 0; r < kNB; ++r)
+                if (r < kb) A[(size_t)(k0 + r) * n + j] = u[r];
+            double nxt[kRowU];
+#pragma unroll
+            for (int q = 0; q < kRowU; ++q) nxt[q] = kb + q < rows ? A[(size_t)(k0 + kb + q) * n + j] : 0.0;
+            for (int i0 = kb; i0 < rows; i0 += kRowU) {
+                double acc[kRowU];
+#pragma unroll
+                for (int q = 0; q < kRowU; ++q) acc[q] = nxt[q];
+#pragma unroll
+                for (int q = 0; q < kRowU; ++q) {
+                    const int i = i0 + kRowU + q;
+                    nxt[q] = i < rows ? A[(size_t)(k0 + i) * n + j] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < kRowU; ++q) {
+                    const int i = i0 + q;
+                    if (i < rows) {
+#pragma unroll
+                        for (int c = 0; c < kNB; ++c) acc[q] -= panel[i * kNB + c] * u[c];
+                        A[(size_t)(k0 + i) * n + j] = acc[q];
+                    }
+                }
             }
         }
         __syncthreads();
@@ -150,7 +205,8 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
     double* Xg = Xs + (size_t)blockIdx.x * n * ldx + j0;
     const int tid = threadIdx.x;
 
-    for (int t = tid; t < n * w; t += kThreads) X[t] = Xg[(size_t)(t / w) * ldx + t % w];
+    copy_batched<8>(n * w, tid, kThreads, [&](int t) { return Xg[(size_t)(t / w) * ldx + t % w]; },
+                    [&](int t, double v) { X[t] = v; });
     __syncthreads();
     for (int j = tid; j < w; j += kThreads) {            // row interchanges, one column per thread
         for (int k = 0; k < n; ++k) {
@@ -166,10 +222,8 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
     // ---- forward substitution with the unit lower factor --------------------------------------
     for (int k0 = 0; k0 < n; k0 += kNB) {
         const int kb = min(kNB, n - k0), rows = n - k0;
-        for (int t = tid; t < rows * kb; t += kThreads) {
-            const int r = t / kb, c = t % kb;
-            panel[r * kNB + c] = A[(size_t)(k0 + r) * n + k0 + c];
-        }
+        copy_batched<8>(rows * kb, tid, kThreads, [&](int t) { return A[(size_t)(k0 + t / kb) * n + k0 + t % kb]; },
+                        [&](int t, double v) { panel[(t / kb) * kNB + t % kb] = v; });
         __syncthreads();
         for (int c = 0; c + 1 < kb; ++c) {
             for (int t = tid; t < (kb - 1 - c) * w; t += kThreads) {
@@ -189,10 +243,8 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
     // ---- backward substitution with the upper factor ------------------------------------------
     for (int k1 = ((n - 1) / kNB) * kNB; k1 >= 0; k1 -= kNB) {
         const int kb = min(kNB, n - k1), rows = k1 + kb;
-        for (int t = tid; t < rows * kb; t += kThreads) {
-            const int r = t / kb, c = t % kb;
-            panel[r * kNB + c] = A[(size_t)r * n + k1 + c];
-        }
+        copy_batched<8>(rows * kb, tid, kThreads, [&](int t) { return A[(size_t)(t / kb) * n + k1 + t % kb]; },
+                        [&](int t, double v) { panel[(t / kb) * kNB + t % kb] = v; });
         __syncthreads();
         for (int c = kb - 1; c >= 0; --c) {
             for (int j = tid; j < w; j += kThreads) X[(k1 + c) * w + j] /= panel[(k1 + c) * kNB + c];
@@ -236,18 +288,61 @@ constexpr size_t kSolveLds = 144 * 1024;
 //   cond ~1e11), so every block solve takes one refinement step with D'_k: Y += D'^-1 (Z - D' Y).
 // The factorisation is reused by every solve of an interior-point iteration (iterative
 // refinement), and the apply is one launch per solve instead of a library LU's dozens.
+// Templated on the workgroup size and the block limit.  A one-wave instantiation <64, 24> for the
+// MPC's m = 22 (no barriers between the Gauss-Jordan columns, the same arithmetic) measured slower
+// than <256, 48>: 1.28 vs 1.06 ms per 21-stage factorisation at B = 64 (tools/awelu_ab.py), so only
+// <256, 48> is instantiated.
 constexpr int kBtdMaxM = 48;
 constexpr int kBtdMaxRhs = 64;
-constexpr int kRG = kThreads / 64;                            // row groups of the 4 x 64 grid
 
-__global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, double* __restrict__ Ts,
-                                                             double* __restrict__ Dinvs) {
+// Max over the 64 lanes of a wave by DPP moves (quad permutes, row rotations, row broadcasts: VALU
+// latency) instead of a __shfl_xor butterfly (six dependent LDS-permute round trips); the result
+// is read from lane 63 and is uniform.  fmax is order-independent, so the value is the butterfly's.
+template <int Ctrl>
+__device__ __forceinline__ double mov_dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, Ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), Ctrl, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+    v = fmax(v, mov_dpp_f64<0xb1>(v));                        // quad_perm [1,0,3,2]
+    v = fmax(v, mov_dpp_f64<0x4e>(v));                        // quad_perm [2,3,0,1]
+    v = fmax(v, mov_dpp_f64<0x124>(v));                       // row_ror 4
+    v = fmax(v, mov_dpp_f64<0x128>(v));                       // row_ror 8
+    v = fmax(v, mov_dpp_f64<0x142>(v));                       // row_bcast 15
+    v = fmax(v, mov_dpp_f64<0x143>(v));                       // row_bcast 31
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Gauss-Jordan tile helpers of btd_factor_kernel (compile-time register indices)
+template <int Q, int TR, int TC>
+__device__ __forceinline__ void gj_publish_col(const double (&a)[TR][TC], double* colbuf, int rg, int m) {
+#pragma unroll
+    for (int r = 0; r < TR; ++r)
+        if (rg * TR + r < m) colbuf[rg * TR + r] = a[r][Q];
+}
+
+template <int R, int TR, int TC>
+__device__ __forceinline__ void gj_publish_row(const double (&a)[TR][TC], double* rowbuf, int cg) {
+#pragma unroll
+    for (int q = 0; q < TC; ++q) rowbuf[cg * TC + q] = a[R][q];
+}
+
+template <int NT, int MAXM>
+__global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* __restrict__ Ts,
+                                                       double* __restrict__ Dinvs) {
+    constexpr int kRG = NT / 64;                              // row groups of the kRG x 64 grid
     // two buffers of the augmented block [D | U | I]: every Gauss-Jordan column reads one and writes
     // the other (row interchange folded into the update), so a column costs one barrier; the
     // second buffer holds L_k while D' = D - L_k W_{k-1} is formed
-    __shared__ double R0[kBtdMaxM][3 * kBtdMaxM + 1];
-    __shared__ double R1[kBtdMaxM][3 * kBtdMaxM + 1];
-    __shared__ double Wp[kBtdMaxM][kBtdMaxM + 1];             // W_{k-1}
+    __shared__ double R0[MAXM][3 * MAXM + 1];
+    __shared__ double R1[MAXM][3 * MAXM + 1];
+    __shared__ double Wp[MAXM][MAXM + 1];             // W_{k-1}
     const int tid = threadIdx.x, tj = tid & 63, ti = tid >> 6;
     const size_t mm = (size_t)m * m;
     double* T = Ts + (size_t)blockIdx.x * nb * 3 * mm;
@@ -262,7 +357,7 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
         {
             // the stage's three blocks: every global load of a thread issued before its first LDS
             // store, so the 3 x 12 row loads overlap instead of paying one memory latency each
-            constexpr int R = kBtdMaxM / kRG;
+            constexpr int R = MAXM / kRG;
             double vd[R], vu[R], vl[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -287,7 +382,7 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
         if (k > 0) {                                          // D -= L_k W_{k-1}
             // thread (ti, tj): column j = tj (< m <= 48 < 64), rows ti, ti + 4, ...: 12 independent
             // accumulators per thread, so the LDS loads of one c step pipeline
-            constexpr int kRows = kBtdMaxM / kRG;
+            constexpr int kRows = MAXM / kRG;
             const int j = tj;
             if (j < m) {
                 double acc[kRows];
@@ -316,9 +411,9 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
         // owners publish column c and then the pivot row through LDS (two barriers), every thread
         // updates its 32 entries.  Rows are not interchanged: row piv[c] ends as row c of
         // [I | W | D'^-1] and is written there.
-        constexpr int kTR = 8, kTC = 4, kNCG = (3 * kBtdMaxM) / kTC;   // 36 column groups
+        constexpr int kTR = 8, kTC = 4, kNCG = (3 * MAXM) / kTC;   // 36 column groups
         const int rg = tid / kNCG, cg = tid - rg * kNCG;
-        const bool owner = rg < kBtdMaxM / kTR;
+        const bool owner = rg < MAXM / kTR;
         double a[kTR][kTC];
         if (owner) {
 #pragma unroll
@@ -339,32 +434,35 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
         for (int c = 0; c < m; ++c) {
             double* colbuf = &R1[(c & 1) ? 2 : 0][0];         // column c of the current matrix
             double* rowbuf = &R1[(c & 1) ? 3 : 1][0];         // the pivot row (3 m entries)
-            if (owner && cg == c / kTC) {
-#pragma unroll
-                for (int r = 0; r < kTR; ++r) {
-                    const int i = rg * kTR + r;
-#pragma unroll
-                    for (int q = 0; q < kTC; ++q)
-                        if (q == c % kTC && i < m) colbuf[i] = a[r][q];
+            if (owner && cg == c / kTC) {                     // c % kTC is uniform: a branch, not
+                switch (c % kTC) {                            // a select per register
+                    case 0: gj_publish_col<0>(a, colbuf, rg, m); break;
+                    case 1: gj_publish_col<1>(a, colbuf, rg, m); break;
+                    case 2: gj_publish_col<2>(a, colbuf, rg, m); break;
+                    default: gj_publish_col<3>(a, colbuf, rg, m); break;
                 }
             }
             __syncthreads();
-            // every wave finds the same pivot: the largest |entry| among unused rows by a max
-            // butterfly, then the smallest such row by one ballot (ties as before: lowest row)
+            // every wave finds the same pivot: the largest |entry| among unused rows by a DPP max
+            // reduction, then the smallest such row by one ballot (ties as before: lowest row)
             const bool cand = tj < m && !((usedmask >> tj) & 1ull);
             const double best = cand ? fabs(colbuf[tj]) : -1.0;
-            double mx = best;
-            for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+            const double mx = wave_max(best);
             unsigned long long hit = __ballot(cand && best == mx);
             if (hit == 0ull) hit = ~usedmask & ((1ull << m) - 1ull);    // all-NaN column: any unused row
             const int p = __ffsll((long long)hit) - 1;
             usedmask |= 1ull << p;
             if (owner && rg == p / kTR) {
-#pragma unroll
-                for (int r = 0; r < kTR; ++r)
-                    if (rg * kTR + r == p)
-#pragma unroll
-                        for (int q = 0; q < kTC; ++q) rowbuf[cg * kTC + q] = a[r][q];
+                switch (p % kTR) {
+                    case 0: gj_publish_row<0>(a, rowbuf, cg); break;
+                    case 1: gj_publish_row<1>(a, rowbuf, cg); break;
+                    case 2: gj_publish_row<2>(a, rowbuf, cg); break;
+                    case 3: gj_publish_row<3>(a, rowbuf, cg); break;
+                    case 4: gj_publish_row<4>(a, rowbuf, cg); break;
+                    case 5: gj_publish_row<5>(a, rowbuf, cg); break;
+                    case 6: gj_publish_row<6>(a, rowbuf, cg); break;
+                    default: gj_publish_row<7>(a, rowbuf, cg); break;
+                }
             }
             __syncthreads();
             const double rp = 1.0 / colbuf[p];
@@ -372,13 +470,25 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
                 double pr[kTC];
 #pragma unroll
                 for (int q = 0; q < kTC; ++q) pr[q] = rowbuf[cg * kTC + q] * rp;
+                if (rg == p / kTR) {                          // the pivot row's own group
 #pragma unroll
-                for (int r = 0; r < kTR; ++r) {
-                    const int i = rg * kTR + r;
-                    if (i < m) {
-                        const double f = colbuf[i];
+                    for (int r = 0; r < kTR; ++r) {
+                        const int i = rg * kTR + r;
+                        if (i < m) {
+                            const double f = colbuf[i];
 #pragma unroll
-                        for (int q = 0; q < kTC; ++q) a[r][q] = i == p ? pr[q] : a[r][q] - f * pr[q];
+                            for (int q = 0; q < kTC; ++q) a[r][q] = i == p ? pr[q] : a[r][q] - f * pr[q];
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < kTR; ++r) {
+                        const int i = rg * kTR + r;
+                        if (i < m) {
+                            const double f = colbuf[i];
+#pragma unroll
+                            for (int q = 0; q < kTC; ++q) a[r][q] = a[r][q] - f * pr[q];
+                        }
                     }
                 }
             }
@@ -396,9 +506,9 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
                 }
         }
         __syncthreads();
-        double (*src)[3 * kBtdMaxM + 1] = R0;
+        double (*src)[3 * MAXM + 1] = R0;
         int* rowof = reinterpret_cast<int*>(&R1[5][0]);
-        for (int c = tid; c < m; c += kThreads) rowof[c] = pivrow[c];
+        for (int c = tid; c < m; c += NT) rowof[c] = pivrow[c];
         __syncthreads();
         for (int i = ti; i < m; i += kRG) {
             const int ri = rowof[i];
@@ -419,11 +529,11 @@ __global__ __launch_bounds__(kThreads) void btd_factor_kernel(int nb, int m, dou
 // sides (six dependent cross-lane steps per row), one thread per (row group, column) otherwise (12
 // rows serially per thread; 4 of 256 threads busy for one column) -- were latency-bound: the
 // 41-stage solve took 3.1 ms, 2.2 ms with this mapping for one column.
-template <int SIGN>
-__device__ __forceinline__ void btd_matmul(double (*M)[kBtdMaxM + 1], double (*Yv)[kBtdMaxRhs + 1],
+template <int SIGN, int NT, int MAXM>
+__device__ __forceinline__ void btd_matmul(double (*M)[MAXM + 1], double (*Yv)[kBtdMaxRhs + 1],
                                            double (*Zv)[kBtdMaxRhs + 1], double (*Out)[kBtdMaxRhs + 1],
                                            int m, int w, int ti, int tj, bool init_zero) {
-    for (int p = ti * 64 + tj; p < m * w; p += kThreads) {
+    for (int p = ti * 64 + tj; p < m * w; p += NT) {
         const int i = p / w, j = p - i * w;
         double acc = 0.0;
 #pragma unroll 8
@@ -432,16 +542,18 @@ __device__ __forceinline__ void btd_matmul(double (*M)[kBtdMaxM + 1], double (*Y
     }
 }
 
-__global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int ldx, int j0, int w,
+template <int NT, int MAXM>
+__global__ __launch_bounds__(NT) void btd_apply_kernel(int nb, int m, int ldx, int j0, int w,
                                                             const double* __restrict__ Ts,
                                                             const double* __restrict__ Dinvs,
                                                             double* __restrict__ Xs) {
-    __shared__ double A[kBtdMaxM][kBtdMaxM + 1];
-    __shared__ double Ai[kBtdMaxM][kBtdMaxM + 1];
-    __shared__ double Dp[kBtdMaxM][kBtdMaxM + 1];
-    __shared__ double Y[kBtdMaxM][kBtdMaxRhs + 1];
-    __shared__ double Z[kBtdMaxM][kBtdMaxRhs + 1];
-    __shared__ double Q[kBtdMaxM][kBtdMaxRhs + 1];
+    __shared__ double A[MAXM][MAXM + 1];
+    __shared__ double Ai[MAXM][MAXM + 1];
+    __shared__ double Dp[MAXM][MAXM + 1];
+    __shared__ double Y[MAXM][kBtdMaxRhs + 1];
+    __shared__ double Z[MAXM][kBtdMaxRhs + 1];
+    __shared__ double Q[MAXM][kBtdMaxRhs + 1];
+    constexpr int kRG = NT / 64;
     const int tid = threadIdx.x, tj = tid & 63, ti = tid >> 6;
     const size_t mm = (size_t)m * m;
     const double* T = Ts + (size_t)blockIdx.x * nb * 3 * mm;
@@ -450,7 +562,7 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
     // a stage's global loads (right-hand sides and up to three blocks, 12 rows each per thread,
     // tj < 64 covers the m <= 48 and w <= 64 columns) are all issued before the first LDS store:
     // one memory latency per stage instead of one per row and block (the chain is latency-bound)
-    constexpr int R = kBtdMaxM / kRG;
+    constexpr int R = MAXM / kRG;
 
     for (int k = 0; k < nb; ++k) {                            // forward: Y_k
         double* Xk = X + (size_t)k * m * ldx;
@@ -476,14 +588,14 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
         }
         __syncthreads();
         if (k > 0) {                                          // Z -= L_k Y_{k-1}
-            btd_matmul<-1>(A, Y, Z, Z, m, w, ti, tj, false);
+            btd_matmul<-1, NT, MAXM>(A, Y, Z, Z, m, w, ti, tj, false);
             __syncthreads();
         }
-        btd_matmul<1>(Ai, Z, Z, Y, m, w, ti, tj, true);       // Y = D'^-1 Z
+        btd_matmul<1, NT, MAXM>(Ai, Z, Z, Y, m, w, ti, tj, true);       // Y = D'^-1 Z
         __syncthreads();
-        btd_matmul<-1>(Dp, Y, Z, Q, m, w, ti, tj, false);     // one refinement step: Q = Z - D' Y
+        btd_matmul<-1, NT, MAXM>(Dp, Y, Z, Q, m, w, ti, tj, false);     // one refinement step: Q = Z - D' Y
         __syncthreads();
-        btd_matmul<1>(Ai, Q, Y, Y, m, w, ti, tj, false);      // Y += D'^-1 Q
+        btd_matmul<1, NT, MAXM>(Ai, Q, Y, Y, m, w, ti, tj, false);      // Y += D'^-1 Q
         __syncthreads();
         for (int i = ti; i < m; i += kRG)
             for (int j = tj; j < w; j += 64) Xk[(size_t)i * ldx + j] = Y[i][j];
@@ -508,7 +620,7 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
             }
         }
         __syncthreads();
-        btd_matmul<-1>(A, Y, Z, Z, m, w, ti, tj, false);
+        btd_matmul<-1, NT, MAXM>(A, Y, Z, Z, m, w, ti, tj, false);
         __syncthreads();
         for (int i = ti; i < m; i += kRG) {
             for (int j = tj; j < w; j += 64) {
@@ -522,17 +634,26 @@ __global__ __launch_bounds__(kThreads) void btd_apply_kernel(int nb, int m, int 
 
 
 // Inertia (numbers of positive, negative and zero eigenvalues) of `batch` symmetric n x n matrices
-// by Bunch-Kaufman symmetric indefinite elimination (LAPACK dsytf2, lower triangle, alpha =
-// (1 + sqrt 17) / 8), Sylvester's law on the block-diagonal factor: a 1 x 1 pivot counts its sign,
-// a 2 x 2 pivot by the signs of its determinant and trace.  IPOPT's inertia correction needs
-// exactly these counts of the KKT matrix (MA27/MA57 report them); ipm.StructuredKKT adds them over
-// the interval blocks and the separator pivot blocks (Haynsworth additivity).
-// One workgroup per matrix, working in place on the lower triangle of A[b] (row-major, the upper
-// triangle is ignored; the matrix is destroyed).  Per elimination step: column max by wave
-// shuffles (+ the row max of the candidate when the diagonal is small), a symmetric interchange,
-// the pivot column(s) staged in LDS, then the trailing lower triangle updated one row per wave
-// (lanes over the row's columns: coalesced row-major accesses).  A pivot with max(|a_kk|, colmax) <=
-// ztol * max|A| counts as a zero eigenvalue and is skipped.
+// by Bunch-Kaufman symmetric indefinite elimination (LAPACK's pivoting, alpha = (1 + sqrt 17) / 8),
+// Sylvester's law on the block-diagonal factor: a 1 x 1 pivot counts its sign, a 2 x 2 pivot by
+// the signs of its determinant and trace.  IPOPT's inertia correction needs exactly these counts of
+// the KKT matrix (MA27/MA57 report them); ipm.StructuredKKT adds them over the interval blocks and
+// the separator pivot blocks (Haynsworth additivity).  A pivot with max(|a_kk|, colmax) <= ztol *
+// max|A| counts as a zero eigenvalue and is skipped.
+//
+// One workgroup per matrix, in place on A[b] (row-major; the lower triangle is read, the matrix is
+// destroyed).  Blocked with delayed updates (the scheme of LAPACK's dlasyf): a panel of up to nb
+// pivot columns is eliminated keeping the trailing matrix un-updated in global memory; every column
+// the pivot search needs (column k, and column imax when |a_kk| is small) is formed on the fly as
+//     S(r, g) = A(r, g) - sum_c W(r, c) L(g, c),     W = L D (the panel's columns, LDS),
+// interchanges are applied to the un-updated matrix and to the rows of W; after the panel one pass
+// applies the rank-nb update A -= W D^-1 W^T to the trailing lower triangle.  The unblocked
+// elimination (dsytf2) re-read and re-wrote the whole trailing triangle per pivot (n^3 / 3 doubles
+// of global traffic; 7.4 ms for the dual-kite sweep's 640-row blocks); here that traffic falls by
+// the panel width.  The lower triangle is first mirrored into the upper storage, so column c of the
+// lower triangle is row c of the array: the column gathers, the interchanges of rows below the
+// pivot and the trailing update (a wave per 4 columns, lanes over rows, W from LDS column-major)
+// all touch contiguous memory.  tools/bk_blocked_model.py is a host model of exactly this scheme.
 __device__ __forceinline__ void block_argmax(double& v, int& i, double* rv, int* ri, int tid) {
     for (int off = 32; off > 0; off >>= 1) {
         const double ov = __shfl_xor(v, off);
@@ -548,8 +669,13 @@ __device__ __forceinline__ void block_argmax(double& v, int& i, double* rv, int*
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kThreads) void sym_inertia_kernel(int n, double* __restrict__ As, double ztol,
-                                                               int* __restrict__ counts) {
+// Small matrices (the separator pivot blocks, the MPC's 126-row interval blocks): the unblocked
+// elimination (dsytf2) -- per pivot a column max, the interchange, and the trailing lower triangle
+// updated one row per wave with lanes over the row's columns (row-major, coalesced).  Below ~200
+// rows its per-pivot work is cheaper than the panel bookkeeping of the blocked kernel, and the
+// trailing triangle is L2-resident.
+__global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, double* __restrict__ As, double ztol,
+                                                                         int* __restrict__ counts) {
     extern __shared__ double pc[];                      // pivot columns: [2][n]
     __shared__ double rv[kThreads / 64];
     __shared__ int ri[kThreads / 64];
@@ -670,6 +796,205 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_kernel(int n, double* __
     }
 }
 
+constexpr int kSyNB = 16;                                 // panel width (W columns in LDS)
+constexpr size_t kSyLds = 150 * 1024;
+constexpr int kSyBlockedMinN = 200;                      // blocked from here (tools/awelu_ab.py)
+
+// Column g of the current Schur complement, rows [k, n), into W slot dst.  Storage: lower-triangle
+// entry (r, c), r >= c, at A[c n + r].
+__device__ __forceinline__ void bk_gather(const double* __restrict__ A, double* W, int n, int k, int g, int j,
+                                          int dst, const double* ca, const double* cb, const int* cp, int tid) {
+    double lg[kSyNB];                                     // L(g, c): wave-uniform
+#pragma unroll
+    for (int c = 0; c < kSyNB; ++c) lg[c] = c < j ? ca[c] * W[c * n + g] + cb[c] * W[cp[c] * n + g] : 0.0;
+    constexpr int U = 4;                                  // the rows' global loads issued together
+    for (int rb = k; rb < n; rb += U * kThreads) {        // uniform trip count
+        const int r0 = rb + tid;
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = r0 + u * kThreads;
+            v[u] = r < n ? (r >= g ? A[(size_t)g * n + r] : A[(size_t)r * n + g]) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = r0 + u * kThreads;
+            if (r < n) {
+#pragma unroll
+                for (int c = 0; c < kSyNB; ++c)
+                    if (c < j) v[u] -= W[c * n + r] * lg[c];
+                W[dst * n + r] = v[u];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void sym_inertia_kernel(int n, int nb, double* __restrict__ As, double ztol,
+                                                               int* __restrict__ counts) {
+    extern __shared__ double W[];                       // [nb][n], column-major panel W = L D
+    __shared__ double rv[kThreads / 64];
+    __shared__ int ri[kThreads / 64];
+    __shared__ double ca[kSyNB], cb[kSyNB];              // L(s, c) = ca[c] W(s, c) + cb[c] W(s, cp[c])
+    __shared__ int cp[kSyNB];
+    double* A = As + (size_t)blockIdx.x * n * n;
+    const int tid = threadIdx.x;
+    const int wv = tid >> 6, ln = tid & 63;
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    // the lower triangle mirrored into the upper storage; its scale for the zero-pivot test
+    double amax = 0.0;
+    int dummy = 0;
+    for (int t = tid; t < n * n; t += kThreads) {
+        const int i = t / n, j = t - i * n;
+        if (j <= i) {
+            const double v = A[t];
+            amax = fmax(amax, fabs(v));
+            if (j < i) A[(size_t)j * n + i] = v;
+        }
+    }
+    block_argmax(amax, dummy, rv, ri, tid);              // (its barriers also order the mirror)
+    const double zlim = ztol * amax;
+    int pos = 0, neg = 0, zero = 0;                     // uniform across the workgroup
+    int k = 0;
+    while (k < n) {
+        int j = 0;                                      // panel columns used
+        while (k < n && j < nb - 1) {                   // (a 2 x 2 pivot needs two free slots)
+            bk_gather(A, W, n, k, k, j, j, ca, cb, cp, tid);
+            __syncthreads();
+            const double absakk = fabs(W[j * n + k]);
+            double colmax = 0.0;
+            int imax = k;
+            for (int r = k + 1 + tid; r < n; r += kThreads) {
+                const double v = fabs(W[j * n + r]);
+                if (v > colmax) { colmax = v; imax = r; }
+            }
+            block_argmax(colmax, imax, rv, ri, tid);
+            imax = __builtin_amdgcn_readfirstlane(imax);
+            if (__builtin_amdgcn_readfirstlane(fmax(absakk, colmax) <= zlim)) {   // zero column: a zero eigenvalue
+                ++zero;
+                ++k;
+                continue;
+            }
+            int kp = k, kstep = 1;
+            if (__builtin_amdgcn_readfirstlane(absakk < alpha * colmax)) {
+                bk_gather(A, W, n, k, imax, j, j + 1, ca, cb, cp, tid);
+                __syncthreads();
+                double rowmax = 0.0;
+                int jm = 0;
+                for (int r = k + tid; r < n; r += kThreads)
+                    if (r != imax) {
+                        const double v = fabs(W[(j + 1) * n + r]);
+                        if (v > rowmax) { rowmax = v; jm = r; }
+                    }
+                block_argmax(rowmax, jm, rv, ri, tid);
+                if (absakk >= alpha * colmax * (colmax / rowmax)) {
+                    kp = k;
+                } else if (fabs(W[(j + 1) * n + imax]) >= alpha * rowmax) {
+                    kp = imax;
+                } else {
+                    kp = imax;
+                    kstep = 2;
+                }
+                kp = __builtin_amdgcn_readfirstlane(kp);     // uniform by construction; made
+                kstep = __builtin_amdgcn_readfirstlane(kstep);   // scalar for the compiler
+            }
+            const int kk = k + kstep - 1;
+            if (kp != kk) {
+                // symmetric interchange of kk and kp in the un-updated matrix ...
+                for (int i = kp + 1 + tid; i < n; i += kThreads) {
+                    const double a = A[(size_t)kk * n + i];
+                    A[(size_t)kk * n + i] = A[(size_t)kp * n + i];
+                    A[(size_t)kp * n + i] = a;
+                }
+                for (int jj = kk + 1 + tid; jj < kp; jj += kThreads) {
+                    const double a = A[(size_t)kk * n + jj];
+                    A[(size_t)kk * n + jj] = A[(size_t)jj * n + kp];
+                    A[(size_t)jj * n + kp] = a;
+                }
+                if (tid == 0) {
+                    const double a = A[(size_t)kk * n + kk];
+                    A[(size_t)kk * n + kk] = A[(size_t)kp * n + kp];
+                    A[(size_t)kp * n + kp] = a;
+                }
+                // ... in the rows of the panel's earlier columns ...
+                for (int c = tid; c < j; c += kThreads) {
+                    const double a = W[c * n + kk];
+                    W[c * n + kk] = W[c * n + kp];
+                    W[c * n + kp] = a;
+                }
+                // ... and in the pivot column(s) formed above
+                if (kstep == 1) {                       // column imax becomes column k
+                    for (int r = k + tid; r < n; r += kThreads)
+                        W[j * n + r] = W[(j + 1) * n + (r == k ? kp : r == kp ? k : r)];
+                } else if (tid < 2) {
+                    const int sl = j + tid;
+                    const double a = W[sl * n + kk];
+                    W[sl * n + kk] = W[sl * n + kp];
+                    W[sl * n + kp] = a;
+                }
+            }
+            __syncthreads();
+            const double d11 = W[j * n + k];
+            if (kstep == 1) {
+                if (d11 > 0.0) ++pos; else if (d11 < 0.0) ++neg; else ++zero;
+                if (tid == 0) { ca[j] = 1.0 / d11; cb[j] = 0.0; cp[j] = j; }
+            } else {
+                const double d21 = W[j * n + k + 1], d22 = W[(j + 1) * n + k + 1];
+                const double det = d11 * d22 - d21 * d21;
+                if (det < 0.0) { ++pos; ++neg; }
+                else if (det > 0.0) { if (d11 + d22 > 0.0) pos += 2; else neg += 2; }
+                else { ++zero; if (d11 + d22 > 0.0) ++pos; else if (d11 + d22 < 0.0) ++neg; else ++zero; }
+                if (tid == 0) {                         // D^-1 = [d22, -d21; -d21, d11] / det
+                    ca[j] = d22 / det; cb[j] = -d21 / det; cp[j] = j + 1;
+                    ca[j + 1] = d11 / det; cb[j + 1] = -d21 / det; cp[j + 1] = j;
+                }
+            }
+            __syncthreads();
+            j += kstep;
+            k += kstep;
+        }
+        if (k < n && j > 0) {
+            // trailing update A(r, s) -= sum_c L(s, c) W(r, c), k <= s <= r: a wave takes 4 columns,
+            // their L rows in registers, lanes over r (one LDS read of W(r, c) feeds 4 columns)
+            constexpr int kCB = 4;
+            for (int s0 = k + kCB * wv; s0 < n; s0 += kCB * (kThreads / 64)) {
+                double ls[kCB][kSyNB];
+#pragma unroll
+                for (int q = 0; q < kCB; ++q) {
+                    const int s = min(s0 + q, n - 1);
+#pragma unroll
+                    for (int c = 0; c < kSyNB; ++c)
+                        ls[q][c] = c < j ? ca[c] * W[c * n + s] + cb[c] * W[cp[c] * n + s] : 0.0;
+                }
+                for (int rb = s0; rb < n; rb += 64) {             // wave-uniform trip count
+                    const int r = rb + ln;
+                    const bool in = r < n;
+                    double acc[kCB];
+#pragma unroll
+                    for (int q = 0; q < kCB; ++q) acc[q] = (in && s0 + q <= r) ? A[(size_t)(s0 + q) * n + r] : 0.0;
+                    const int rr = in ? r : n - 1;
+#pragma unroll
+                    for (int c = 0; c < kSyNB; ++c) {
+                        if (c < j) {
+                            const double w = W[c * n + rr];
+#pragma unroll
+                            for (int q = 0; q < kCB; ++q) acc[q] -= ls[q][c] * w;
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < kCB; ++q)
+                        if (in && s0 + q <= r) A[(size_t)(s0 + q) * n + r] = acc[q];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        counts[3 * blockIdx.x + 0] = pos;
+        counts[3 * blockIdx.x + 1] = neg;
+        counts[3 * blockIdx.x + 2] = zero;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -732,7 +1057,7 @@ int awelu_btd_factor_batched(int nb, int m, int batch, double* T, double* Dinv, 
         g_err = "need nb >= 1, 1 <= m <= 48, batch >= 1 and device pointers";
         return 1;
     }
-    btd_factor_kernel<<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, T, Dinv);
+    btd_factor_kernel<kThreads, kBtdMaxM><<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, T, Dinv);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);
@@ -751,7 +1076,8 @@ int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, const double* T,
     }
     for (int j0 = 0; j0 < nrhs; j0 += kBtdMaxRhs) {
         const int w = std::min(kBtdMaxRhs, nrhs - j0);
-        btd_apply_kernel<<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, nrhs, j0, w, T, Dinv, X);
+        btd_apply_kernel<kThreads, kBtdMaxM><<<dim3((unsigned)batch), kThreads, 0, (hipStream_t)stream>>>(nb, m, nrhs, j0, w, T,
+                                                                                                     Dinv, X);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -764,14 +1090,22 @@ int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, const double* T,
 // Inertia of `batch` symmetric n x n matrices A[b][n][n] (lower triangle read, A destroyed):
 // counts[b][3] = (positive, negative, zero) eigenvalue counts.  Asynchronous on `stream`.
 int awelu_sym_inertia_batched(int n, int batch, double* A, double ztol, int* counts, void* stream) {
-    if (n < 1 || n > 4000 || batch < 1 || !A || !counts) {
-        g_err = "need 1 <= n <= 4000 (pivot columns in LDS), batch >= 1 and device pointers";
+    const int nb = std::min<long>(kSyNB, (long)(kSyLds / sizeof(double)) / std::max(n, 1));
+    if (n < 1 || nb < 4 || batch < 1 || !A || !counts) {
+        g_err = "need 1 <= n <= 4800 (a panel of >= 4 columns in LDS), batch >= 1 and device pointers";
         return 1;
     }
-    const size_t lds = sizeof(double) * 2 * (size_t)n;
-    if (lds > 64 * 1024)
-        hipFuncSetAttribute((const void*)sym_inertia_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    sym_inertia_kernel<<<dim3((unsigned)batch), kThreads, lds, (hipStream_t)stream>>>(n, A, ztol, counts);
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)sym_inertia_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSyLds);
+        attr = true;
+    }
+    if (n < kSyBlockedMinN)
+        sym_inertia_unblocked_kernel<<<dim3((unsigned)batch), kThreads, sizeof(double) * 2 * (size_t)n,
+                                       (hipStream_t)stream>>>(n, A, ztol, counts);
+    else
+        sym_inertia_kernel<<<dim3((unsigned)batch), kThreads, sizeof(double) * (size_t)nb * n, (hipStream_t)stream>>>(
+            n, nb, A, ztol, counts);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

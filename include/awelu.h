@@ -34,8 +34,9 @@ int awelu_btd_factor_batched(int nb, int m, int batch, double* T, double* Dinv, 
 int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, const double* T, const double* Dinv, double* X,
                             void* stream);
 
-/* Inertia of `batch` symmetric n x n matrices A[b][n][n] (lower triangle read; A is destroyed) by
- * Bunch-Kaufman elimination: counts[b][3] = (positive, negative, zero) eigenvalue counts, a pivot
+/* Inertia of `batch` symmetric n x n matrices A[b][n][n], n <= 4800 (lower triangle read; A is
+ * destroyed) by blocked Bunch-Kaufman elimination (delayed updates, panels of up to 16 pivot
+ * columns): counts[b][3] = (positive, negative, zero) eigenvalue counts, a pivot
  * column below ztol * max|A| counting as zero.  IPOPT's inertia correction (IpPDFullSpaceSolver,
  * MA27/MA57 inertia) for the structured KKT of awebox_amd/ipm.py. */
 int awelu_sym_inertia_batched(int n, int batch, double* A, double ztol, int* counts, void* stream);

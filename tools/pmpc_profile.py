@@ -52,7 +52,13 @@ def main():
                      "phase_ms_per_step": {k: v / args.steps * 1e3 for k, v in timing.items()}}
         if prof:
             s = io.StringIO()
-            pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(25)
+            pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(40)
+            pstats.Stats(prof, stream=s).sort_stats("cumulative").print_stats(60)
+            st = pstats.Stats(prof, stream=s)
+            st.print_callees("solve_batch")
+            st.print_callers("method 'cpu'")
+            st.print_callers("method 'item'")
+            st.print_callers("torch.tensor")
             out[mode]["top"] = s.getvalue()
         print(json.dumps({k: v for k, v in out[mode].items() if k != "top"}), flush=True)
     with open(args.out, "w") as fh:
