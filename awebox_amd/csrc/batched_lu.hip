@@ -193,11 +193,13 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
 //   backward (U):      panel U[0:k1+16, k1:k1+16], bottom block first, same two phases.
 // The library path (rocBLAS trsv for one right-hand side) re-reads the factors per column step
 // from HBM: 20 ms for 256 systems of n = 463 against ~0.1 ms here.
-__global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int j0, int w,
+__global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int wchunk,
                                                            const double* __restrict__ LUs,
                                                            const int* __restrict__ pivs,
                                                            double* __restrict__ Xs) {
     extern __shared__ double sm[];
+    const int j0 = blockIdx.y * wchunk;                  // this workgroup's right-hand sides
+    const int w = min(wchunk, ldx - j0);
     double* panel = sm;                                  // [n][kNB]
     double* X = sm + (size_t)n * kNB;                    // [n][w]
     const double* A = LUs + (size_t)blockIdx.x * n * n;
@@ -267,6 +269,8 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
 }
 
 constexpr size_t kSolveLds = 144 * 1024;
+constexpr long kSolveTargetWgs = 256;                   // one per CU
+constexpr long kSolveMinChunk = 16;
 
 // Block-tridiagonal systems, one workgroup per system: nb diagonal blocks of m x m (m <= 48),
 // T[b][k][3][m][m] = (sub-diagonal block L_k = (k, k-1), diagonal block D_k, super-diagonal block
@@ -388,13 +392,12 @@ __global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* _
                 double acc[kRows];
 #pragma unroll
                 for (int r = 0; r < kRows; ++r) acc[r] = 0.0;
+                // rows i >= m (padding, < MAXM) are accumulated too and never written: a guard per
+                // row compiled to a branch with its own LDS wait per product
                 for (int c = 0; c < m; ++c) {
                     const double wc = Wp[c][j];
 #pragma unroll
-                    for (int r = 0; r < kRows; ++r) {
-                        const int i = ti + r * kRG;
-                        if (i < m) acc[r] += R1[i][c] * wc;
-                    }
+                    for (int r = 0; r < kRows; ++r) acc[r] += R1[ti + r * kRG][c] * wc;
                 }
 #pragma unroll
                 for (int r = 0; r < kRows; ++r) {
@@ -470,26 +473,24 @@ __global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* _
                 double pr[kTC];
 #pragma unroll
                 for (int q = 0; q < kTC; ++q) pr[q] = rowbuf[cg * kTC + q] * rp;
+                // padding rows i >= m (< MAXM) are updated with stale column entries and never
+                // published or written back (a guard per row compiled to a branch and an LDS wait
+                // per row)
+                double f[kTR];
+#pragma unroll
+                for (int r = 0; r < kTR; ++r) f[r] = colbuf[rg * kTR + r];
                 if (rg == p / kTR) {                          // the pivot row's own group
 #pragma unroll
                     for (int r = 0; r < kTR; ++r) {
                         const int i = rg * kTR + r;
-                        if (i < m) {
-                            const double f = colbuf[i];
 #pragma unroll
-                            for (int q = 0; q < kTC; ++q) a[r][q] = i == p ? pr[q] : a[r][q] - f * pr[q];
-                        }
+                        for (int q = 0; q < kTC; ++q) a[r][q] = i == p ? pr[q] : a[r][q] - f[r] * pr[q];
                     }
                 } else {
 #pragma unroll
-                    for (int r = 0; r < kTR; ++r) {
-                        const int i = rg * kTR + r;
-                        if (i < m) {
-                            const double f = colbuf[i];
+                    for (int r = 0; r < kTR; ++r)
 #pragma unroll
-                            for (int q = 0; q < kTC; ++q) a[r][q] = a[r][q] - f * pr[q];
-                        }
-                    }
+                        for (int q = 0; q < kTC; ++q) a[r][q] = a[r][q] - f[r] * pr[q];
                 }
             }
             if (tid == 0) pivrow[c] = p;
@@ -1035,11 +1036,17 @@ int awelu_solve_batched(int n, int nrhs, int batch, const double* LU, const int*
         hipFuncSetAttribute((const void*)lu_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSolveLds);
         attr = true;
     }
-    for (int j0 = 0; j0 < nrhs; j0 += (int)cap) {
-        const int w = (int)std::min<long>(cap, nrhs - j0);
-        const size_t lds = sizeof(double) * (size_t)n * (kNB + w);
-        lu_solve_kernel<<<dim3((unsigned)batch), kThreads, lds, (hipStream_t)stream>>>(n, nrhs, j0, w, LU, piv, X);
-    }
+    // one workgroup per (matrix, chunk of right-hand sides), all in one launch: enough
+    // workgroups to fill the CUs for small batches (>= 16 columns per chunk: every chunk streams
+    // the whole factor), at most `cap` columns (LDS)
+    const long want = std::max<long>(1, (kSolveTargetWgs + batch - 1) / batch);
+    long w = std::max<long>(kSolveMinChunk, (nrhs + want - 1) / want);
+    w = std::min<long>(w, cap);
+    const long nchunks = (nrhs + w - 1) / w;
+    w = (nrhs + nchunks - 1) / nchunks;                   // balanced chunk widths
+    const size_t lds = sizeof(double) * (size_t)n * (kNB + w);
+    lu_solve_kernel<<<dim3((unsigned)batch, (unsigned)nchunks), kThreads, lds, (hipStream_t)stream>>>(n, nrhs, (int)w, LU,
+                                                                                                     piv, X);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);
