@@ -337,6 +337,12 @@ __device__ __forceinline__ void gj_publish_row(const double (&a)[TR][TC], double
     for (int q = 0; q < TC; ++q) rowbuf[cg * TC + q] = a[R][q];
 }
 
+template <int R, int TR, int TC>
+__device__ __forceinline__ void gj_set_row(double (&a)[TR][TC], const double (&pr)[TC]) {
+#pragma unroll
+    for (int q = 0; q < TC; ++q) a[R][q] = pr[q];
+}
+
 template <int NT, int MAXM>
 __global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* __restrict__ Ts,
                                                        double* __restrict__ Dinvs) {
@@ -467,30 +473,37 @@ __global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* _
                     default: gj_publish_row<7>(a, rowbuf, cg); break;
                 }
             }
-            __syncthreads();
+            // off the critical path (before the barrier): the reciprocal pivot and this thread's
+            // column entries -- colbuf stays valid until column c + 2
             const double rp = 1.0 / colbuf[p];
+            double f[kTR];
+            if (owner) {
+#pragma unroll
+                for (int r = 0; r < kTR; ++r) f[r] = colbuf[rg * kTR + r];
+            }
+            __syncthreads();
             if (owner) {
                 double pr[kTC];
 #pragma unroll
                 for (int q = 0; q < kTC; ++q) pr[q] = rowbuf[cg * kTC + q] * rp;
-                // padding rows i >= m (< MAXM) are updated with stale column entries and never
-                // published or written back (a guard per row compiled to a branch and an LDS wait
-                // per row)
-                double f[kTR];
+                // every row eliminated (padding rows i >= m, < MAXM, with stale column entries: never
+                // published or written back), then the pivot row set to the scaled pivot row: no
+                // divergent select per entry
 #pragma unroll
-                for (int r = 0; r < kTR; ++r) f[r] = colbuf[rg * kTR + r];
-                if (rg == p / kTR) {                          // the pivot row's own group
+                for (int r = 0; r < kTR; ++r)
 #pragma unroll
-                    for (int r = 0; r < kTR; ++r) {
-                        const int i = rg * kTR + r;
-#pragma unroll
-                        for (int q = 0; q < kTC; ++q) a[r][q] = i == p ? pr[q] : a[r][q] - f[r] * pr[q];
+                    for (int q = 0; q < kTC; ++q) a[r][q] = a[r][q] - f[r] * pr[q];
+                if (rg == p / kTR) {
+                    switch (p % kTR) {
+                        case 0: gj_set_row<0>(a, pr); break;
+                        case 1: gj_set_row<1>(a, pr); break;
+                        case 2: gj_set_row<2>(a, pr); break;
+                        case 3: gj_set_row<3>(a, pr); break;
+                        case 4: gj_set_row<4>(a, pr); break;
+                        case 5: gj_set_row<5>(a, pr); break;
+                        case 6: gj_set_row<6>(a, pr); break;
+                        default: gj_set_row<7>(a, pr); break;
                     }
-                } else {
-#pragma unroll
-                    for (int r = 0; r < kTR; ++r)
-#pragma unroll
-                        for (int q = 0; q < kTC; ++q) a[r][q] = a[r][q] - f[r] * pr[q];
                 }
             }
             if (tid == 0) pivrow[c] = p;
