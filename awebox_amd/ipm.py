@@ -596,6 +596,41 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
                        None if zu0 is None else np.atleast_2d(zu0), opts=opts, device=device)[0]
 
 
+_STRUCT_CACHE: dict = {}
+
+
+def _structure(ev, nlp, dev, opts):
+    """(StructuredKKT, J^T product, H product) for one NLP structure, shared by the solves of the
+    same evaluator and the same fixed-variable / inequality sets (every sampling time of the MPC
+    solves its pre-solve and main solve on one structure): their construction is host work of
+    ~3 ms per solve_batch call.  Only structural data enters them; the per-solve state (the
+    factorisation, the counters, the separator switches) is reset or overwritten by every solve."""
+    import hashlib
+    import weakref
+    h = hashlib.sha1()
+    for a in (nlp.free, nlp.ineq, nlp.j_row.cpu().numpy(), nlp.j_col.cpu().numpy(), nlp.h_r.cpu().numpy(),
+              nlp.h_c.cpu().numpy()):
+        h.update(np.ascontiguousarray(a, dtype=np.int64).tobytes())
+        h.update(b"|")
+    key = (id(ev), h.hexdigest(), str(torch.device(dev)), opts.lu_backend, opts.separators)
+    ent = _STRUCT_CACHE.get(key)
+    if ent is not None and ent[0]() is ev:
+        skkt = ent[1]
+        skkt.n_solve = skkt.n_dense = 0
+        skkt.force_btd = skkt.btd_off = False
+        return ent[1], ent[2], ent[3]
+    skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators)
+    ny, m = nlp.ny, nlp.m
+    jt_op = _GatherMv(nlp.j_col.cpu().numpy(), nlp.j_row.cpu().numpy(), (ny, m), dev)
+    hr_np, hc_np = nlp.h_r.cpu().numpy(), nlp.h_c.cpu().numpy()
+    off_np = hr_np != hc_np
+    h_op = _GatherMv(np.concatenate([hr_np, hc_np[off_np]]), np.concatenate([hc_np, hr_np[off_np]]), (ny, ny), dev)
+    if len(_STRUCT_CACHE) >= 8:
+        _STRUCT_CACHE.clear()
+    _STRUCT_CACHE[key] = (weakref.ref(ev), skkt, jt_op, h_op)
+    return skkt, jt_op, h_op
+
+
 def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: IpmOptions | None = None,
                 device="cuda") -> list[IpmResult]:
     """Solve B instances of one NLP structure (P [B, n_p], x0 [B, n_v], shared bounds) side by side
@@ -686,7 +721,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     iters = np.zeros(B, dtype=np.int64)
     kkt_err = np.full(B, math.inf)
     active = np.ones(B, dtype=bool)
-    skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators)
+    skkt, jt_op, h_op = _structure(ev, nlp, dev, opts)
     skkt.force_btd = opts.separators == "btd"                   # the block sweep on host tensors too
     # exact inertia needs the separator pivot blocks of the block sweep on the device (a dense
     # Bunch-Kaufman pass over the whole Schur complement is ~1 s); otherwise the curvature test
@@ -742,12 +777,6 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
 
     def grad_y(gradv):
         return torch.cat([gradv, torch.zeros(B, mI, **f64)], 1)
-
-    Op = _GatherMv
-    jt_op = Op(nlp.j_col.cpu().numpy(), nlp.j_row.cpu().numpy(), (ny, m), dev)
-    hr_np, hc_np = nlp.h_r.cpu().numpy(), nlp.h_c.cpu().numpy()
-    off_np = hr_np != hc_np
-    h_op = Op(np.concatenate([hr_np, hc_np[off_np]]), np.concatenate([hc_np, hr_np[off_np]]), (ny, ny), dev)
 
     def A_T_lam(jvv, lamv):
         r = jt_op.mv(jvv, lamv)
@@ -808,7 +837,10 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     hv_zero = torch.zeros(B, len(nlp.h_keep), **f64)
 
     def dev_b(a):
-        return torch.tensor(np.asarray(a, dtype=np.float64), **f64)
+        """A host [B] array on the device: staged through pinned memory and copied asynchronously
+        (a pageable copy waits for the device; ~80 of them per MPC sampling time)."""
+        t = torch.from_numpy(np.array(a, dtype=np.float64))
+        return t.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else t
 
     # ---- the newton direction with inertia correction (all instances in `want`) ------------------
     def newton_direction(want, dw_floor, hv, sigma, rhs, mu_t):
