@@ -7,6 +7,10 @@
 
 Plain ``hipcc -shared -fPIC`` (no JIT cache): the .so files live next to this file so that they
 travel with the repository snapshot to the GPU box.
+
+Before libawegpu.so is compiled, ``generate()`` refreshes ``csrc/ap2_nodejac.gen.hpp``: the node
+model is traced and differentiated by ``csrc/gen/ap2_jacgen.cpp`` (g++, host) for the default AP2
+constants, and the straight-line node-Jacobian code it writes is what ap2_node_kernel runs.
 """
 from __future__ import annotations
 
@@ -21,10 +25,13 @@ LIB = os.path.join(HERE, "libawegpu.so")
 LIB_MPC = os.path.join(HERE, "libawempc.so")
 LIB_DUAL = os.path.join(HERE, "libawedual.so")
 LIB_LU = os.path.join(HERE, "libawelu.so")
+GEN_HEADER = os.path.join(CSRC, "ap2_nodejac.gen.hpp")
+GEN_SOURCES = [os.path.join(CSRC, "gen", f) for f in ("ap2_jacgen.cpp", "sym.hpp")] + [
+    os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")]
 _COMMON = [os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
     os.path.join(INCLUDE, "awegpu.h")]
 TARGETS = {
-    LIB: ([os.path.join(CSRC, "awegpu.hip")], _COMMON),
+    LIB: ([os.path.join(CSRC, "awegpu.hip")], _COMMON + [GEN_HEADER]),
     LIB_MPC: ([os.path.join(CSRC, "awempc.hip")],
               _COMMON + [os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp")]
               + [os.path.join(INCLUDE, "awempc.h")]),
@@ -58,8 +65,42 @@ def build_one(lib: str, force: bool = False, verbose: bool = False) -> str:
     return lib
 
 
+def generate(force: bool = False, verbose: bool = False) -> str:
+    """Regenerate csrc/ap2_nodejac.gen.hpp when the model or the generator changed; the file is
+    rewritten only if its content differs (so an unchanged model does not trigger a rebuild)."""
+    if not force and not _stale(GEN_HEADER, GEN_SOURCES):
+        return GEN_HEADER
+    import tempfile
+
+    import numpy as np
+
+    from . import problem as pb
+    consts = pb.build_constants(pb.Ap2Config())
+    with tempfile.TemporaryDirectory() as tmp:
+        exe = os.path.join(tmp, "ap2_jacgen")
+        cmd = [os.environ.get("CXX", "g++"), "-O1", "-std=c++17", os.path.join(CSRC, "gen", "ap2_jacgen.cpp"),
+               "-o", exe]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        cfile = os.path.join(tmp, "consts.txt")
+        np.savetxt(cfile, consts.consts)
+        out = os.path.join(tmp, "gen.hpp")
+        r = subprocess.run([exe, cfile, out], check=True, capture_output=True, text=True)
+        if verbose:
+            print(r.stdout.strip(), file=sys.stderr)
+        new = open(out).read()
+    old = open(GEN_HEADER).read() if os.path.exists(GEN_HEADER) else None
+    if new != old:
+        with open(GEN_HEADER + ".tmp", "w") as fh:
+            fh.write(new)
+        os.replace(GEN_HEADER + ".tmp", GEN_HEADER)
+    return GEN_HEADER
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Build every library; returns the AP2 library path (the headline evaluator)."""
+    generate(force=force, verbose=verbose)
     for lib in TARGETS:
         build_one(lib, force=force, verbose=verbose)
     return LIB

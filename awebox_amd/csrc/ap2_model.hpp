@@ -49,19 +49,19 @@ AWE_HD T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] 
 
 // ISA density (atmosphere.py:60-78): rho_ref ((T_ref - gamma_air zz) / T_ref)^(g/(gamma_air R) - 1),
 // evaluated as exp(expo log(.)) -- two short transcendental kernels instead of a full pow
-template <class T>
-AWE_HD T isa_density(const T& zz, const double* th) {
-    const double expo = th[AWE_TH_G] / th[AWE_TH_GAMMA_AIR] / th[AWE_TH_R] - 1.0;
+template <class T, class PT>
+AWE_HD T isa_density(const T& zz, const PT* th) {
+    const auto expo = th[AWE_TH_G] / th[AWE_TH_GAMMA_AIR] / th[AWE_TH_R] - 1.0;
     T ratio = 1.0 - zz * (th[AWE_TH_GAMMA_AIR] / th[AWE_TH_T_REF]);
     return th[AWE_TH_RHO_REF] * exp(expo * log(ratio));
 }
 
 // power-law wind speed u_ref (smooth_abs(zz, eps=1) / z_ref)^c_f (wind.py:184-208), with
 // smooth_abs(zz) = sqrt(zz^2 + 1) folded into the logarithm
-template <class T>
-AWE_HD T wind_speed(const T& zz, const double* th) {
-    const double p = th[AWE_TH_EXP_REF];
-    const double scale = th[AWE_TH_U_REF] * ::exp(-p * ::log(th[AWE_TH_Z_REF]));
+template <class T, class PT>
+AWE_HD T wind_speed(const T& zz, const PT* th) {
+    const auto p = th[AWE_TH_EXP_REF];
+    const auto scale = th[AWE_TH_U_REF] * exp(-p * log(th[AWE_TH_Z_REF]));
     return scale * exp((0.5 * p) * log(zz * zz + 1.0));
 }
 
@@ -77,12 +77,12 @@ AWE_HD T tether_element_height(int e, int n_el, const T& qz) {
 // wind speed and air density at the element's midpoint: the drag of element e on the main
 // tether, lumped onto the kite node with the reference's shape factor.  The tether's lower end
 // is the ground (q = dq = 0); its share of the drag is dropped.
-template <class T>
+template <class T, class PT>
 AWE_HD void tether_element_drag(int e, int n_el, const T* q, const T* v, const T& diam, const T& uw,
-                                const T& rho, const double* th, T out[3]) {
+                                const T& rho, const PT* th, T out[3]) {
     const double ds = 1.0 / n_el;
     const double s0 = 0.5 * ds, step = ((1.0 - 0.5 * ds) - s0) / (n_el - 1);
-    const double cd = th[AWE_TH_CD_TETHER];
+    const auto cd = th[AWE_TH_CD_TETHER];
     const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
     T ue[3];
     ue[0] = uw - (v[0] * up + v[0] * lo) / 2.0;
@@ -98,8 +98,8 @@ AWE_HD void tether_element_drag(int e, int n_el, const T* q, const T* v, const T
     for (int i = 0; i < 3; ++i) out[i] = sg * (fac * ue[i]);
 }
 
-template <class T>
-AWE_HD void tether_element(int e, int n_el, const T* q, const T* v, const T& diam, const double* th,
+template <class T, class PT>
+AWE_HD void tether_element(int e, int n_el, const T* q, const T* v, const T& diam, const PT* th,
                            T out[3]) {
     T zz = tether_element_height(e, n_el, q[2]);
     tether_element_drag(e, n_el, q, v, diam, wind_speed(zz, th), isa_density(zz, th), th, out);
@@ -110,15 +110,15 @@ AWE_HD void tether_element(int e, int n_el, const T* q, const T* v, const T& dia
 // substitutes a provider that returns values and partial derivatives preaccumulated once per
 // node, lane-parallel, so that the per-direction model pass does not repeat them.
 struct InlineSubmodels {
-    template <class T>
-    AWE_HD void kite_atmosphere(const T& qz, const double* th, T& uw, T& rho) const {
+    template <class T, class PT>
+    AWE_HD void kite_atmosphere(const T& qz, const PT* th, T& uw, T& rho) const {
         uw = wind_speed(qz, th);
         rho = isa_density(qz, th);
     }
-    template <class T>
-    AWE_HD void tether_drag(const T* q, const T* v, const T& diam, const double* th, const double* cst,
+    template <class T, class PT, class CT>
+    AWE_HD void tether_drag(const T* q, const T* v, const T& diam, const PT* th, const CT* cst,
                             T D[3]) const {
-        const int n_el = (int)cst[AWE_C_N_ELEMENTS];
+        const int n_el = structural(cst[AWE_C_N_ELEMENTS]);
         for (int i = 0; i < 3; ++i) D[i] = T(0.0);
         for (int e = 0; e < n_el; ++e) {
             T c[3];
@@ -131,10 +131,10 @@ struct InlineSubmodels {
 // Rows are emitted phase by phase (DCM, trivial, aero -> rotation -> path constraints, tether
 // drag -> translation -> holonomic) and every phase re-reads its inputs through `in`, so that
 // short live ranges keep the dual-number working set inside the register file of one lane.
-template <class T, class In, class Sink, class Sub = InlineSubmodels>
-AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const double* cst,
+template <class T, class In, class Sink, class Sub = InlineSubmodels, class PT = double, class CT = double>
+AWE_HD void ap2_node(const In& in, const T& gamma, const PT* th, const CT* cst,
                      Sink& out, bool want_ineq, const Sub& sub = Sub()) {
-    const double* s = cst + AWE_C_SCALING;
+    const CT* s = cst + AWE_C_SCALING;
     // SI value of node variable i (dynamics.py:924-934)
     auto SI = [&](int i) -> T { return in(i) * s[i]; };
 
@@ -143,7 +143,7 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
         T R[9], om[3];
         for (int i = 0; i < 9; ++i) R[i] = SI(9 + i);            // column-major R[3*col + row]
         for (int i = 0; i < 3; ++i) om[i] = SI(6 + i);
-        const double kr2 = th[AWE_TH_KAPPA_R] / 2.0;
+        const auto kr2 = th[AWE_TH_KAPPA_R] / 2.0;
         for (int c = 0; c < 3; ++c) {
             T A[3];   // column c of kappa_r/2 (I - R^T R) + skew(omega)
             for (int r = 0; r < 3; ++r) {
@@ -162,11 +162,11 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
 
     // ---- trivial kinematics, sorted names: ddelta10, ddl_t, dl_t, dq10 (lagr_dyn.py:141-169)
     for (int i = 0; i < 3; ++i)
-        out.eq_row(16 + i, (SI(41 + i) - SI(52 + i)) / ::sqrt(s[52 + i] * s[41 + i]));
-    out.eq_row(19, (SI(45) - SI(55)) / ::sqrt(s[55] * s[45]));
-    out.eq_row(20, (SI(44) - SI(22)) / ::sqrt(s[22] * s[44]));
+        out.eq_row(16 + i, (SI(41 + i) - SI(52 + i)) / sqrt(s[52 + i] * s[41 + i]));
+    out.eq_row(19, (SI(45) - SI(55)) / sqrt(s[55] * s[45]));
+    out.eq_row(20, (SI(44) - SI(22)) / sqrt(s[22] * s[44]));
     for (int i = 0; i < 3; ++i)
-        out.eq_row(21 + i, (SI(23 + i) - SI(3 + i)) / ::sqrt(s[3 + i] * s[23 + i]));
+        out.eq_row(21 + i, (SI(23 + i) - SI(3 + i)) / sqrt(s[3 + i] * s[23 + i]));
 
     // ---- kite aerodynamics (kite_aero.py:63-117, six_dof_kite.py:165-201) -------------
     T F_earth[3];
@@ -188,14 +188,14 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
         T alpha = ua_e3 / x_comp;                             // indicators.get_alpha
         T beta = ua_e2 / x_comp;                              // indicators.get_beta
 
-        const double b_ref = th[AWE_TH_B_REF], c_ref = th[AWE_TH_C_REF], s_ref = th[AWE_TH_S_REF];
+        const auto b_ref = th[AWE_TH_B_REF], c_ref = th[AWE_TH_C_REF], s_ref = th[AWE_TH_S_REF];
         T coeff[6];
         {
             // p, q, r in the control frame (stability_derivatives.py:202-226)
             T inv2a = 1.0 / (2.0 * airspeed);
-            const double* sd = th + AWE_TH_STAB_DERIVS;
-            const double* sdl = cst + AWE_C_SD_LEN;
-            const double mf = th[AWE_TH_MOMENT_FACTOR];
+            const PT* sd = th + AWE_TH_STAB_DERIVS;
+            const CT* sdl = cst + AWE_C_SD_LEN;
+            const auto mf = th[AWE_TH_MOMENT_FACTOR];
             T alpha2 = alpha * alpha;
             for (int c = 0; c < 6; ++c) coeff[c] = T(0.0);
             for (int i = 0; i < 9; ++i) {
@@ -211,15 +211,14 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
                 }
                 T ia = inp * alpha, ia2 = inp * alpha2;
                 for (int c = 0; c < 6; ++c) {
-                    const int n = (int)sdl[c * 9 + i];
+                    const int n = structural(sdl[c * 9 + i]);
                     if (n == 0) continue;
-                    const double* dv = sd + (c * 9 + i) * 3;
+                    const PT* dv = sd + (c * 9 + i) * 3;
                     // sum_l deriv[l] * input * alpha^l (stability_derivatives.py:166-200)
                     T contrib = dv[0] * inp;
                     if (n > 1) contrib = contrib + dv[1] * ia;
                     if (n > 2) contrib = contrib + dv[2] * ia2;
-                    const double wgt = (c >= 3 && i >= 6) ? mf : 1.0;
-                    coeff[c] = coeff[c] + wgt * contrib;
+                    coeff[c] = coeff[c] + ((c >= 3 && i >= 6) ? mf * contrib : contrib);
                 }
             }
         }
@@ -235,7 +234,7 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
             M_body[0] = -(qs * (b_ref * coeff[3]));                // frames.from_control_to_body
             M_body[1] = qs * (c_ref * coeff[4]);
             M_body[2] = -(qs * (b_ref * coeff[5]));
-            const double* J = th + AWE_TH_J;   // column-major
+            const PT* J = th + AWE_TH_J;   // column-major
             T om[3], Jw[3];
             for (int i = 0; i < 3; ++i) om[i] = SI(6 + i);
             for (int i = 0; i < 3; ++i) Jw[i] = J[i] * om[0] + J[3 + i] * om[1] + J[6 + i] * om[2];
@@ -243,7 +242,7 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
             wxJw[0] = om[1] * Jw[2] - om[2] * Jw[1];
             wxJw[1] = -(om[0] * Jw[2] - om[2] * Jw[0]);
             wxJw[2] = om[0] * Jw[1] - om[1] * Jw[0];
-            const double inv_ms = 1.0 / cst[AWE_C_M_AERO_SCALING];
+            const auto inv_ms = 1.0 / cst[AWE_C_M_AERO_SCALING];
             for (int i = 0; i < 3; ++i) {
                 T Jdw = J[i] * SI(29) + J[3 + i] * SI(30) + J[6 + i] * SI(31);
                 T M = gamma * SI(49 + i) + M_body[i];
@@ -256,20 +255,20 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
             for (int i = 0; i < 3; ++i) q[i] = SI(i);
             T nq = sqrt(dot3(q, q));
             T tension = SI(56) * nq;
-            const double fscale = cst[AWE_C_LAMBDA_SCALING] * cst[AWE_C_SCALING_LENGTH];
+            const auto fscale = cst[AWE_C_LAMBDA_SCALING] * cst[AWE_C_SCALING_LENGTH];
             out.ineq_row(0, (tension - th[AWE_TH_FORCE_LIMITS + 1]) / fscale);
             out.ineq_row(1, (th[AWE_TH_FORCE_LIMITS + 0] - tension) / fscale);
-            const double u_ref = th[AWE_TH_U_REF];
+            const auto u_ref = th[AWE_TH_U_REF];
             out.ineq_row(2, (airspeed - th[AWE_TH_AIRSPEED_LIMITS + 1]) / u_ref);
             out.ineq_row(3, (th[AWE_TH_AIRSPEED_LIMITS + 0] - airspeed) / u_ref);
-            const double tight = cst[AWE_C_AERO_TIGHTNESS], aref = cst[AWE_C_AIRSPEED_REF];
-            const double amax = cst[AWE_C_ALPHA_MAX], amin = cst[AWE_C_ALPHA_MIN];
-            const double bmax = cst[AWE_C_BETA_MAX], bmin = cst[AWE_C_BETA_MIN];
-            out.ineq_row(4, (ua_e3 - ua_e1 * amax) * tight / aref / ::sqrt(amax * amax + 1e-16));
-            out.ineq_row(5, (-ua_e3 + ua_e1 * amin) * tight / aref / ::sqrt(amin * amin + 1e-16));
-            out.ineq_row(6, (ua_e2 - ua_e1 * bmax) * tight / aref / ::sqrt(bmax * bmax + 1e-16));
-            out.ineq_row(7, (-ua_e2 + ua_e1 * bmin) * tight / aref / ::sqrt(bmin * bmin + 1e-16));
-            const double cos_gmax = ::cos(th[AWE_TH_ROT_ANGLES + 2]);
+            const auto tight = cst[AWE_C_AERO_TIGHTNESS], aref = cst[AWE_C_AIRSPEED_REF];
+            const auto amax = cst[AWE_C_ALPHA_MAX], amin = cst[AWE_C_ALPHA_MIN];
+            const auto bmax = cst[AWE_C_BETA_MAX], bmin = cst[AWE_C_BETA_MIN];
+            out.ineq_row(4, (ua_e3 - ua_e1 * amax) * tight / aref / sqrt(amax * amax + 1e-16));
+            out.ineq_row(5, (-ua_e3 + ua_e1 * amin) * tight / aref / sqrt(amin * amin + 1e-16));
+            out.ineq_row(6, (ua_e2 - ua_e1 * bmax) * tight / aref / sqrt(bmax * bmax + 1e-16));
+            out.ineq_row(7, (-ua_e2 + ua_e1 * bmin) * tight / aref / sqrt(bmin * bmin + 1e-16));
+            const auto cos_gmax = cos(th[AWE_TH_ROT_ANGLES + 2]);
             T yaw = (q[0] * SI(15) + q[1] * SI(16) + q[2] * SI(17) - cos_gmax * nq) / cst[AWE_C_SCALING_LENGTH];
             out.ineq_row(8, -1.0 * yaw);
         }
@@ -278,9 +277,9 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
     out.power(SI(56) * SI(21) * SI(22) / cst[AWE_C_ENERGY_SCALING]);   // dynamics.py:318-330
 
     // ---- translational Lagrangian dynamics (lagr_dyn.py:68-109, 174-204) --------------
-    const double g_grav = th[AWE_TH_G];
-    const double m_k = th[AWE_TH_M_K];
-    const double rho_t = th[AWE_TH_RHO_TETHER];
+    const auto g_grav = th[AWE_TH_G];
+    const auto m_k = th[AWE_TH_M_K];
+    const auto rho_t = th[AWE_TH_RHO_TETHER];
     T q[3], v[3];
     for (int i = 0; i < 3; ++i) q[i] = SI(i);
     for (int i = 0; i < 3; ++i) v[i] = SI(3 + i);
@@ -310,10 +309,10 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
         T pq = g_grav * mu * (q[2] * inv_n) * 0.5;
         T pz = g_grav * mu * nq * 0.5 + g_grav * m_k;
         T mass_flow = mu * sv * inv_n;                        // d(m_t)/dt (lagr_dyn.py:174-204)
-        const double scaling_mass = 3.14159265358979323846 * (cst[AWE_C_SCALING_DIAM] / 2.0) *
+        const auto scaling_mass = 3.14159265358979323846 * (cst[AWE_C_SCALING_DIAM] / 2.0) *
                                     (cst[AWE_C_SCALING_DIAM] / 2.0) * rho_t * cst[AWE_C_SCALING_LENGTH];
-        const double node_mass = scaling_mass / 2.0 + m_k;    // mass.py:62-93
-        const double inv_force_scaling = 1.0 / (node_mass * cst[AWE_C_G_SCALING] * 10.0);
+        const auto node_mass = scaling_mass / 2.0 + m_k;    // mass.py:62-93
+        const auto inv_force_scaling = 1.0 / (node_mass * cst[AWE_C_G_SCALING] * 10.0);
         for (int i = 0; i < 3; ++i) {
             T ddt = cv * v[i] + cq * q[i] + ca * a[i];
             T dLdq = kq * q[i] + kv * v[i] - pq * q[i] - lam * q[i];
@@ -328,9 +327,9 @@ AWE_HD void ap2_node(const In& in, const T& gamma, const double* th, const doubl
         T c0 = 0.5 * (qq - l_t * l_t);
         T c1 = sv - l_t * dl_t;
         T c2 = vv + qa - dl_t * dl_t - l_t * ldd;
-        const double kap = th[AWE_TH_KAPPA];
+        const auto kap = th[AWE_TH_KAPPA];
         T hl = c2 + 2.0 * kap * c1 + kap * kap * c0;
-        const double hscale = kap * kap * (cst[AWE_C_SCALING_LENGTH] * cst[AWE_C_Q_SCALING_MEAN]);
+        const auto hscale = kap * kap * (cst[AWE_C_SCALING_LENGTH] * cst[AWE_C_Q_SCALING_MEAN]);
         out.eq_row(3, hl / hscale);
     }
 }

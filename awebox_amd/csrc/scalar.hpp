@@ -199,6 +199,10 @@ AWE_HD Dep2 sqrt(Dep2 a) { return a; }
 AWE_HD Dep2 exp(Dep2 a) { return a; }
 AWE_HD Dep2 log(Dep2 a) { return a; }
 
+// integer structure read from a model constant (element counts, table lengths); the tracing
+// scalar of the code generator (gen/sym.hpp) overloads it with the value recorded at trace time
+AWE_HD int structural(double a) { return (int)a; }
+
 AWE_HD double value(double a) { return a; }
 AWE_HD double sqrt(double a) { return ::sqrt(a); }
 AWE_HD double exp(double a) { return ::exp(a); }

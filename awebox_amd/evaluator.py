@@ -70,6 +70,9 @@ def load_library(path: str = _LIB_PATH):
     lib.awe_eval_hess.argtypes = [h] + [ctypes.c_void_p] * 6
     lib.awe_eval_hess_host.argtypes = [h, dp, dp, dp, dp, dp]
     lib.awe_last_hess_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float)]
+    lib.awe_set_eval_path.argtypes = [h, ctypes.c_int]
+    lib.awe_get_eval_path.argtypes = [h, ip]
+    lib.awe_last_kernel_ms_gen.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     _LIB = lib
     return lib
 
@@ -244,6 +247,26 @@ class Ap2Evaluator:
     def last_kernel_ms(self):
         a, b = ctypes.c_float(), ctypes.c_float()
         self._check(self._lib.awe_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    # evaluation path of eval_nlp (include/awegpu.h): "generated" (one thread per collocation
+    # node, build-time generated sparse-Jacobian code) or "colour" (compressed forward mode)
+    PATHS = {"colour": 0, "generated": 1}
+
+    @property
+    def path(self):
+        p = ctypes.c_int()
+        self._check(self._lib.awe_get_eval_path(self._h, ctypes.byref(p)))
+        return {v: k for k, v in self.PATHS.items()}[p.value]
+
+    @path.setter
+    def path(self, name):
+        self._check(self._lib.awe_set_eval_path(self._h, self.PATHS[name]))
+
+    def last_kernel_ms_gen(self):
+        """(node kernel ms, assembly kernel ms) of the last eval_nlp on the generated path."""
+        a, b = ctypes.c_float(), ctypes.c_float()
+        self._check(self._lib.awe_last_kernel_ms_gen(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
     # ---------------------------------------------- host path (numpy) ----------------

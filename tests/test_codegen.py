@@ -1,0 +1,60 @@
+"""The generated node-Jacobian code (awebox_amd/csrc/ap2_nodejac.gen.hpp, written by
+csrc/gen/ap2_jacgen.cpp from the templated node model) against the same model evaluated in
+dual-number arithmetic, one forward pass per seed direction with the seeding of awegpu.hip's colour
+kernel (csrc/gen/check_ap2_gen.cpp), on the host.  The GPU parity of the generated path against the
+oracle is in tests/test_gpu_parity.py (it is the default path of awe_eval_nlp)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from awebox_amd import build as B
+from awebox_amd import problem as pb
+from awebox_amd.initial_guess import initial_guess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "awebox_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    tmp = tmp_path_factory.mktemp("gen")
+    exe = str(tmp / "check")
+    subprocess.run(["g++", "-O1", "-std=c++17", os.path.join(CSRC, "gen", "check_ap2_gen.cpp"), "-o", exe],
+                   check=True)
+    return tmp, exe
+
+
+def test_committed_header_is_current():
+    """The header in the tree is what the generator writes for the current model."""
+    before = open(B.GEN_HEADER).read()
+    B.generate(force=True)
+    assert open(B.GEN_HEADER).read() == before, "ap2_nodejac.gen.hpp is stale: run python -m awebox_amd.build"
+
+
+@pytest.mark.parametrize("k,seed", [(0, 0), (7, 1), (23, 2), (39, 3)])
+def test_generated_jacobian_matches_dual_model(checker, k, seed):
+    tmp, exe = checker
+    consts = pb.build_constants(pb.Ap2Config(n_k=40, d=4))
+    lay = pb.NlpLayout(40, 4)
+    v0 = initial_guess(consts, lay)
+    P = pb.pack_p(lay, consts, v0)
+    th = P[lay.n_v + pb.NW + pb.NCOST:]
+    rng = np.random.default_rng(seed)
+    w = np.concatenate([v0[lay.x(k)], v0[lay.xdot(k)], v0[lay.u(k)], v0[lay.z(k)], v0[lay.theta()],
+                        v0[lay.phi()][:1]])
+    w = w * (1 + 0.05 * rng.standard_normal(w.shape)) + 0.01 * rng.standard_normal(w.shape)
+    for name, arr in (("consts", consts.consts), ("th", th), ("w", w)):
+        np.savetxt(str(tmp / f"{name}.txt"), arr)
+    cxx, inv_tf = 2.0 + rng.random(), 1.0 / (20.0 + 30.0 * rng.random())
+    out = subprocess.run([exe, str(tmp / "consts.txt"), str(tmp / "th.txt"), str(tmp / "w.txt"), repr(cxx),
+                          repr(inv_tf)], check=True, capture_output=True, text=True)
+    rec = json.loads(out.stdout)
+    for kind in ("shooting", "radau"):
+        r = rec[kind]
+        assert r["entries"] == r["n_tan"], "every tangent slot is a pattern entry"
+        assert r["value_rel"] < 1e-14, (kind, r)
+        assert r["tangent_rel"] < 1e-12, (kind, r)
+        assert r["tangent_max"] > 1.0
