@@ -52,6 +52,8 @@ struct KindOut {
     int n_tan = 0;
 };
 
+std::vector<int> ko_dbp_dirs;   // directions of the Radau node's dbp entries, in order
+
 KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs& ct, int n_strips) {
     awe::Tape tape;
     awe::active_tape() = &tape;
@@ -63,6 +65,15 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs&
     RowSink sink;
     SymIn in{w.data()};
     awe::ap2_node<Sym>(in, w[awt::kDirGamma], th.data(), cs.data(), sink, kind == 0);
+    // Radau node: the objective terms in the side slip and the power integrand (objective.py:390-421,
+    // the (1 - psi) power cost), cb beta^2 + cpp p with cb = c_beta w_j / norm_beta (ex2) and
+    // cpp = (1 - psi)(-c_P) w_j / N (ex3); its directional derivatives go to dbp[dir]
+    int objbp = -1;
+    if (kind == 1) {
+        const Sym cb = Sym::of(tape.leaf(Op::Extra, 2)), cpp = Sym::of(tape.leaf(Op::Extra, 3));
+        const Sym bt = Sym::of(sink.rows[awt::kRowBeta]), pw = Sym::of(sink.rows[awt::kRowPower]);
+        objbp = (cb * (bt * bt) + cpp * pw).id;
+    }
     const int n0 = (int)tape.n.size();
 
     const int one = tape.cnst(1.0);
@@ -83,8 +94,6 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs&
         for (int r = 0; r < awt::kRowPower; ++r) rows.push_back(r);
     } else {
         for (int r = 0; r < AWE_N_EQ; ++r) rows.push_back(r);
-        rows.push_back(awt::kRowPower);
-        rows.push_back(awt::kRowBeta);
     }
     if (const char* rr = std::getenv("AWE_GEN_ROWS")) {   // experiment: a row range only
         int lo = 0, hi = 0;
@@ -113,6 +122,16 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs&
             stores.push_back({node, 1, r, dir});
         }
     }
+    if (kind == 1) {   // objective: beta and power values (obv) and the tangents of cb beta^2 + cpp p (dbp)
+        stores.push_back({sink.rows[awt::kRowBeta], 3, 0, -1});
+        stores.push_back({sink.rows[awt::kRowPower], 3, 1, -1});
+        // compact: dbp[i] is the derivative along direction kDbpDir[i]
+        for (auto& e : G[objbp]) {
+            if (e.first > awt::kDirGamma) continue;
+            stores.push_back({e.second, 2, -1, (int)ko_dbp_dirs.size()});
+            ko_dbp_dirs.push_back(e.first);
+        }
+    }
     KindOut ko;
     const char* fe = std::getenv("AWE_GEN_FENCE_EVERY");
     const int fence = fe ? std::atoi(fe) : 0;
@@ -135,7 +154,7 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs&
     for (int sidx = 0; sidx < n_strips; ++sidx) {
         std::vector<awe::Store> part;
         for (auto& s : stores)
-            if ((s.kind == 0 && sidx == 0) || (s.kind == 1 && strip_of[s.dir] == sidx)) part.push_back(s);
+            if ((s.kind != 1 && sidx == 0) || (s.kind == 1 && strip_of[s.dir] == sidx)) part.push_back(s);
         if (part.empty()) continue;
         awe::EmitStats st;
         const int before = slot_base;
@@ -192,7 +211,9 @@ int main(int argc, char** argv) {
          "#if defined(__HIP_DEVICE_COMPILE__)\n"
          "__device__ __forceinline__ double awe_gen_opaque(double x) { asm volatile(\"\" : \"+v\"(x)); return x; }\n"
          "#define AWE_GEN_OPAQUE(x) awe_gen_opaque(x)\n"
-         "#else\n#define AWE_GEN_OPAQUE(x) (x)\n#endif\n\nnamespace awe_gen {\n\n";
+         "__device__ __forceinline__ double awe_gen_keep(double x) { asm(\"\" : \"+v\"(x)); return x; }\n"
+         "#define AWE_GEN_KEEP(x) awe_gen_keep(x)\n"
+         "#else\n#define AWE_GEN_OPAQUE(x) (x)\n#define AWE_GEN_KEEP(x) (x)\n#endif\n\nnamespace awe_gen {\n\n";
     o << "// integer structure of the model constants the code was generated for (awe_create checks it)\n";
     o << "constexpr int kNElements = " << (int)cst[AWE_C_N_ELEMENTS] << ";\n";
     o << "constexpr int kSdLen[54] = {";
@@ -203,6 +224,11 @@ int main(int argc, char** argv) {
     o << "// algorithmic operations per node kind: adds/muls/reciprocals, transcendental calls\n";
     o << "constexpr int kFlops[2] = {" << ks.st.flops << ", " << kr.st.flops << "};\n";
     o << "constexpr int kTranscendental[2] = {" << ks.st.transcendental << ", " << kr.st.transcendental << "};\n";
+    o << "// dbp[i] of the Radau node is the derivative along seed direction kDbpDir[i]\n";
+    o << "constexpr int kNDbp = " << ko_dbp_dirs.size() << ";\n";
+    o << "constexpr int kDbpDir[" << std::max<size_t>(1, ko_dbp_dirs.size()) << "] = {";
+    for (size_t i = 0; i < ko_dbp_dirs.size(); ++i) o << (i ? ", " : "") << ko_dbp_dirs[i];
+    o << "};\n";
     o << "// tangent-buffer slot of (row, direction), -1 where the pattern has no entry\n";
     o << "constexpr short kTanIdx[2][35][64] = {\n";
     for (const KindOut* k : {&ks, &kr}) {
@@ -219,11 +245,12 @@ int main(int argc, char** argv) {
     o << "template <class In>\nAWE_HD void ap2_node_shoot(const In& in, const double* __restrict__ th, "
          "const double* __restrict__ cst, double* __restrict__ val, double* __restrict__ tan) {\n";
     o << ks.body << "}\n\n";
-    o << "// Radau node: val[0..23] equalities, val[33] power integrand, val[34] side slip, tan[kNTan[1]];\n";
+    o << "// Radau node: val[0..23] equalities, tan[kNTan[1]]; obv[0] side slip, obv[1] power integrand;\n";
+    o << "// dbp[i] = directional derivative of ex2 beta^2 + ex3 power along seed direction kDbpDir[i];\n";
     o << "// ex0 = C[j][j] / (h t_f), ex1 = 1 / t_f\n";
     o << "template <class In>\nAWE_HD void ap2_node_radau(const In& in, const double ex0, const double ex1, "
-         "const double* __restrict__ th, const double* __restrict__ cst, double* __restrict__ val, "
-         "double* __restrict__ tan) {\n";
+         "const double ex2, const double ex3, const double* __restrict__ th, const double* __restrict__ cst, "
+         "double* __restrict__ val, double* __restrict__ tan, double* __restrict__ dbp, double* __restrict__ obv) {\n";
     o << kr.body << "}\n\n}  // namespace awe_gen\n";
 
     std::ofstream out(argv[2]);

@@ -52,10 +52,12 @@ int main(int argc, char** argv) {
     if ((int)cst.size() != AWE_NCONST || (int)th.size() != AWE_NTHETA0 || (int)w.size() != AWE_NW + 1) return 3;
     std::printf("{");
     for (int kind = 0; kind < 2; ++kind) {
-        std::vector<double> val(36, 0.0), tan(awe_gen::kNTan[kind], 0.0);
+        std::vector<double> val(36, 0.0), tan(awe_gen::kNTan[kind], 0.0), dbp(64, 0.0), obv(2, 0.0);
+        const double cb = 0.37, cpp = -1.9;   // objective weights of the beta^2 and power terms
         PlainIn pin{w.data()};
         if (kind == 0) awe_gen::ap2_node_shoot(pin, th.data(), cst.data(), val.data(), tan.data());
-        else awe_gen::ap2_node_radau(pin, cxx, inv_tf, th.data(), cst.data(), val.data(), tan.data());
+        else awe_gen::ap2_node_radau(pin, cxx, inv_tf, cb, cpp, th.data(), cst.data(), val.data(), tan.data(),
+                                     dbp.data(), obv.data());
         double dv = 0.0, dt = 0.0, tmax = 0.0;
         int covered = 0;
         for (int dir = 0; dir <= awt::kDirGamma; ++dir) {
@@ -63,11 +65,20 @@ int main(int argc, char** argv) {
             awe::NodeResult<awe::Dual> res;
             awe::Dual gamma(w[awt::kDirGamma], dir == awt::kDirGamma ? 1.0 : 0.0);
             awe::ap2_node<awe::Dual>(in, gamma, th.data(), cst.data(), res, kind == 0);
-            for (int r = 0; r < 35; ++r) {
-                if (kind == 0 && r >= awt::kRowPower) continue;
-                if (kind == 1 && r >= AWE_N_EQ && r < awt::kRowPower) continue;
-                const awe::Dual ref = r < AWE_N_EQ ? res.eq[r] : r < awt::kRowPower ? res.ineq[r - AWE_N_EQ]
-                                                    : r == awt::kRowPower ? res.pw : res.bt;
+            if (kind == 1) {   // objective terms cb beta^2 + cpp p
+                if (dir == 0) {
+                    dv = std::fmax(dv, std::fabs(obv[0] - res.bt.v) / std::fmax(1.0, std::fabs(res.bt.v)));
+                    dv = std::fmax(dv, std::fabs(obv[1] - res.pw.v) / std::fmax(1.0, std::fabs(res.pw.v)));
+                }
+                const double ref = 2.0 * cb * res.bt.v * res.bt.d + cpp * res.pw.d;
+                double got = 0.0;   // dbp is compact: entry i is direction kDbpDir[i]
+                for (int i = 0; i < awe_gen::kNDbp; ++i)
+                    if (awe_gen::kDbpDir[i] == dir) got = dbp[i];
+                dt = std::fmax(dt, std::fabs(got - ref) / std::fmax(1.0, std::fabs(ref)));
+            }
+            for (int r = 0; r < AWE_N_EQ + AWE_N_INEQ; ++r) {
+                if (kind == 1 && r >= AWE_N_EQ) continue;
+                const awe::Dual ref = r < AWE_N_EQ ? res.eq[r] : res.ineq[r - AWE_N_EQ];
                 if (dir == 0) dv = std::fmax(dv, std::fabs(val[r] - ref.v) / std::fmax(1.0, std::fabs(ref.v)));
                 const int idx = awe_gen::kTanIdx[kind][r][dir];
                 const double got = idx >= 0 ? tan[idx] : 0.0;

@@ -15,6 +15,7 @@
 #pragma once
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -55,12 +56,21 @@ class Tape {
     }
     bool is_c(int id, double x) const { double v; return is_const(id, &v) && v == x && !std::signbit(v - x); }
 
+    // Negations are pushed outward (all rewrites are exact in IEEE arithmetic): a + (-b) = a - b,
+    // a - (-b) = a + b, (-a) b = -(a b), 1 / (-a) = -(1 / a).  They end up absorbed by additions or at
+    // the stores, so that the emitted code has (almost) no separate negation for the compiler to
+    // fold back into a multiply at the consumer's position, which would stretch the multiply's
+    // operands' live ranges.
+    bool is_neg(int id) const { return n[id].op == Op::Neg; }
     int add(int a, int b) {
         double va, vb;
         const bool ca = is_const(a, &va), cb = is_const(b, &vb);
         if (ca && cb) return cnst(va + vb);
         if (ca && va == 0.0) return b;
         if (cb && vb == 0.0) return a;
+        if (is_neg(a) && is_neg(b)) return neg(add(n[a].a, n[b].a));
+        if (is_neg(b)) return sub(a, n[b].a);
+        if (is_neg(a)) return sub(b, n[a].a);
         if (a > b) std::swap(a, b);
         return make(Op::Add, a, b);
     }
@@ -70,12 +80,19 @@ class Tape {
         if (ca && cb) return cnst(va - vb);
         if (cb && vb == 0.0) return a;
         if (ca && va == 0.0) return neg(b);
+        if (is_neg(b)) return add(a, n[b].a);
+        if (is_neg(a)) return neg(add(n[a].a, b));
         return make(Op::Sub, a, b);
     }
     int mul(int a, int b) {
         double va, vb;
         const bool ca = is_const(a, &va), cb = is_const(b, &vb);
         if (ca && cb) return cnst(va * vb);
+        if (is_neg(a) && is_neg(b)) return mul(n[a].a, n[b].a);
+        if (is_neg(a)) return neg(mul(n[a].a, b));
+        if (is_neg(b)) return neg(mul(a, n[b].a));
+        if (ca && va < 0.0 && va != -1.0) return neg(mul(cnst(-va), b));
+        if (cb && vb < 0.0 && vb != -1.0) return neg(mul(a, cnst(-vb)));
         if (ca) {
             if (va == 0.0) return cnst(0.0);
             if (va == 1.0) return b;
@@ -98,6 +115,7 @@ class Tape {
     int rcp(int a) {
         double va;
         if (is_const(a, &va)) return cnst(1.0 / va);
+        if (is_neg(a)) return neg(rcp(n[a].a));
         return make(Op::Rcp, a, -1);
     }
     int div(int a, int b) {
@@ -291,7 +309,7 @@ inline std::vector<SparseGrad> forward_grads(Tape& t, int n0, const std::functio
 // ---- emission --------------------------------------------------------------------------------
 struct Store {
     int node;        // tape node stored
-    int kind;        // 0 value row, 1 tangent
+    int kind;        // 0 value row val[row], 1 tangent tan[slot], 2 dbp[dir], 3 obv[row]
     int row, dir;
     int slot = -1;   // tangent-buffer index (kind 1), assigned by emit
 };
@@ -317,34 +335,32 @@ inline int res(const Tape& t, int v) { return (v >= 0 && t.n[v].op == Op::Neg) ?
 // (operands whose last consumer it is, net of the value it defines, which counts as free when
 // only stores use it) goes first, ties broken by the baseline position.  Loads therefore wait
 // until their consumer can run, and a chain is finished before the next one is opened.
+using Operands = std::array<int, 3>;   // resolved operands of an emitted node (-1: none)
+
 inline std::vector<int> pressure_schedule(const Tape& t, const std::vector<int>& order,
-                                          const std::vector<Store>& stores) {
+                                          const std::vector<Operands>& ops) {
     const int N = (int)t.n.size();
     std::vector<int> base(N, -1);
     for (size_t i = 0; i < order.size(); ++i) base[order[i]] = (int)i;
     auto in_sched = [&](int v) { return v >= 0 && base[v] >= 0; };
+    // distinct scheduled operands of v (a node may use one operand twice: x * x)
+    auto dops = [&](int v) {
+        std::vector<int> r;
+        for (int o : ops[v])
+            if (in_sched(o) && std::find(r.begin(), r.end(), o) == r.end()) r.push_back(o);
+        return r;
+    };
     std::vector<std::vector<int>> users(N);
     std::vector<int> remaining(N, 0), pending(N, 0);
-    auto A = [&](int v) { return res(t, t.n[v].a); };
-    auto B = [&](int v) { return res(t, t.n[v].b); };
     for (int v : order)
-        for (int o : {A(v), B(v)})
-            if (in_sched(o)) {
-                // a node may use the same operand twice (x * x): count distinct consumers once
-                if (std::find(users[o].begin(), users[o].end(), v) == users[o].end()) users[o].push_back(v);
-            }
+        for (int o : dops(v)) users[o].push_back(v);
     for (int v : order) {
         remaining[v] = (int)users[v].size();
-        int np = 0;
-        if (in_sched(A(v))) ++np;
-        if (in_sched(B(v)) && B(v) != A(v)) ++np;
-        pending[v] = np;
+        pending[v] = (int)dops(v).size();
     }
     auto score = [&](int v) {
         int freed = 0;
-        const int a = A(v), b = B(v);
-        if (in_sched(a) && remaining[a] == 1) ++freed;
-        if (in_sched(b) && b != a && remaining[b] == 1) ++freed;
+        for (int o : dops(v)) if (remaining[o] == 1) ++freed;
         const int def = users[v].empty() ? 0 : 1;    // stored-only values die at once
         return freed - def;
     };
@@ -384,8 +400,7 @@ inline std::vector<int> pressure_schedule(const Tape& t, const std::vector<int>&
                     }
             }
         };
-        consume(A(v));
-        if (B(v) != A(v)) consume(B(v));
+        for (int o : dops(v)) consume(o);
         for (int u : users[v])
             if (--pending[u] == 0) push(u);
     }
@@ -398,8 +413,9 @@ inline std::vector<int> pressure_schedule(const Tape& t, const std::vector<int>&
 // through memory sequentially.  Names: in(i) inputs, th[i] / cst[i] parameters, ex<i> extras,
 // val[r] / tan[s] outputs.
 inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool schedule = true,
-                        int barrier_every = 0, bool opaque = false, int slot_base_in = 0) {
+                        int barrier_every = 0, bool opaque = false, int slot_base_in = 0, bool fuse = true) {
     int slot_base = slot_base_in;
+    const bool keep_all = std::getenv("AWE_GEN_KEEP_ALL") != nullptr;
     const int N = (int)t.n.size();
     std::vector<char> live(N, 0);
     std::vector<int> stack;
@@ -432,7 +448,46 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
     for (int v = 0; v < N; ++v)
         if (live[v] && t.n[v].op != Op::Const && t.n[v].op != Op::Neg) order.push_back(v);
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
-    if (schedule) order = pressure_schedule(t, order, stores);
+    // operands as emitted: negations resolved; a multiply used only by one addition or
+    // subtraction is fused into it (an explicit fma: one rounding, and the multiply's operands are
+    // consumed where the sum is formed, which the schedule then accounts for)
+    std::vector<Operands> ops(N, Operands{-1, -1, -1});
+    struct Fused { int m = -1, other = -1; bool neg_prod = false, neg_other = false; };
+    std::vector<Fused> fz(N);
+    {
+        std::vector<int> uses(N, 0);
+        for (int v : order) {
+            std::vector<int> seen;
+            for (int o : {res(t, t.n[v].a), res(t, t.n[v].b)})
+                if (o >= 0 && std::find(seen.begin(), seen.end(), o) == seen.end()) { seen.push_back(o); uses[o]++; }
+        }
+        for (auto& x : stores) uses[res(t, x.node)]++;
+        std::vector<char> absorbed(N, 0);
+        for (int v : order) {
+            const SNode& s = t.n[v];
+            ops[v] = Operands{res(t, s.a), res(t, s.b), -1};
+            if (!fuse || (s.op != Op::Add && s.op != Op::Sub)) continue;
+            // v = a + b or a - b; try the operand slots in turn
+            for (int slot = 0; slot < 2; ++slot) {
+                const int raw = slot == 0 ? s.a : s.b, oraw = slot == 0 ? s.b : s.a;
+                const int m = res(t, raw);
+                if (t.n[m].op != Op::Mul || uses[m] != 1 || absorbed[m] || m == res(t, oraw)) continue;
+                Fused f;
+                f.m = m;
+                f.other = oraw;
+                f.neg_prod = (raw != m) != (s.op == Op::Sub && slot == 1);
+                f.neg_other = s.op == Op::Sub && slot == 0;
+                fz[v] = f;
+                absorbed[m] = 1;
+                ops[v] = Operands{res(t, t.n[m].a), res(t, t.n[m].b), res(t, oraw)};
+                break;
+            }
+        }
+        std::vector<int> kept;
+        for (int v : order) if (!absorbed[v]) kept.push_back(v);
+        order.swap(kept);
+    }
+    if (schedule) order = pressure_schedule(t, order, ops);
     std::vector<int> pos(N, -1);
     for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int)i;
     // stores of constant nodes (zero tangents) go first, the others after their node
@@ -446,7 +501,7 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
     {   // register pressure of this order: values live from definition to last use
         std::vector<int> last(N, -1);
         for (size_t i = 0; i < order.size(); ++i)
-            for (int o : {res(t, t.n[order[i]].a), res(t, t.n[order[i]].b)})
+            for (int o : ops[order[i]])
                 if (o >= 0 && pos[o] >= 0) last[o] = std::max(last[o], (int)i);
         for (size_t i = 0; i < order.size(); ++i)
             for (int sidx : after[i]) {
@@ -496,6 +551,10 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
         Store& x = stores[s];
         if (x.kind == 0) {
             std::snprintf(buf, sizeof(buf), "    val[%d] = %s;\n", x.row, ref(x.node).c_str());
+        } else if (x.kind == 2) {
+            std::snprintf(buf, sizeof(buf), "    dbp[%d] = %s;\n", x.dir, ref(x.node).c_str());
+        } else if (x.kind == 3) {
+            std::snprintf(buf, sizeof(buf), "    obv[%d] = %s;\n", x.row, ref(x.node).c_str());
         } else {
             x.slot = next_slot++;
             std::snprintf(buf, sizeof(buf), "    tan[%d] = %s;\n", x.slot, ref(x.node).c_str());
@@ -514,9 +573,20 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
             case Op::Th: e = opq("th[" + std::to_string(s.idx) + "]"); st.loads++; break;
             case Op::Cs: e = opq("cst[" + std::to_string(s.idx) + "]"); st.loads++; break;
             case Op::Extra: e = opq("ex" + std::to_string(s.idx)); break;
-            case Op::Add: e = ref(s.a) + " + " + ref(s.b); st.flops++; break;
-            case Op::Sub: e = ref(s.a) + " - " + ref(s.b); st.flops++; break;
-            case Op::Mul: e = ref(s.a) + " * " + ref(s.b); st.flops++; break;
+            case Op::Add:
+            case Op::Sub:
+                if (fz[v].m >= 0) {
+                    const SNode& m = t.n[fz[v].m];
+                    auto sg = [](bool neg, const std::string& x) { return neg ? "(-" + x + ")" : x; };
+                    e = "__builtin_fma(" + sg(fz[v].neg_prod, ref(m.a)) + ", " + ref(m.b) + ", " +
+                        sg(fz[v].neg_other, ref(fz[v].other)) + ")";
+                    st.flops += 2;
+                    break;
+                }
+                e = ref(s.a) + (s.op == Op::Add ? " + " : " - ") + ref(s.b);
+                st.flops++;
+                break;
+            case Op::Mul: e = ref(s.a) + " * " + ref(s.b); if (std::getenv("AWE_GEN_KEEP_MUL")) e = "AWE_GEN_KEEP(" + e + ")"; st.flops++; break;
             case Op::Neg: break;   // folded into its consumers (ref)
             case Op::Rcp: e = "awe::rcp(" + ref(s.a) + ")"; st.flops++; break;
             case Op::Sqrt: e = "::sqrt(" + ref(s.a) + ")"; st.transcendental++; break;
@@ -527,6 +597,7 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
             case Op::Const: break;
         }
         st.ops++;
+        if (keep_all && (s.op == Op::Add || s.op == Op::Sub || s.op == Op::Rcp)) e = "AWE_GEN_KEEP(" + e + ")";
         out += "    const double v" + std::to_string(v) + " = " + e + ";\n";
         if (barrier_every > 0 && st.ops % barrier_every == 0) out += "    AWE_GEN_FENCE();\n";
         for (int sidx : after[i]) put_store(sidx);

@@ -28,7 +28,8 @@ EXPORTED_SYMBOLS = ["awe_create", "awe_destroy", "awe_last_error", "awe_sizes", 
                     "awe_eval_nlp", "awe_eval_g", "awe_eval_f", "awe_eval_nlp_host", "awe_eval_f_host",
                     "awe_eval_g_host",
                     "awe_last_kernel_ms", "awe_device_count", "awe_hess_nnz", "awe_sparsity_hess",
-                    "awe_sparsity_hess_static", "awe_eval_hess", "awe_eval_hess_host", "awe_last_hess_ms"]
+                    "awe_sparsity_hess_static", "awe_eval_hess", "awe_eval_hess_host", "awe_last_hess_ms",
+                    "awe_set_eval_path", "awe_get_eval_path", "awe_last_kernel_ms_gen"]
 
 
 class AwegpuUnavailable(RuntimeError):

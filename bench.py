@@ -9,11 +9,13 @@ For N > 1 (torch.distributed.run, one process per GPU) every rank evaluates its 
 over ranks is reported.  `value` = evaluations/s of the whole job.
 
 Also reported:
-  roofline     -- the dominant kernel (ap2_interval_kernel): algorithmic HBM bytes per launch
-                  (SURVEY 8(d) formula with the exact nnz, x B) / its mean duration from HIP events
-                  on the launch stream, against 8 TB/s.  `traffic` is the HBM byte rate from the
-                  rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE passes recorded in
-                  profiles/pmc_traffic.json, used only when that record was taken for the same
+  roofline     -- one evaluation = ap2_node_kernel (generated straight-line node Jacobians, one
+                  thread per collocation node) + ap2_gather_kernel (J_g values, gradient): the
+                  algorithmic HBM bytes per launch (SURVEY 8(d) formula with the exact nnz, x B) /
+                  the two kernels' duration from HIP events on the launch stream, against 8 TB/s;
+                  per-kernel times and rates in roofline.kernels.  `traffic` is the HBM byte rate
+                  from the rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE passes recorded
+                  in profiles/pmc_traffic.json, used only when that record was taken for the same
                   kernel sources and batch size (else null).
   fp64         -- algorithmic FP64 rate (the op-counting count of profiles/r03/flops_ap2.json /
                   kernel time) and the issued FP64 lane rate of the PMC record, both against the
@@ -60,7 +62,7 @@ def kernel_source_hash() -> str:
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "awebox_amd", "csrc")
-    for name in ("ap2_model.hpp", "ap2_tables.hpp", "awegpu.hip", "scalar.hpp"):   # the AP2 kernel's sources
+    for name in ("ap2_model.hpp", "ap2_tables.hpp", "awegpu.hip", "scalar.hpp", "ap2_nodejac.gen.hpp"):
         with open(os.path.join(csrc, name), "rb") as fh:
             h.update(name.encode() + fh.read())
     with open(os.path.join(ROOT, "include", "awegpu.h"), "rb") as fh:
@@ -70,7 +72,7 @@ def kernel_source_hash() -> str:
 
 SOURCES = {   # the files each evaluator kernel is built from (a PMC record is tied to their hash)
     "ap2": ["awebox_amd/csrc/ap2_model.hpp", "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/awegpu.hip",
-            "awebox_amd/csrc/scalar.hpp", "include/awegpu.h"],
+            "awebox_amd/csrc/scalar.hpp", "awebox_amd/csrc/ap2_nodejac.gen.hpp", "include/awegpu.h"],
     "dual": ["awebox_amd/csrc/dual_model.hpp", "awebox_amd/csrc/dual_tables.hpp", "awebox_amd/csrc/awedual.hip",
              "awebox_amd/csrc/ap2_model.hpp", "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/scalar.hpp",
              "include/awedual.h", "include/awegpu.h"],
@@ -117,6 +119,33 @@ def config_traffic(which: str, batch: int, kernel_ms: float):
         out["measured_limiter"] = ("fp64 VALU issue + latency (SQ_WAIT_ANY {:.0%} of wave cycles)".format(
             out["fp64_issued"]["wait_frac"]) if tf / FP64_PEAK_TFLOPS > hbm_frac else "hbm")
     return out
+
+
+def gen_kernels(ev, lay, B, node_ms, gather_ms):
+    """Per-kernel view of the generated path: the node kernel's operation rate (the generated
+    program's adds / multiplies / reciprocals per node, ap2_nodejac.gen.hpp kFlops, x nodes) against
+    the FP64 vector peak, and the gather kernel's algorithmic byte rate (its nodebuf run in, J_g and
+    the gradient out) against HBM peak."""
+    import re
+    txt = open(os.path.join(ROOT, "awebox_amd", "csrc", "ap2_nodejac.gen.hpp")).read()
+    fl = [int(x) for x in re.search(r"kFlops\[2\] = \{(\d+), (\d+)\}", txt).groups()]
+    tr = [int(x) for x in re.search(r"kTranscendental\[2\] = \{(\d+), (\d+)\}", txt).groups()]
+    nt = [int(x) for x in re.search(r"kNTan\[2\] = \{(\d+), (\d+)\}", txt).groups()]
+    n_k, d = lay.n_k, lay.d
+    node_ops = n_k * fl[0] + n_k * d * fl[1]
+    tf_node = node_ops * B / (node_ms * 1e-3) / 1e12
+    obj = (2 * d * 64 + d + 1) & ~1
+    gather_bytes = 8 * (n_k * (obj + nt[0] + d * nt[1]) + ev.nnz + lay.n_v) + 8 * lay.n_v   # run in; J, grad out; V (tf)
+    gbs = gather_bytes * B / (gather_ms * 1e-3) / 1e9
+    return {"ap2_node_kernel": {"ms": node_ms, "bound": "fp64",
+                                "achieved": tf_node, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                "frac": tf_node / FP64_PEAK_TFLOPS, "ops_per_eval": node_ops,
+                                "transcendentals_per_eval": n_k * tr[0] + n_k * d * tr[1],
+                                "note": "adds, multiplies and reciprocals of the generated node programs "
+                                        "(kFlops of ap2_nodejac.gen.hpp) x nodes / node-kernel time"},
+            "ap2_gather_kernel": {"ms": gather_ms, "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "bytes_per_eval": gather_bytes,
+                                  "note": "nodebuf run read + J_g and gradient written per evaluation"}}
 
 
 def pmc_record(batch: int):
@@ -219,12 +248,17 @@ def main():
         elapsed = float(t.item())
 
     # dominant-kernel duration from the HIP events the library records on the launch stream
-    kms, fms = [], []
+    kms, fms, nms, gms = [], [], [], []
+    gen = ev.path == "generated"
     for _ in range(min(args.steps, 20)):
         step()
         a, b_ = ev.last_kernel_ms()
         kms.append(a)
         fms.append(b_)
+        if gen:
+            n_, g_ = ev.last_kernel_ms_gen()
+            nms.append(n_)
+            gms.append(g_)
     torch.cuda.synchronize()
     finite = bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item())
 
@@ -273,11 +307,16 @@ def main():
                    "parallelism": f"replicas x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "ap2_interval_kernel", "kernel_ms": kernel_ms,
-                     "finalize_ms": float(np.mean(fms)), "bytes_per_eval": bytes_per_eval},
+                     "kernel": "ap2_node_kernel + ap2_gather_kernel" if gen else "ap2_interval_kernel",
+                     "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)), "bytes_per_eval": bytes_per_eval},
         "outputs_finite": finite,
+        "eval_path": ev.path,
     }
+    if gen:
+        line["roofline"]["kernels"] = gen_kernels(ev, lay, B, float(np.mean(nms)), float(np.mean(gms)))
     rec = pmc_record(B)
+    if rec is not None and rec.get("path", "colour") != ev.path:
+        rec = None
     fp64 = {}
     alg = flops_record()
     if alg is not None:

@@ -158,8 +158,8 @@ int awe_last_hess_ms(awe_handle h, float* ms);
 /* Evaluation path of awe_eval_nlp (f, g, grad f, J_g):
  *   AWE_PATH_GENERATED (default when the model constants have the structure the code was generated
  *     for): ap2_node_kernel, one thread per collocation node running straight-line value + sparse
- *     Jacobian code generated at build time from the node model (csrc/gen/ap2_jacgen.cpp), then
- *     the interval assembly kernel;
+ *     Jacobian code generated at build time from the node model (csrc/gen/ap2_jacgen.cpp; it also
+ *     writes the g rows and the objective terms), then the gather kernel (J_g values, gradient);
  *   AWE_PATH_COLOUR: the single interval kernel with compressed forward mode, one colour of seed
  *     directions per lane.
  * Both return the same values to rounding.  The environment variable AWE_EVAL_PATH=colour selects
@@ -168,8 +168,8 @@ int awe_last_hess_ms(awe_handle h, float* ms);
 #define AWE_PATH_GENERATED 1
 int awe_set_eval_path(awe_handle h, int path);
 int awe_get_eval_path(awe_handle h, int* path);
-/* Kernel times of the last awe_eval_nlp call on the generated path: node kernel, assembly kernel. */
-int awe_last_kernel_ms_gen(awe_handle h, float* ms_node, float* ms_assemble);
+/* Kernel times of the last awe_eval_nlp call on the generated path: node kernel, gather kernel. */
+int awe_last_kernel_ms_gen(awe_handle h, float* ms_node, float* ms_gather);
 
 /* Kernel time of the last awe_eval_* call on its stream, in milliseconds (HIP events). */
 int awe_last_kernel_ms(awe_handle h, float* ms_main, float* ms_finalize);
