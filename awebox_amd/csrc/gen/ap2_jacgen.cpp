@@ -242,13 +242,15 @@ int main(int argc, char** argv) {
     }
     o << "};\n\n";
     o << "// shooting node: val[0..32] = 24 equalities + 9 path inequalities, tan[kNTan[0]]\n";
-    o << "template <class In>\nAWE_HD void ap2_node_shoot(const In& in, const double* __restrict__ th, "
+    o << "// tangent s of the node is stored at tan[s * TS] (TS = 64: lane-interleaved, one wavefront's nodes\n";
+    o << "// side by side, so that a store instruction writes 64 consecutive doubles)\n";
+    o << "template <int TS, class In>\nAWE_HD void ap2_node_shoot(const In& in, const double* __restrict__ th, "
          "const double* __restrict__ cst, double* __restrict__ val, double* __restrict__ tan) {\n";
     o << ks.body << "}\n\n";
     o << "// Radau node: val[0..23] equalities, tan[kNTan[1]]; obv[0] side slip, obv[1] power integrand;\n";
     o << "// dbp[i] = directional derivative of ex2 beta^2 + ex3 power along seed direction kDbpDir[i];\n";
     o << "// ex0 = C[j][j] / (h t_f), ex1 = 1 / t_f\n";
-    o << "template <class In>\nAWE_HD void ap2_node_radau(const In& in, const double ex0, const double ex1, "
+    o << "template <int TS, class In>\nAWE_HD void ap2_node_radau(const In& in, const double ex0, const double ex1, "
          "const double ex2, const double ex3, const double* __restrict__ th, const double* __restrict__ cst, "
          "double* __restrict__ val, double* __restrict__ tan, double* __restrict__ dbp, double* __restrict__ obv) {\n";
     o << kr.body << "}\n\n}  // namespace awe_gen\n";

@@ -55,8 +55,8 @@ int main(int argc, char** argv) {
         std::vector<double> val(36, 0.0), tan(awe_gen::kNTan[kind], 0.0), dbp(64, 0.0), obv(2, 0.0);
         const double cb = 0.37, cpp = -1.9;   // objective weights of the beta^2 and power terms
         PlainIn pin{w.data()};
-        if (kind == 0) awe_gen::ap2_node_shoot(pin, th.data(), cst.data(), val.data(), tan.data());
-        else awe_gen::ap2_node_radau(pin, cxx, inv_tf, cb, cpp, th.data(), cst.data(), val.data(), tan.data(),
+        if (kind == 0) awe_gen::ap2_node_shoot<1>(pin, th.data(), cst.data(), val.data(), tan.data());
+        else awe_gen::ap2_node_radau<1>(pin, cxx, inv_tf, cb, cpp, th.data(), cst.data(), val.data(), tan.data(),
                                      dbp.data(), obv.data());
         double dv = 0.0, dt = 0.0, tmax = 0.0;
         int covered = 0;

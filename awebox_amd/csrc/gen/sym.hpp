@@ -557,7 +557,7 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
             std::snprintf(buf, sizeof(buf), "    obv[%d] = %s;\n", x.row, ref(x.node).c_str());
         } else {
             x.slot = next_slot++;
-            std::snprintf(buf, sizeof(buf), "    tan[%d] = %s;\n", x.slot, ref(x.node).c_str());
+            std::snprintf(buf, sizeof(buf), "    tan[%d * TS] = %s;\n", x.slot, ref(x.node).c_str());
             st.n_tan++;
             if (t.n[x.node].op == Op::Const) st.n_zero_tan++;
         }
