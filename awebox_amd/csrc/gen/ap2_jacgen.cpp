@@ -95,13 +95,6 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs&
     } else {
         for (int r = 0; r < AWE_N_EQ; ++r) rows.push_back(r);
     }
-    if (const char* rr = std::getenv("AWE_GEN_ROWS")) {   // experiment: a row range only
-        int lo = 0, hi = 0;
-        std::sscanf(rr, "%d-%d", &lo, &hi);
-        std::vector<int> keep;
-        for (int r : rows) if (r >= lo && r <= hi) keep.push_back(r);
-        rows.swap(keep);
-    }
     std::vector<awe::Store> stores;
     const int zero = tape.cnst(0.0);
     for (int r : rows) {
