@@ -177,6 +177,8 @@ def main():
                     help="closed loops per GPU for the converged-MPC block (Pmpc.step on the batched IPM; 0: skip)")
     ap.add_argument("--dual-batch", type=int, default=128,
                     help="dual-kite NLP instances for the config-3 block (N=60 d=4 single_reelout; 0: skip)")
+    ap.add_argument("--no-dual-chain", action="store_true",
+                    help="skip the chain-mode (sequential warm start) rate of the config-4 shard")
     ap.add_argument("--dual-sweep-points", type=int, default=8,
                     help="dual-kite u_ref sweep points per GPU (config 4: 8 of linspace(5, 8, 64), example "
                          "discretization N=20; 0: skip)")
@@ -277,7 +279,7 @@ def main():
         sweep = sweep_block(args.sweep_points, world, dist, dev, consts)
     dual_sweep = None
     if args.dual_sweep_points > 0:
-        dual_sweep = dual_sweep_block(args.dual_sweep_points, world, dist, dev)
+        dual_sweep = dual_sweep_block(args.dual_sweep_points, world, dist, dev, with_chain=not args.no_dual_chain)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -691,7 +693,7 @@ def sweep_block(per_gpu, world, dist, dev, consts):
             "utilisation": sweep_profile("ap2")}
 
 
-def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
+def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4, with_chain=True):
     """Config 4: the dual-kite power curve (examples/dual_kites_power_curve.py: architecture
     {1:0, 2:1, 3:1}, N=20 d=4 as in the example, single_reelout), each GPU's shard of
     u_ref = linspace(5, 8, 64): `per_gpu` contiguous points (weak scaling), template broadcast / seed
@@ -710,6 +712,21 @@ def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
     torch.cuda.synchronize()
     res = run_sweep(u, n_k=n_k, d=d, make_evaluator=lambda c, b=1: make_evaluator(c, device=str(dev), batch=b),
                     dist=dist, device=str(dev), opts=IpmOptions(max_iter=3000), arch="dual", mode="fan")
+    chain = None
+    if with_chain:
+        # the reference's own sweep order (awebox/sweep.py:154-163): the shard's points one after
+        # the other, each warm-started from the previous solution
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        rc = run_sweep(u, n_k=n_k, d=d, make_evaluator=lambda c, b=1: make_evaluator(c, device=str(dev), batch=b),
+                       dist=dist, device=str(dev), opts=IpmOptions(max_iter=3000), arch="dual", mode="chain")
+        if rc is not None:
+            chain = {"value": rc["trials_per_s"], "unit": "trials/s", "wall_s": rc["wall_s"],
+                     "all_converged": bool(all(rc["ok"])), "iterations": rc["iterations"],
+                     "avg_power_W": [round(p, 1) for p in rc["avg_power_W"]],
+                     "mode": "chain: homotopy for the shard's first point, then each point warm-started from the "
+                             "previous one, sequentially (the reference's sweep)"}
     if res is None:
         return None
     return {"metric": f"sweep trials/sec, dual-kite power curve N={n_k} d={d} (config 4)",
@@ -721,7 +738,8 @@ def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4):
             "solver": "GPU interior point (awebox_amd/ipm.py): homotopy for the shard's first point, batched warm "
                       "start for the rest; structured KKT with the block-recursion separator sweep, exact KKT "
                       "inertia; exact Hessian of the Lagrangian (dual_hess_kernel: colour-pair hyper-dual forward mode)",
-            "utilisation": sweep_profile("dual")}
+            "mode": "fan: homotopy for the shard's first point, one batched warm start for the rest",
+            "chain": chain, "utilisation": sweep_profile("dual")}
 
 
 def hessian_block(ev, V, P, B, lay, dev, steps=10):

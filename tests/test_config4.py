@@ -73,3 +73,18 @@ def test_config4_shard_at_stated_shape_fan_vs_chain(gpu):
     assert pf[0] == pc[0]                                       # the same homotopy for point 0
     assert np.allclose(pf, pc, rtol=1e-3), (pf, pc)
     assert np.allclose(fan["period_s"], chain["period_s"], rtol=1e-2)
+
+
+def test_config4_hardest_shard_converges_with_rising_power(gpu):
+    """Rank 7's shard of config 4 -- points 56..63 of linspace(5, 8, 64), u_ref 7.62..8.0 m/s, the
+    far end of the power curve from the homotopy's standard initial guess -- at the example's N=20
+    d=4 in fan mode: the homotopy of the shard's first point and the batched warm start of the
+    other seven converge, and the power rises with u_ref (profiles/r04/config4_full.jsonl holds all
+    eight shards)."""
+    u = np.linspace(5.0, 8.0, 64)[56:64]
+    res = _sweep(u, n_k=20, mode="fan")
+    print("shard 7", res["avg_power_W"], res["period_s"], res["iterations"], res["wall_s"])
+    assert all(res["ok"]), res
+    p = np.asarray(res["avg_power_W"])
+    assert np.all(np.isfinite(p)) and p[0] > 1000.0 and np.all(np.diff(p) > 0), p
+    assert np.allclose(res["u_ref"], u)
