@@ -16,6 +16,7 @@
 // The model constants enter as run-time loads (cst[i]); only the integer structure read from
 // them (tether elements, stability-derivative table lengths) is fixed at generation time and
 // written out, so that awe_create can check it.
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -126,8 +127,11 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs&
         }
     }
     KindOut ko;
-    const char* fe = std::getenv("AWE_GEN_FENCE_EVERY");
-    const int fence = fe ? std::atoi(fe) : 0;
+    // a scheduling fence every kFenceEvery statements keeps the compiler's machine scheduler near
+    // the pressure-scheduled order (without fences it hoists and interleaves until the register
+    // allocator spills to scratch: 392 -> 127 scratch reloads in the instance-minor node kernel)
+    constexpr int kFenceEvery = 32;
+    const int fence = kFenceEvery;
     // direction strips: contiguous direction ranges with balanced tangent counts; strip 0 also
     // stores the row values.  Each strip is its own scope and recomputes the values it needs.
     std::vector<int> per_dir(awt::kDirs, 0);
@@ -222,6 +226,21 @@ int main(int argc, char** argv) {
     o << "constexpr int kDbpDir[" << std::max<size_t>(1, ko_dbp_dirs.size()) << "] = {";
     for (size_t i = 0; i < ko_dbp_dirs.size(); ++i) o << (i ? ", " : "") << ko_dbp_dirs[i];
     o << "};\n";
+    // theta0 entries the node code reads (either kind): the instance-minor kernel stages only these
+    std::vector<int> th_row(AWE_NTHETA0, -1);
+    int n_th = 0;
+    for (const std::string* b : {&ks.body, &kr.body})
+        for (size_t p = b->find("th["); p != std::string::npos; p = b->find("th[", p + 3)) {
+            if (p > 0 && (std::isalnum((unsigned char)(*b)[p - 1]) || (*b)[p - 1] == '_')) continue;
+            const int i = std::atoi(b->c_str() + p + 3);
+            if (i >= 0 && i < AWE_NTHETA0 && th_row[i] < 0) th_row[i] = 0;
+        }
+    for (int i = 0; i < AWE_NTHETA0; ++i) if (th_row[i] == 0) th_row[i] = n_th++;
+    o << "// theta0 entries read by the node code: kThRow[i] is the compact row of th[i] (-1: unused)\n";
+    o << "constexpr int kNThUsed = " << n_th << ";\n";
+    o << "constexpr short kThRow[" << AWE_NTHETA0 << "] = {";
+    for (int i = 0; i < AWE_NTHETA0; ++i) o << (i ? "," : "") << th_row[i];
+    o << "};\n";
     o << "// tangent-buffer slot of (row, direction), -1 where the pattern has no entry\n";
     o << "constexpr short kTanIdx[2][35][64] = {\n";
     for (const KindOut* k : {&ks, &kr}) {
@@ -237,15 +256,18 @@ int main(int argc, char** argv) {
     o << "// shooting node: val[0..32] = 24 equalities + 9 path inequalities, tan[kNTan[0]]\n";
     o << "// tangent s of the node is stored at tan[s * TS] (TS = 64: lane-interleaved, one wavefront's nodes\n";
     o << "// side by side, so that a store instruction writes 64 consecutive doubles)\n";
-    o << "template <int TS, class In>\nAWE_HD void ap2_node_shoot(const In& in, const double* __restrict__ th, "
-         "const double* __restrict__ cst, double* __restrict__ val, double* __restrict__ tan) {\n";
+    o << "// th, val, tan: pointers, or accessor objects with operator[] (the instance-minor kernel reads\n"
+         "// th[i] at THT[i * ld + b] and sends tan[s] to the J_g entries of slot s)\n";
+    o << "template <int TS, class In, class Th, class Val, class Tan>\nAWE_HD void ap2_node_shoot(const In& in, Th th, "
+         "const double* __restrict__ cst, Val val, Tan tan) {\n";
     o << ks.body << "}\n\n";
     o << "// Radau node: val[0..23] equalities, tan[kNTan[1]]; obv[0] side slip, obv[1] power integrand;\n";
     o << "// dbp[i] = directional derivative of ex2 beta^2 + ex3 power along seed direction kDbpDir[i];\n";
     o << "// ex0 = C[j][j] / (h t_f), ex1 = 1 / t_f\n";
-    o << "template <int TS, class In>\nAWE_HD void ap2_node_radau(const In& in, const double ex0, const double ex1, "
-         "const double ex2, const double ex3, const double* __restrict__ th, const double* __restrict__ cst, "
-         "double* __restrict__ val, double* __restrict__ tan, double* __restrict__ dbp, double* __restrict__ obv) {\n";
+    o << "template <int TS, class In, class Th, class Val, class Tan, class Dbp, class Obv>\n"
+         "AWE_HD void ap2_node_radau(const In& in, const double ex0, const double ex1, "
+         "const double ex2, const double ex3, Th th, const double* __restrict__ cst, "
+         "Val val, Tan tan, Dbp dbp, Obv obv) {\n";
     o << kr.body << "}\n\n}  // namespace awe_gen\n";
 
     std::ofstream out(argv[2]);

@@ -29,7 +29,10 @@ EXPORTED_SYMBOLS = ["awe_create", "awe_destroy", "awe_last_error", "awe_sizes", 
                     "awe_eval_g_host",
                     "awe_last_kernel_ms", "awe_device_count", "awe_hess_nnz", "awe_sparsity_hess",
                     "awe_sparsity_hess_static", "awe_eval_hess", "awe_eval_hess_host", "awe_last_hess_ms",
-                    "awe_set_eval_path", "awe_get_eval_path", "awe_last_kernel_ms_gen"]
+                    "awe_set_eval_path", "awe_get_eval_path", "awe_last_kernel_ms_gen", "awe_eval_nlp_im",
+                    "awe_last_kernel_ms_soa"]
+
+PATH_COLOUR, PATH_GENERATED, PATH_SOA = 0, 1, 2
 
 
 class AwegpuUnavailable(RuntimeError):
@@ -57,6 +60,9 @@ def load_library(path: str = _LIB_PATH):
     lib.awe_sparsity_jac.argtypes = [h, ip, ip]
     lib.awe_eval_nlp.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.awe_eval_nlp_im.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    lib.awe_last_kernel_ms_soa.argtypes = [h, ctypes.POINTER(ctypes.c_float)]
     lib.awe_eval_g.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.awe_eval_f.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.awe_eval_nlp_host.argtypes = [h, dp, dp, dp, dp, dp, dp]
@@ -180,17 +186,43 @@ class Ap2Evaluator:
 
     # ---------------------------------------------- device path (torch CUDA tensors) ---
     def eval_nlp_device(self, V, P, f, g, grad_f, jac, stream=None):
-        """f, g, grad f, J_g values for all batch members; tensors must be contiguous fp64 on
-        the GPU with shapes [B, n_v], [B, n_p], [B], [B, n_g], [B, n_v], [B, nnz]."""
+        """f, g, grad f, J_g values for all batch members; fp64 CUDA tensors of shapes [B, n_v],
+        [B, n_p], [B], [B, n_g], [B, n_v] (contiguous) and jac [B, nnz]: contiguous (awe_eval_nlp),
+        or the instance-minor view ``jac_t.t()`` of a contiguous [nnz, ld] tensor with ld >= B
+        (awe_eval_nlp_im, the layout the batched solver reads; ``alloc_jac``)."""
         import torch
-        for t, n in ((V, self.n_v), (P, self.n_p), (g, self.n_g), (grad_f, self.n_v), (jac, self.nnz)):
+        for t, n in ((V, self.n_v), (P, self.n_p), (g, self.n_g), (grad_f, self.n_v)):
             if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
                 raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
         if f.numel() != self.batch:
             raise ValueError("f must hold one value per batch member")
+        if jac.dtype != torch.float64 or not jac.is_cuda or tuple(jac.shape) != (self.batch, self.nnz):
+            raise ValueError("jac must be a float64 CUDA tensor of shape [batch, nnz]")
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        self._check(self._lib.awe_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
-                                           grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
+        if jac.is_contiguous():
+            self._check(self._lib.awe_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
+                                               grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
+        elif jac.stride(0) == 1 and jac.stride(1) >= self.batch:
+            self._check(self._lib.awe_eval_nlp_im(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(),
+                                                  g.data_ptr(), grad_f.data_ptr(), jac.data_ptr(),
+                                                  int(jac.stride(1)), ctypes.c_void_p(s)))
+        else:
+            raise ValueError("jac must be contiguous or an instance-minor view (strides (1, ld))")
+
+    def alloc_jac(self, device="cuda", instance_minor=True):
+        """A J_g value tensor [B, nnz]; instance-minor (the transposed view of [nnz, B], which the
+        instance-minor kernel writes with coalesced stores) unless asked otherwise."""
+        import torch
+        if instance_minor:
+            return torch.zeros(self.nnz, self.batch, dtype=torch.float64, device=device).t()
+        return torch.zeros(self.batch, self.nnz, dtype=torch.float64, device=device)
+
+    def last_kernel_ms_soa(self):
+        """HIP-event times of the last instance-minor call: input transpose, node kernel, interval
+        kernel, finalize, output transpose (ms)."""
+        ms = (ctypes.c_float * 5)()
+        self._check(self._lib.awe_last_kernel_ms_soa(self._h, ms))
+        return [float(x) for x in ms]
 
     def eval_g_device(self, V, P, g, stream=None):
         import torch
@@ -250,9 +282,11 @@ class Ap2Evaluator:
         self._check(self._lib.awe_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
-    # evaluation path of eval_nlp (include/awegpu.h): "generated" (one thread per collocation
-    # node, build-time generated sparse-Jacobian code) or "colour" (compressed forward mode)
-    PATHS = {"colour": 0, "generated": 1}
+    # evaluation path of eval_nlp (include/awegpu.h): "soa" (the default: one lane per instance,
+    # the build-time generated sparse-Jacobian code storing straight into J_g), "generated" (one
+    # thread per collocation node, tangents gathered by a second kernel) or "colour" (compressed
+    # forward mode)
+    PATHS = {"colour": PATH_COLOUR, "generated": PATH_GENERATED, "soa": PATH_SOA}
 
     @property
     def path(self):

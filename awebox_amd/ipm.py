@@ -172,7 +172,9 @@ class DeviceNlp:
         self.f = torch.zeros(B, **f64)
         self.g = torch.zeros(B, n_g, **f64)
         self.grad = torch.zeros(B, n_v, **f64)
-        self.jac = torch.zeros(B, ev.nnz, **f64)
+        # J_g in the evaluator's instance-minor layout where it has one (the AP2 evaluator writes it
+        # with coalesced stores, awe_eval_nlp_im); a [B, nnz] view either way
+        self.jac = ev.alloc_jac(device) if hasattr(ev, "alloc_jac") else torch.zeros(B, ev.nnz, **f64)
         self.H = torch.zeros(B, ev.nnz_h, **f64)
         self.sig = torch.ones(B, **f64)
         self.free_t = torch.tensor(self.free, device=device)

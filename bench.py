@@ -148,6 +148,68 @@ def gen_kernels(ev, lay, B, node_ms, gather_ms):
                                   "note": "nodebuf run read + J_g and gradient written per evaluation"}}
 
 
+def soa_kernels(ev, lay, B, ms):
+    """Per-kernel view of the instance-minor path (HIP events per kernel, mean over the timed
+    launches): algorithmic bytes of each kernel against HBM peak, and the node kernel's generated
+    operation rate against the FP64 vector peak."""
+    import re
+    txt = open(os.path.join(ROOT, "awebox_amd", "csrc", "ap2_nodejac.gen.hpp")).read()
+    fl = [int(x) for x in re.search(r"kFlops\[2\] = \{(\d+), (\d+)\}", txt).groups()]
+    ndbp = int(re.search(r"kNDbp = (\d+)", txt).group(1))
+    n_k, d = lay.n_k, lay.d
+    tail = 20 + 200                                         # P's cost + theta0 tail (kSoaThRows)
+    obj = n_k * d * (2 + ndbp)
+    by = {"ap2_soa_in_kernel": 8 * 2 * (lay.n_v + tail),                       # V, P tail in; VT, THT out
+          "ap2_soa_node_kernel": 8 * (lay.n_v + tail + ev.nnz + lay.n_g + obj),  # VT, THT in; J_g, g, objb out
+          "ap2_gather_kernel<D, true>": 8 * (2 * lay.n_v + 59 + 20 + 2 + obj + lay.n_v + lay.n_g // 8)}
+    names = ["ap2_soa_in_kernel", "ap2_soa_node_kernel", "ap2_gather_kernel<D, true>", "ap2_finalize_kernel",
+             "soa_to_aos_kernel"]
+    out = {}
+    for i, name in enumerate(names):
+        t = float(ms[i])
+        if t <= 0:
+            continue
+        o = {"ms": t}
+        if name in by:
+            gbs = by[name] * B / (t * 1e-3) / 1e9
+            o.update({"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_eval": by[name]})
+        if name == "ap2_soa_node_kernel":
+            ops = n_k * fl[0] + n_k * d * fl[1]
+            o["fp64_generated_ops"] = {"achieved": ops * B / (t * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                                       "unit": "TFLOP/s", "ops_per_eval": ops}
+        out[name] = o
+    return out
+
+
+def path_ab(ev, V, P, f, g, gr, B, dev, stream, reps=10):
+    """The same evaluation on every path and J_g layout, HIP-event time per call (ms): the
+    instance-minor path writing the solver's layout (the headline) or per-instance J_g (plus the
+    transpose), the node + gather path and the colour path."""
+    import torch
+    import numpy as np
+    keep = ev.path
+    out = {}
+    jac_aos = ev.alloc_jac(dev, instance_minor=False)
+    jac_im = ev.alloc_jac(dev, instance_minor=True)
+    for name, path, jac in (("soa_instance_minor", "soa", jac_im), ("soa_per_instance", "soa", jac_aos),
+                            ("generated", "generated", jac_aos), ("colour", "colour", jac_aos)):
+        try:
+            ev.path = path
+        except Exception:
+            continue
+        ms = []
+        for _ in range(reps + 2):
+            ev.eval_nlp_device(V, P, f, g, gr, jac, stream=stream.cuda_stream)
+            a, b_ = ev.last_kernel_ms()
+            ms.append(a + b_)
+        out[name] = float(np.mean(ms[2:]))
+    ev.path = keep
+    torch.cuda.synchronize()
+    del jac_aos, jac_im
+    return out
+
+
 def pmc_record(batch: int):
     """The committed PMC record for these sources and batch size, or None."""
     try:
@@ -224,7 +286,8 @@ def main():
     f = torch.empty(B, dtype=torch.float64, device=dev)
     g = torch.empty(B, ev.n_g, dtype=torch.float64, device=dev)
     gr = torch.empty(B, ev.n_v, dtype=torch.float64, device=dev)
-    jac = torch.empty(B, ev.nnz, dtype=torch.float64, device=dev)
+    # J_g in the layout the batched solver reads: instance-minor ([nnz, B] storage, [B, nnz] view)
+    jac = ev.alloc_jac(dev, instance_minor=True)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -250,19 +313,23 @@ def main():
         elapsed = float(t.item())
 
     # dominant-kernel duration from the HIP events the library records on the launch stream
-    kms, fms, nms, gms = [], [], [], []
+    kms, fms, nms, gms, sms = [], [], [], [], []
     gen = ev.path == "generated"
+    soa = ev.path == "soa"
     for _ in range(min(args.steps, 20)):
         step()
         a, b_ = ev.last_kernel_ms()
-        kms.append(a)
+        kms.append(a + b_ if soa else a)
         fms.append(b_)
         if gen:
             n_, g_ = ev.last_kernel_ms_gen()
             nms.append(n_)
             gms.append(g_)
+        if soa:
+            sms.append(ev.last_kernel_ms_soa())
     torch.cuda.synchronize()
     finite = bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item())
+    paths = path_ab(ev, V, P, f, g, gr, B, dev, stream) if rank == 0 else None
 
     dual = None
     if args.dual_batch > 0:
@@ -309,13 +376,18 @@ def main():
                    "parallelism": f"replicas x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "ap2_node_kernel + ap2_gather_kernel" if gen else "ap2_interval_kernel",
+                     "kernel": ("ap2_soa_in + ap2_soa_node + ap2_gather<true> + ap2_finalize (one evaluation)"
+                                if soa else "ap2_node_kernel + ap2_gather_kernel" if gen else "ap2_interval_kernel"),
                      "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)), "bytes_per_eval": bytes_per_eval},
         "outputs_finite": finite,
         "eval_path": ev.path,
     }
     if gen:
         line["roofline"]["kernels"] = gen_kernels(ev, lay, B, float(np.mean(nms)), float(np.mean(gms)))
+    if soa:
+        line["roofline"]["kernels"] = soa_kernels(ev, lay, B, np.mean(np.array(sms), axis=0))
+    if paths is not None:
+        line["paths"] = paths
     rec = pmc_record(B)
     if rec is not None and rec.get("path", "colour") != ev.path:
         rec = None

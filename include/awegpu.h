@@ -155,21 +155,40 @@ int awe_eval_hess_host(awe_handle h, const double* V, const double* P, const dou
 /* Kernel time of the last awe_eval_hess call (HIP events), milliseconds. */
 int awe_last_hess_ms(awe_handle h, float* ms);
 
-/* Evaluation path of awe_eval_nlp (f, g, grad f, J_g):
- *   AWE_PATH_GENERATED (default when the model constants have the structure the code was generated
- *     for): ap2_node_kernel, one thread per collocation node running straight-line value + sparse
- *     Jacobian code generated at build time from the node model (csrc/gen/ap2_jacgen.cpp; it also
- *     writes the g rows and the objective terms), then the gather kernel (J_g values, gradient);
+/* nlp_grad_f + nlp_jac_g fused, with J_g instance-minor: the value of CCS entry i of instance b at
+ * jac[i * ldj + b] (ldj >= batch; V, P, g, grad_f and f as in awe_eval_nlp).  The layout the batched
+ * solver consumes (a [batch, nnz] view with strides (1, ldj)); with batch = 1 and ldj = 1 it is
+ * awe_eval_nlp's.  On the instance-minor path the node kernel writes it directly, on the other paths
+ * the per-instance result is transposed. */
+int awe_eval_nlp_im(awe_handle h, const double* V, const double* P, double* f, double* g,
+                    double* grad_f, double* jac, int ldj, void* stream);
+
+/* Evaluation path of awe_eval_nlp / awe_eval_nlp_im (f, g, grad f, J_g):
+ *   AWE_PATH_SOA (default when the model constants have the structure the code was generated for):
+ *     instance-minor generated path -- V and P's tail transposed to instance-minor order, then
+ *     ap2_soa_node_kernel, one wavefront per (interval, node) and one lane per instance, running the
+ *     generated straight-line code and storing every tangent directly into its J_g entries through
+ *     a per-(interval, node) destination table; the interval kernel adds the objective, gradient and
+ *     continuity rows;
+ *   AWE_PATH_GENERATED: ap2_node_kernel, one thread per collocation node running straight-line
+ *     value + sparse Jacobian code generated at build time from the node model
+ *     (csrc/gen/ap2_jacgen.cpp; it also writes the g rows and the objective terms), then the gather
+ *     kernel (J_g values, gradient);
  *   AWE_PATH_COLOUR: the single interval kernel with compressed forward mode, one colour of seed
  *     directions per lane.
- * Both return the same values to rounding.  The environment variable AWE_EVAL_PATH=colour selects
- * the colour path at awe_create. */
+ * All return the same values to rounding.  The environment variable AWE_EVAL_PATH=colour|generated
+ * selects another path at awe_create. */
 #define AWE_PATH_COLOUR 0
 #define AWE_PATH_GENERATED 1
+#define AWE_PATH_SOA 2
 int awe_set_eval_path(awe_handle h, int path);
 int awe_get_eval_path(awe_handle h, int* path);
 /* Kernel times of the last awe_eval_nlp call on the generated path: node kernel, gather kernel. */
 int awe_last_kernel_ms_gen(awe_handle h, float* ms_node, float* ms_gather);
+/* Kernel times of the last call on the instance-minor path (HIP events, ms): ms[0] input transpose,
+ * ms[1] node kernel, ms[2] interval kernel, ms[3] finalize, ms[4] output transpose (awe_eval_nlp at
+ * batch > 1; 0 otherwise). */
+int awe_last_kernel_ms_soa(awe_handle h, float* ms);
 
 /* Kernel time of the last awe_eval_* call on its stream, in milliseconds (HIP events). */
 int awe_last_kernel_ms(awe_handle h, float* ms_main, float* ms_finalize);

@@ -1,6 +1,14 @@
-"""The two evaluation paths of awe_eval_nlp on MI355X: the generated path (ap2_node_kernel with
-build-time generated node-Jacobian code + ap2_assemble_kernel, the default) and the colour path
-(compressed forward mode) return the same f, g, grad f and J_g to rounding, at the bench's shape."""
+"""The evaluation paths of awe_eval_nlp on MI355X return the same f, g, grad f and J_g:
+
+* the instance-minor path (ap2_soa_node_kernel, one lane per instance, tangents stored straight into
+  J_g through the destination table; the default) agrees BITWISE with the node + gather path (the
+  same generated node code and the same interval arithmetic), in both J_g layouts -- per instance
+  (awe_eval_nlp) and instance-minor (awe_eval_nlp_im, the solver's layout);
+* the node + gather path agrees with the colour path (compressed forward mode) to rounding.
+
+At the bench's shape (B = 64, one full instance block), a ragged batch (B = 70: a partial block,
+lanes past the batch idle) and B = 1 (the solver's single-instance calls).  Oracle parity of the
+default path is tests/test_gpu_parity.py."""
 import numpy as np
 import pytest
 
@@ -12,34 +20,56 @@ def _close(a, b, rtol=1e-9):
     assert np.all(np.abs(a - b) <= rtol * np.abs(b) + 1e-11 * scale), float(np.max(np.abs(a - b)))
 
 
-def test_generated_path_is_default_and_matches_colour_path():
+def _inputs(B):
     import torch
 
-    from awebox_amd import evaluator as E
     from awebox_amd import problem as pb
     from awebox_amd.initial_guess import batch_member, initial_guess
     consts = pb.build_constants()
     lay = pb.NlpLayout(40, 4)
     v0 = initial_guess(consts, lay)
-    B = 64
-    ev = E.Ap2Evaluator(consts, batch=B)
-    assert ev.path == "generated"
     V = torch.tensor(np.stack([batch_member(v0, lay, b) for b in range(B)]), device="cuda")
     P = torch.tensor(np.stack([pb.pack_p(lay, consts, v0, u_ref=5.0 + 0.05 * b) for b in range(B)]), device="cuda")
-    out = {}
-    for path in ("generated", "colour"):
-        ev.path = path
-        f = torch.empty(B, dtype=torch.float64, device="cuda")
-        g = torch.empty(B, ev.n_g, dtype=torch.float64, device="cuda")
-        gr = torch.empty(B, ev.n_v, dtype=torch.float64, device="cuda")
-        jac = torch.empty(B, ev.nnz, dtype=torch.float64, device="cuda")
-        ev.eval_nlp_device(V, P, f, g, gr, jac)
-        torch.cuda.synchronize()
-        out[path] = [x.cpu().numpy() for x in (f, g, gr, jac)]
-        if path == "generated":
-            node_ms, asm_ms = ev.last_kernel_ms_gen()
-            assert node_ms > 0 and asm_ms > 0
+    return consts, V, P
+
+
+def _eval(ev, V, P, path, instance_minor):
+    import torch
+    B = ev.batch
+    ev.path = path
+    f = torch.empty(B, dtype=torch.float64, device="cuda")
+    g = torch.empty(B, ev.n_g, dtype=torch.float64, device="cuda")
+    gr = torch.empty(B, ev.n_v, dtype=torch.float64, device="cuda")
+    jac = ev.alloc_jac("cuda", instance_minor=instance_minor)
+    jac.fill_(np.nan)
+    ev.eval_nlp_device(V, P, f, g, gr, jac)
+    torch.cuda.synchronize()
+    return [x.cpu().numpy() for x in (f, g, gr, jac)]
+
+
+@pytest.mark.parametrize("B", [64, 70, 1])
+def test_instance_minor_path_is_default_and_matches_the_other_paths(B):
+    from awebox_amd import evaluator as E
+    consts, V, P = _inputs(B)
+    ev = E.Ap2Evaluator(consts, batch=B)
+    assert ev.path == "soa"
+    out = {"soa_im": _eval(ev, V, P, "soa", True)}
+    ms = ev.last_kernel_ms_soa()
+    assert ms[1] > 0 and ms[2] > 0 and ms[4] < 0.05          # no output transpose in the solver's layout
+    out["soa_aos"] = _eval(ev, V, P, "soa", False)
+    out["generated"] = _eval(ev, V, P, "generated", False)
+    node_ms, asm_ms = ev.last_kernel_ms_gen()
+    assert node_ms > 0 and asm_ms > 0
+    out["colour"] = _eval(ev, V, P, "colour", False)
+    labels = ("f", "g", "grad_f", "jac")
+    diffs = {name: {lab: float(np.max(np.abs(a - b))) for lab, a, b in zip(labels, out[name], out["generated"])}
+             for name in ("soa_im", "soa_aos", "colour")}
+    print(diffs)
+    for name in ("soa_im", "soa_aos"):
+        for lab, a, b in zip(labels, out[name], out["generated"]):
+            assert np.isfinite(a).all(), (name, lab)
+            assert np.array_equal(a, b), (name, lab, diffs[name])
     for a, b in zip(out["generated"], out["colour"]):
         for i in range(B):
             _close(a[i], b[i])
-    ev.path = "generated"
+    ev.path = "soa"

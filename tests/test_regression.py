@@ -93,7 +93,8 @@ def _default_homotopy(path):
     consts = pb.build_constants()
     lay = pb.NlpLayout(40, 4)
     ev = Ap2Evaluator(consts, batch=1)
-    ev.path = path
+    if path is not None:
+        ev.path = path
     V, summary, out, res = optimize(consts, ev, IpmOptions(max_iter=2000))
     print(path, [(r["step"], r["iterations"], round(r["f"], 6)) for r in summary], out)
     return consts, lay, ev, V, summary, out
@@ -111,7 +112,7 @@ def _default_homotopy_cached(path):
 @pytest.mark.gpu
 def test_ap2_n40_homotopy_converges_and_repeats_bitwise():
     """The product's default path -- the full N=40 d=4 homotopy from the standard initial guess on
-    the HIP evaluator (generated path) with the default solver options (IPOPT's defaults as the
+    the HIP evaluator (its default instance-minor path, bitwise equal to the node + gather path) with the default solver options (IPOPT's defaults as the
     reference sets them, max_iter 2000, default.py:324): every step converges; the power anchor of
     test_examples.py:29-58 (4.7 kW within 20 %) holds; interval 0 of the returned V passes the
     collocation-integrator check of test_discretization.py (1e-7); a second run returns
@@ -120,7 +121,7 @@ def test_ap2_n40_homotopy_converges_and_repeats_bitwise():
     import torch
     if not torch.cuda.is_available():
         pytest.fail("GPU test on a machine without a visible GPU")
-    consts, lay, ev, V, summary, out = _default_homotopy_cached("generated")
+    consts, lay, ev, V, summary, out = _default_homotopy_cached(None)
     assert all(r["status"] == "solve_succeeded" for r in summary), summary
     err_p = (4.7 - out["avg_power_W"] / 1e3) / 4.7
     assert abs(err_p) <= ANCHOR_THRESHOLD, out
@@ -146,7 +147,7 @@ def test_ap2_n40_default_path_meets_the_reference_anchors():
     import torch
     if not torch.cuda.is_available():
         pytest.fail("GPU test on a machine without a visible GPU")
-    consts, lay, ev, V, summary, out = _default_homotopy_cached("generated")
+    consts, lay, ev, V, summary, out = _default_homotopy_cached(None)
     err_p = (4.7 - out["avg_power_W"] / 1e3) / 4.7
     err_t = (35.0 - out["period_s"]) / 35.0
     assert abs(err_p) <= ANCHOR_THRESHOLD and abs(err_t) <= ANCHOR_THRESHOLD, out
