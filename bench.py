@@ -150,19 +150,24 @@ def gen_kernels(ev, lay, B, node_ms, gather_ms):
 
 def soa_kernels(ev, lay, B, ms):
     """Per-kernel view of the instance-minor path (HIP events per kernel, mean over the timed
-    launches): algorithmic bytes of each kernel against HBM peak, and the node kernel's generated
-    operation rate against the FP64 vector peak."""
+    launches): algorithmic bytes of each kernel against HBM peak, and the node kernels' generated
+    operation rate against the FP64 vector peak.  ms: input transpose, shooting + Radau node
+    kernels, interval kernel, finalize, output transpose."""
     import re
     txt = open(os.path.join(ROOT, "awebox_amd", "csrc", "ap2_nodejac.gen.hpp")).read()
     fl = [int(x) for x in re.search(r"kFlops\[2\] = \{(\d+), (\d+)\}", txt).groups()]
     ndbp = int(re.search(r"kNDbp = (\d+)", txt).group(1))
+    nth = int(re.search(r"kNThUsed = (\d+)", txt).group(1))
     n_k, d = lay.n_k, lay.d
-    tail = 20 + 200                                         # P's cost + theta0 tail (kSoaThRows)
     obj = n_k * d * (2 + ndbp)
-    by = {"ap2_soa_in_kernel": 8 * 2 * (lay.n_v + tail),                       # V, P tail in; VT, THT out
-          "ap2_soa_node_kernel": 8 * (lay.n_v + tail + ev.nnz + lay.n_g + obj),  # VT, THT in; J_g, g, objb out
-          "ap2_gather_kernel<D, true>": 8 * (2 * lay.n_v + 59 + 20 + 2 + obj + lay.n_v + lay.n_g // 8)}
-    names = ["ap2_soa_in_kernel", "ap2_soa_node_kernel", "ap2_gather_kernel<D, true>", "ap2_finalize_kernel",
+    stride = 2 * 23 + 10 + 1 + d * 24
+    by = {"ap2_soa_in_kernel": 8 * 2 * (lay.n_v + lay.n_p),                      # V, P in; VT, PT out
+          # the interval slices + theta0 rows each node workgroup stages; J_g, g, objective terms out
+          "ap2_soa_shoot + ap2_soa_radau": 8 * (n_k * (stride + 2 * (nth + 6)) + ev.nnz + lay.n_g + obj),
+          # V and P slices, objective terms in; gradient, continuity rows, partials out
+          "ap2_soa_interval_kernel": 8 * (n_k * (stride + 23) + lay.n_v + 59 + 20 + 2 + obj + lay.n_v
+                                          + n_k * 23 + n_k * 4)}
+    names = ["ap2_soa_in_kernel", "ap2_soa_shoot + ap2_soa_radau", "ap2_soa_interval_kernel", "ap2_finalize_kernel",
              "soa_to_aos_kernel"]
     out = {}
     for i, name in enumerate(names):
@@ -174,7 +179,7 @@ def soa_kernels(ev, lay, B, ms):
             gbs = by[name] * B / (t * 1e-3) / 1e9
             o.update({"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": gbs / HBM_PEAK_GBS, "bytes_per_eval": by[name]})
-        if name == "ap2_soa_node_kernel":
+        if name == "ap2_soa_shoot + ap2_soa_radau":
             ops = n_k * fl[0] + n_k * d * fl[1]
             o["fp64_generated_ops"] = {"achieved": ops * B / (t * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
                                        "unit": "TFLOP/s", "ops_per_eval": ops}
@@ -376,7 +381,8 @@ def main():
                    "parallelism": f"replicas x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": ("ap2_soa_in + ap2_soa_node + ap2_gather<true> + ap2_finalize (one evaluation)"
+                     "kernel": ("ap2_soa_in + ap2_soa_shoot + ap2_soa_radau + ap2_soa_interval + ap2_finalize "
+                                "(one evaluation)"
                                 if soa else "ap2_node_kernel + ap2_gather_kernel" if gen else "ap2_interval_kernel"),
                      "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)), "bytes_per_eval": bytes_per_eval},
         "outputs_finite": finite,

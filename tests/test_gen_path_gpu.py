@@ -1,9 +1,11 @@
 """The evaluation paths of awe_eval_nlp on MI355X return the same f, g, grad f and J_g:
 
-* the instance-minor path (ap2_soa_node_kernel, one lane per instance, tangents stored straight into
-  J_g through the destination table; the default) agrees BITWISE with the node + gather path (the
-  same generated node code and the same interval arithmetic), in both J_g layouts -- per instance
-  (awe_eval_nlp) and instance-minor (awe_eval_nlp_im, the solver's layout);
+* the instance-minor path (ap2_soa_shoot / ap2_soa_radau kernels, one lane per instance, tangents
+  stored straight into J_g through the destination table; the default) agrees BITWISE with the
+  node + gather path in g and J_g (the same generated node code), in both J_g layouts -- per
+  instance (awe_eval_nlp) and instance-minor (awe_eval_nlp_im, the solver's layout) -- and to 1e-12
+  in f and grad f (its interval kernel sums the objective per lane, the gather kernel across a
+  wavefront);
 * the node + gather path agrees with the colour path (compressed forward mode) to rounding.
 
 At the bench's shape (B = 64, one full instance block), a ragged batch (B = 70: a partial block,
@@ -68,7 +70,11 @@ def test_instance_minor_path_is_default_and_matches_the_other_paths(B):
     for name in ("soa_im", "soa_aos"):
         for lab, a, b in zip(labels, out[name], out["generated"]):
             assert np.isfinite(a).all(), (name, lab)
-            assert np.array_equal(a, b), (name, lab, diffs[name])
+            if lab in ("g", "jac"):
+                assert np.array_equal(a, b), (name, lab, diffs[name])
+            else:                # the objective's sums run per lane instead of across a wavefront
+                for i in range(B):
+                    _close(a[i], b[i], rtol=1e-12)
     for a, b in zip(out["generated"], out["colour"]):
         for i in range(B):
             _close(a[i], b[i])
