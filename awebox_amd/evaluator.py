@@ -187,35 +187,46 @@ class Ap2Evaluator:
     # ---------------------------------------------- device path (torch CUDA tensors) ---
     def eval_nlp_device(self, V, P, f, g, grad_f, jac, stream=None):
         """f, g, grad f, J_g values for all batch members; fp64 CUDA tensors of shapes [B, n_v],
-        [B, n_p], [B], [B, n_g], [B, n_v] (contiguous) and jac [B, nnz]: contiguous (awe_eval_nlp),
-        or the instance-minor view ``jac_t.t()`` of a contiguous [nnz, ld] tensor with ld >= B
-        (awe_eval_nlp_im, the layout the batched solver reads; ``alloc_jac``)."""
+        [B, n_p], [B], [B, n_g] (contiguous), grad_f [B, n_v] and jac [B, nnz]: both contiguous
+        (awe_eval_nlp), or both instance-minor views ``x_t.t()`` of contiguous [n, ld] tensors with
+        one ld >= B (awe_eval_nlp_im, the layout the batched solver reads; ``alloc_grad`` /
+        ``alloc_jac``)."""
         import torch
-        for t, n in ((V, self.n_v), (P, self.n_p), (g, self.n_g), (grad_f, self.n_v)):
+        for t, n in ((V, self.n_v), (P, self.n_p), (g, self.n_g)):
             if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
                 raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
         if f.numel() != self.batch:
             raise ValueError("f must hold one value per batch member")
-        if jac.dtype != torch.float64 or not jac.is_cuda or tuple(jac.shape) != (self.batch, self.nnz):
-            raise ValueError("jac must be a float64 CUDA tensor of shape [batch, nnz]")
+        for t, n, name in ((jac, self.nnz, "jac"), (grad_f, self.n_v, "grad_f")):
+            if t.dtype != torch.float64 or not t.is_cuda or tuple(t.shape) != (self.batch, n):
+                raise ValueError(f"{name} must be a float64 CUDA tensor of shape [batch, {n}]")
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        if jac.is_contiguous():
+        im = lambda t: t.stride(0) == 1 and t.stride(1) >= self.batch   # noqa: E731
+        if self.batch == 1 or (jac.is_contiguous() and grad_f.is_contiguous()):
             self._check(self._lib.awe_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
                                                grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
-        elif jac.stride(0) == 1 and jac.stride(1) >= self.batch:
+        elif im(jac) and im(grad_f) and jac.stride(1) == grad_f.stride(1):
             self._check(self._lib.awe_eval_nlp_im(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(),
                                                   g.data_ptr(), grad_f.data_ptr(), jac.data_ptr(),
                                                   int(jac.stride(1)), ctypes.c_void_p(s)))
         else:
-            raise ValueError("jac must be contiguous or an instance-minor view (strides (1, ld))")
+            raise ValueError("jac and grad_f must both be contiguous or both instance-minor views "
+                             "(strides (1, ld), one ld)")
 
     def alloc_jac(self, device="cuda", instance_minor=True):
         """A J_g value tensor [B, nnz]; instance-minor (the transposed view of [nnz, B], which the
-        instance-minor kernel writes with coalesced stores) unless asked otherwise."""
+        instance-minor kernels write with coalesced stores) unless asked otherwise."""
         import torch
         if instance_minor:
             return torch.zeros(self.nnz, self.batch, dtype=torch.float64, device=device).t()
         return torch.zeros(self.batch, self.nnz, dtype=torch.float64, device=device)
+
+    def alloc_grad(self, device="cuda", instance_minor=True):
+        """A grad f tensor [B, n_v], instance-minor unless asked otherwise (pairs with alloc_jac)."""
+        import torch
+        if instance_minor:
+            return torch.zeros(self.n_v, self.batch, dtype=torch.float64, device=device).t()
+        return torch.zeros(self.batch, self.n_v, dtype=torch.float64, device=device)
 
     def last_kernel_ms_soa(self):
         """HIP-event times of the last instance-minor call: input transpose, node kernel, interval

@@ -171,7 +171,7 @@ class DeviceNlp:
         self.V = torch.tensor(np.tile(self.x_fix, (B, 1)), device=device)
         self.f = torch.zeros(B, **f64)
         self.g = torch.zeros(B, n_g, **f64)
-        self.grad = torch.zeros(B, n_v, **f64)
+        self.grad = ev.alloc_grad(device) if hasattr(ev, "alloc_grad") else torch.zeros(B, n_v, **f64)
         # J_g in the evaluator's instance-minor layout where it has one (the AP2 evaluator writes it
         # with coalesced stores, awe_eval_nlp_im); a [B, nnz] view either way
         self.jac = ev.alloc_jac(device) if hasattr(ev, "alloc_jac") else torch.zeros(B, ev.nnz, **f64)

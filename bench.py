@@ -195,23 +195,23 @@ def path_ab(ev, V, P, f, g, gr, B, dev, stream, reps=10):
     import numpy as np
     keep = ev.path
     out = {}
-    jac_aos = ev.alloc_jac(dev, instance_minor=False)
-    jac_im = ev.alloc_jac(dev, instance_minor=True)
-    for name, path, jac in (("soa_instance_minor", "soa", jac_im), ("soa_per_instance", "soa", jac_aos),
-                            ("generated", "generated", jac_aos), ("colour", "colour", jac_aos)):
+    jac_aos, gr_aos = ev.alloc_jac(dev, instance_minor=False), ev.alloc_grad(dev, instance_minor=False)
+    jac_im, gr_im = ev.alloc_jac(dev, instance_minor=True), ev.alloc_grad(dev, instance_minor=True)
+    for name, path, jac, grd in (("soa_instance_minor", "soa", jac_im, gr_im), ("soa_per_instance", "soa", jac_aos, gr_aos),
+                                 ("generated", "generated", jac_aos, gr_aos), ("colour", "colour", jac_aos, gr_aos)):
         try:
             ev.path = path
         except Exception:
             continue
         ms = []
         for _ in range(reps + 2):
-            ev.eval_nlp_device(V, P, f, g, gr, jac, stream=stream.cuda_stream)
+            ev.eval_nlp_device(V, P, f, g, grd, jac, stream=stream.cuda_stream)
             a, b_ = ev.last_kernel_ms()
             ms.append(a + b_)
         out[name] = float(np.mean(ms[2:]))
     ev.path = keep
     torch.cuda.synchronize()
-    del jac_aos, jac_im
+    del jac_aos, jac_im, gr_aos, gr_im
     return out
 
 
@@ -290,8 +290,8 @@ def main():
     P = torch.tensor(Ph, device=dev)
     f = torch.empty(B, dtype=torch.float64, device=dev)
     g = torch.empty(B, ev.n_g, dtype=torch.float64, device=dev)
-    gr = torch.empty(B, ev.n_v, dtype=torch.float64, device=dev)
-    # J_g in the layout the batched solver reads: instance-minor ([nnz, B] storage, [B, nnz] view)
+    # J_g and grad f in the layout the batched solver reads: instance-minor ([n, B] storage, [B, n] view)
+    gr = ev.alloc_grad(dev, instance_minor=True)
     jac = ev.alloc_jac(dev, instance_minor=True)
     stream = torch.cuda.current_stream(dev)
 

@@ -155,11 +155,12 @@ int awe_eval_hess_host(awe_handle h, const double* V, const double* P, const dou
 /* Kernel time of the last awe_eval_hess call (HIP events), milliseconds. */
 int awe_last_hess_ms(awe_handle h, float* ms);
 
-/* nlp_grad_f + nlp_jac_g fused, with J_g instance-minor: the value of CCS entry i of instance b at
- * jac[i * ldj + b] (ldj >= batch; V, P, g, grad_f and f as in awe_eval_nlp).  The layout the batched
- * solver consumes (a [batch, nnz] view with strides (1, ldj)); with batch = 1 and ldj = 1 it is
- * awe_eval_nlp's.  On the instance-minor path the node kernel writes it directly, on the other paths
- * the per-instance result is transposed. */
+/* nlp_grad_f + nlp_jac_g fused, with J_g and grad f instance-minor: the value of CCS entry i of
+ * instance b at jac[i * ldj + b], gradient entry i at grad_f[i * ldj + b] (ldj >= batch; V, P, g and f
+ * as in awe_eval_nlp).  The layout the batched solver consumes ([batch, nnz] and [batch, n_v] views
+ * with strides (1, ldj)); with batch = 1 and ldj = 1 it is awe_eval_nlp's.  On the instance-minor path
+ * the kernels write it directly (every store one contiguous run over 64 instances), on the other
+ * paths the per-instance result is transposed. */
 int awe_eval_nlp_im(awe_handle h, const double* V, const double* P, double* f, double* g,
                     double* grad_f, double* jac, int ldj, void* stream);
 

@@ -41,9 +41,10 @@ def _eval(ev, V, P, path, instance_minor):
     ev.path = path
     f = torch.empty(B, dtype=torch.float64, device="cuda")
     g = torch.empty(B, ev.n_g, dtype=torch.float64, device="cuda")
-    gr = torch.empty(B, ev.n_v, dtype=torch.float64, device="cuda")
+    gr = ev.alloc_grad("cuda", instance_minor=instance_minor)
     jac = ev.alloc_jac("cuda", instance_minor=instance_minor)
     jac.fill_(np.nan)
+    gr.fill_(np.nan)
     ev.eval_nlp_device(V, P, f, g, gr, jac)
     torch.cuda.synchronize()
     return [x.cpu().numpy() for x in (f, g, gr, jac)]

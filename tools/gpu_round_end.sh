@@ -17,5 +17,5 @@ step 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
 step 600 bench.log python bench.py
 step 300 rocprof_ap2.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ap2 -o run --output-format csv -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --sweep-points 0 --dual-sweep-points 0 --no-hessian --no-latency
 find gpurun_out/prof_ap2 -name '*_trace.csv' -size +4M -delete
-step 500 pmc_gen.log bash tools/gpu_pmc_gen.sh
+step 500 pmc_soa.log bash tools/gpu_pmc_soa.sh
 echo ROUND_END_DONE

@@ -26,7 +26,7 @@ def ap2(B=2048):
     ev = Ap2Evaluator(consts, batch=B)
     # J_g in the layout the bench and the solver use (instance-minor on the default path)
     out = [torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, ev.n_g, dtype=torch.float64, device=dev),
-           torch.empty(B, ev.n_v, dtype=torch.float64, device=dev), ev.alloc_jac(dev)]
+           ev.alloc_grad(dev), ev.alloc_jac(dev)]
     for _ in range(5):
         ev.eval_nlp_device(V, P, *out)
     torch.cuda.synchronize()

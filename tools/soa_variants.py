@@ -24,7 +24,7 @@ ev = E.Ap2Evaluator(consts, batch=B)
 assert ev._lib is lib, "variant library not in use"
 assert ev.path == "soa", ev.path
 f = torch.empty(B, dtype=torch.float64, device="cuda"); g = torch.empty(B, ev.n_g, dtype=torch.float64, device="cuda")
-gr = torch.empty(B, ev.n_v, dtype=torch.float64, device="cuda"); jac = ev.alloc_jac("cuda")
+gr = ev.alloc_grad("cuda"); jac = ev.alloc_jac("cuda")
 ks = []
 for i in range(25):
     ev.eval_nlp_device(V, P, f, g, gr, jac)
