@@ -8,8 +8,9 @@
   wavefront);
 * the node + gather path agrees with the colour path (compressed forward mode) to rounding.
 
-At the bench's shape (B = 64, one full instance block), a ragged batch (B = 70: a partial block,
-lanes past the batch idle) and B = 1 (the solver's single-instance calls).  Oracle parity of the
+At B = 128 (two full instance blocks; the instance-minor path is the default from here on), a
+ragged batch (B = 70: a partial block, lanes past the batch idle) and B = 1 (the solver's
+single-instance calls, where the colour path is the default).  Oracle parity of the
 default path is tests/test_gpu_parity.py."""
 import numpy as np
 import pytest
@@ -50,12 +51,12 @@ def _eval(ev, V, P, path, instance_minor):
     return [x.cpu().numpy() for x in (f, g, gr, jac)]
 
 
-@pytest.mark.parametrize("B", [64, 70, 1])
+@pytest.mark.parametrize("B", [128, 70, 1])
 def test_instance_minor_path_is_default_and_matches_the_other_paths(B):
     from awebox_amd import evaluator as E
     consts, V, P = _inputs(B)
     ev = E.Ap2Evaluator(consts, batch=B)
-    assert ev.path == "soa"
+    assert ev.path == ("soa" if B >= 128 else "colour")   # the default follows the batch size
     out = {"soa_im": _eval(ev, V, P, "soa", True)}
     ms = ev.last_kernel_ms_soa()
     assert ms[1] > 0 and ms[2] > 0 and ms[4] < 0.05          # no output transpose in the solver's layout
@@ -79,4 +80,3 @@ def test_instance_minor_path_is_default_and_matches_the_other_paths(B):
     for a, b in zip(out["generated"], out["colour"]):
         for i in range(B):
             _close(a[i], b[i])
-    ev.path = "soa"

@@ -70,13 +70,19 @@ def _oracle_all(orc, lay, V, P):
     return f, g, grad, J
 
 
-@pytest.mark.parametrize("n_k,d,member", [(40, 4, None), (40, 4, 0), (40, 4, 7), (5, 3, 1), (3, 2, 2)])
-def test_nlp_eval_matches_oracle(gpu, n_k, d, member):
+@pytest.mark.parametrize("n_k,d,member,path", [(40, 4, None, None), (40, 4, 0, None), (40, 4, 7, None),
+                                                (5, 3, 1, None), (3, 2, 2, None), (40, 4, 7, "soa"),
+                                                (5, 3, 1, "soa"), (3, 2, 2, "soa"), (40, 4, 7, "generated")])
+def test_nlp_eval_matches_oracle(gpu, n_k, d, member, path):
+    """One instance on the default path (the colour kernel at batch 1) and on the instance-minor and
+    node + gather paths."""
     from awebox_amd.evaluator import Ap2Evaluator
     consts, lay, v0, orc = _setup(n_k, d)
     V = v0 if member is None else batch_member(v0, lay, member)
     P = pb.pack_p(lay, consts, v0)
     ev = Ap2Evaluator(consts, batch=1)
+    if path is not None:
+        ev.path = path
     out = ev.eval_nlp(V, P)
     f, g, grad, J = _oracle_all(orc, lay, V, P)
     _close(out["g"][0], g, "g")
@@ -85,17 +91,23 @@ def test_nlp_eval_matches_oracle(gpu, n_k, d, member):
     _close_jac(ev.jac_csc(out["jac"][0]), J)
 
 
-def test_batched_sweep_members_match_oracle(gpu):
-    """8 instances per launch with different V and different u_ref (the sweep parameter)."""
+@pytest.mark.parametrize("B,path,members", [(8, None, (0, 3, 7)), (130, None, (0, 77, 129)),
+                                             (8, "generated", (0, 7))])
+def test_batched_sweep_members_match_oracle(gpu, B, path, members):
+    """B instances per launch with different V and different u_ref (the sweep parameter): 8 on the
+    default (colour) path and on the node + gather path, 130 on the default instance-minor path
+    (two full blocks of 64 instances and a partial one)."""
     from awebox_amd.evaluator import Ap2Evaluator
     consts, lay, v0, orc = _setup()
-    B = 8
     u_refs = np.linspace(5, 8, B)                      # dual_kites_power_curve sweep range
     Vs = np.stack([batch_member(v0, lay, b) for b in range(B)])
     Ps = np.stack([pb.pack_p(lay, consts, v0, u_ref=u) for u in u_refs])
     ev = Ap2Evaluator(consts, batch=B)
+    assert ev.path == ("soa" if B >= 128 else "colour")
+    if path is not None:
+        ev.path = path
     out = ev.eval_nlp(Vs, Ps)
-    for b in (0, 3, 7):
+    for b in members:
         f, g, grad, J = _oracle_all(orc, lay, Vs[b], Ps[b])
         _close(out["g"][b], g, f"g[{b}]")
         assert out["f"][b] == pytest.approx(f, rel=1e-12)
