@@ -148,6 +148,27 @@ def gen_kernels(ev, lay, B, node_ms, gather_ms):
                                   "note": "nodebuf run read + J_g and gradient written per evaluation"}}
 
 
+def measured_limiter(rec, hbm_frac, fp64_frac):
+    """What the PMC record says limits the evaluation: per kernel the share of wave cycles spent
+    waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and the share with a VALU instruction issuing, against
+    the HBM and FP64 fractions -- latency-bound when waves mostly wait while neither HBM nor FP64 is
+    near its peak."""
+    per = {}
+    for name, k in (rec.get("kernels") or {"evaluation": rec}).items():
+        cyc = k.get("SQ_WAVE_CYCLES")
+        if not cyc:
+            continue
+        per[name] = {"wait_frac": k.get("SQ_WAIT_ANY", 0.0) / cyc,
+                     "valu_active_frac": k.get("SQ_ACTIVE_INST_VALU", 0.0) / cyc}
+    if not per:
+        return None
+    wait = max(v["wait_frac"] for v in per.values())
+    fp = fp64_frac if fp64_frac is not None else 0.0
+    bound = ("latency (waves waiting on memory / LDS while HBM is at {:.0%} and FP64 at {:.0%} of peak)".format(
+        hbm_frac, fp) if wait > 0.5 and hbm_frac < 0.6 and fp < 0.6 else "hbm" if hbm_frac >= fp else "fp64")
+    return {"bound": bound, "kernels": per}
+
+
 def soa_kernels(ev, lay, B, ms):
     """Per-kernel view of the instance-minor path (HIP events per kernel, mean over the timed
     launches): algorithmic bytes of each kernel against HBM peak, and the node kernels' generated
@@ -430,12 +451,9 @@ def main():
                 fp64["issued_over_algorithmic"] = flops / (fp64["algorithmic"]["flops_per_eval"] * B)
     if fp64:
         line["fp64"] = fp64
-        if "issued" in fp64 and rec is not None:
-            wait = rec.get("SQ_WAIT_ANY", 0.0) / max(rec.get("SQ_WAVE_CYCLES", 1.0), 1.0)
-            line["roofline"]["measured_limiter"] = (
-                f"fp64 VALU issue + latency (issued FP64 {fp64['issued']['frac']:.1%} of peak, SQ_WAIT_ANY "
-                f"{wait:.0%} of wave cycles); HBM at {line['roofline']['frac']:.1%}"
-                if fp64["issued"]["frac"] > line["roofline"]["frac"] else "hbm")
+    if rec is not None:
+        line["roofline"]["measured_limiter"] = measured_limiter(rec, line["roofline"]["frac"],
+                                                                fp64.get("issued", {}).get("frac"))
     if dual is not None:
         line["dual"] = dual
     if mpc is not None:

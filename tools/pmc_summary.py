@@ -95,8 +95,38 @@ def record_gen(batch, dirs):
     print("wrote profiles/pmc_traffic.json", json.dumps({k: v for k, v in tot.items()}))
 
 
+SOA_KERNELS = ("ap2_soa_in_kernel", "ap2_soa_shoot_kernel", "ap2_soa_radau_kernel", "ap2_soa_interval_kernel",
+               "ap2_finalize_kernel")
+
+
+def record_soa(batch, dirs):
+    """profiles/pmc_traffic.json for the instance-minor evaluation path: counters per dispatch of each
+    of its kernels (tools/gpu_pmc_soa.sh) and their sum over one evaluation at the top level, which
+    bench.py reads (FETCH_SIZE x 2 + WRITE_SIZE = HBM bytes per evaluation, the gfx950 correction)."""
+    sys.path.insert(0, ROOT)
+    from bench import kernel_source_hash
+    paths = [p for d in dirs for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)]
+    rec = {"batch": batch, "source_hash": kernel_source_hash(), "path": "soa",
+           "kernel": " + ".join(SOA_KERNELS), "kernels": {},
+           "units": "FETCH/WRITE_SIZE in kB per dispatch; SQ_* per dispatch; mean over 5 dispatches "
+                    "(tools/pmc_kernels.py --ap2, tools/gpu_pmc_soa.sh)"}
+    tot = defaultdict(float)
+    for kern in SOA_KERNELS:
+        summ = summarise(paths, kern)
+        rec["kernels"][kern] = {k + ("_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else ""): v for k, v in summ.items()}
+        for k, v in summ.items():
+            tot[k + ("_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else "")] += v
+    rec.update(tot)
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
+        json.dump(rec, fh, indent=1, sort_keys=True)
+    print("wrote profiles/pmc_traffic.json", json.dumps({k: v for k, v in tot.items()}))
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
+    if args and args[0] == "--record-soa":
+        record_soa(int(args[1]), args[2:])
+        sys.exit(0)
     if args and args[0] == "--record-gen":
         record_gen(int(args[1]), args[2:])
         sys.exit(0)
