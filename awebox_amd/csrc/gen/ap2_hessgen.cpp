@@ -86,6 +86,7 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::Ap2HessTab
     const int n1 = (int)tape.n.size();
     std::vector<awe::SparseGrad> G2 = awe::forward_grads(tape, n1, seed);
     std::vector<awe::Store> stores;
+    std::vector<int> first_dir;
     KindOut ko;
     for (const auto& pe : g1) {
         const int p = pe.first;
@@ -99,10 +100,36 @@ KindOut generate(int kind, const std::vector<double>& cst, const awt::Ap2HessTab
             }
             awe::Store s{qe.second, 3, pidx, -1};   // obv[row] = ... : hd[pidx]
             stores.push_back(s);
+            first_dir.push_back(p);
             ko.n_pairs++;
         }
     }
-    ko.body = awe::emit(tape, stores, ko.st, true);
+    // direction strips: the pairs grouped by their first direction into n_strips balanced groups,
+    // each emitted as its own scope that recomputes the values it needs (opaque leaf copies)
+    const char* ns = std::getenv("AWE_HESS_STRIPS");
+    const int n_strips = ns ? std::atoi(ns) : 1;
+    std::vector<int> per_dir(awt::kDirs, 0);
+    for (int p : first_dir) per_dir[p]++;
+    std::vector<int> strip_of(awt::kDirs, 0);
+    {
+        int acc = 0;
+        for (int d = 0; d < awt::kDirs; ++d) {
+            strip_of[d] = std::min(n_strips - 1, (int)((long long)acc * n_strips / std::max(1, ko.n_pairs)));
+            acc += per_dir[d];
+        }
+    }
+    for (int sidx = 0; sidx < n_strips; ++sidx) {
+        std::vector<awe::Store> part;
+        for (size_t i = 0; i < stores.size(); ++i)
+            if (strip_of[first_dir[i]] == sidx) part.push_back(stores[i]);
+        if (part.empty()) continue;
+        awe::EmitStats st;
+        std::string body = awe::emit(tape, part, st, true, 32, sidx > 0, 0);
+        ko.body += "    {   // strip " + std::to_string(sidx) + "\n" + body + "    }\n";
+        ko.st.ops += st.ops; ko.st.flops += st.flops; ko.st.transcendental += st.transcendental;
+        ko.st.max_live = std::max(ko.st.max_live, st.max_live);
+        std::fprintf(stderr, "kind %d strip %d: %zu pairs, %d ops, max_live %d\n", kind, sidx, part.size(), st.ops, st.max_live);
+    }
     awe::active_tape() = nullptr;
     return ko;
 }
