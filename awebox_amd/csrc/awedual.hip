@@ -236,16 +236,37 @@ __device__ __forceinline__ FrontGeo dual_front(const DArgs& a, FrontLds<D>& s, d
     const int nthv = a.n_thv;
     const int base = a.v_int0 + k * STRIDE;
     // ---- stage -------------------------------------------------------------------------
-    for (int i = tid; i < NLOC; i += NT) {
-        double v = 0.0;
-        if (i < ADL_NTHV) v = i < nthv ? V[i] : 0.0;
-        else if (i < ADL_NTHV + 7) v = V[nthv + (i - ADL_NTHV)];
-        else v = V[base + (i - ADL_NTHV - 7)];
-        vloc[i] = v;
+    // every load of a thread's share issued before its LDS stores, unconditionally (a guarded load
+    // per element is a branch, and the compiler then waits for each load before the next)
+    {
+        constexpr int NR = ADL_NTHV + STRIDE;
+        constexpr int U = (NLOC + NR + NT - 1) / NT;
+        double r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = tid + u * NT;
+            const double* src;
+            if (i < NLOC) {
+                src = i < ADL_NTHV ? V + (i < nthv ? i : 0)
+                    : i < ADL_NTHV + 7 ? V + nthv + (i - ADL_NTHV) : V + base + (i - ADL_NTHV - 7);
+            } else {
+                const int q = i < NLOC + NR ? i - NLOC : 0;
+                src = q < ADL_NTHV ? P + (q < nthv ? q : 0) : P + base + (q - ADL_NTHV);
+            }
+            r[u] = *src;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = tid + u * NT;
+            if (i < NLOC) vloc[i] = (i < ADL_NTHV && i >= nthv) ? 0.0 : r[u];
+            else if (i < NLOC + NR) {
+                const int q = i - NLOC;
+                rloc[q] = (q < ADL_NTHV && q >= nthv) ? 0.0 : r[u];
+            }
+        }
     }
-    for (int i = tid; i < ADL_NTHV + STRIDE; i += NT)
-        rloc[i] = i < ADL_NTHV ? (i < nthv ? P[i] : 0.0) : P[base + (i - ADL_NTHV)];
     for (int i = tid; i < 256; i += NT) colb[i >> 7][i & 127] = a.ct->col[i >> 7][i & 127];
+    __syncthreads();                                    // psi below reads the staged image
     const double* wts = P + a.n_v;
     const double* cost = P + a.n_v + ADL_NW;
     const double* th = P + a.n_v + ADL_NW + 20;
@@ -536,17 +557,30 @@ __global__ __launch_bounds__(kBlock, ADL_MIN_BLOCKS) void dual_interval_kernel(D
     }
 
     // ---- J_g values through the gather list -------------------------------------------------
+    // (the entries' codes and slots are fetched 8 per thread at a time before the stores: a loop that
+    // loads them per entry waits for each pair of loads behind the previous entry's store)
     double* jac = a.jac + (size_t)b * a.nnz;
     const int e0 = a.goff[k], e1 = a.goff[k + 1];
-    for (int e = e0 + tid; e < e1; e += NT) {
-        const uint32_t cd = a.gcode[e];
-        const uint32_t kind = cd >> 29;
-        const int rr = (cd >> 25) & 15, n = (cd >> 21) & 15, idx = cd & ((1u << 21) - 1u);
-        double val;
-        if (kind == kKindTang) val = tang[idx];
-        else if (kind == kKindTangPoly) val = tang[idx] * (C[rr * NN + n] * ihtf);
-        else val = a.kconst[idx];
-        jac[a.gslot[e]] = val;
+    for (int eb = e0 + tid; eb < e1; eb += 8 * NT) {
+        uint32_t cd[8];
+        int sl[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = min(eb + u * NT, e1 - 1);
+            cd[u] = a.gcode[e];
+            sl[u] = a.gslot[e];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (eb + u * NT >= e1) break;
+            const uint32_t kind = cd[u] >> 29;
+            const int rr = (cd[u] >> 25) & 15, n = (cd[u] >> 21) & 15, idx = cd[u] & ((1u << 21) - 1u);
+            double val;
+            if (kind == kKindTang) val = tang[idx];
+            else if (kind == kKindTangPoly) val = tang[idx] * (C[rr * NN + n] * ihtf);
+            else val = a.kconst[idx];
+            jac[sl[u]] = val;
+        }
     }
 }
 

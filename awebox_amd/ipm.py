@@ -828,10 +828,18 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         e = torch.stack(parts).cpu().numpy()
         return tuple(e)
 
-    def ftb(v, dv, mask_pos, tau_t):
-        """Fraction-to-the-boundary step per instance: min(1, min_i -tau v_i / dv_i) (host [B])."""
+    def ftb_dev(v, dv, mask_pos, tau_t):
+        """Fraction-to-the-boundary step per instance on the device: min_i -tau v_i / dv_i ([B])."""
         ratio = torch.where(mask_pos & (dv < 0), -tau_t[:, None] * v / dv, torch.full_like(v, math.inf))
-        return np.minimum(1.0, ratio.amin(1).cpu().numpy()) if ratio.shape[1] else np.ones(B)
+        return ratio.amin(1) if ratio.shape[1] else torch.full((B,), math.inf, **f64)
+
+    def ftb2(vl, dvl, vu, dvu, tau_t, extra=None):
+        """min(1, step to the lower bounds, step to the upper bounds) per instance (host [B]), in one
+        device-to-host copy together with the rows of ``extra`` (returned after the step)."""
+        rows = [ftb_dev(vl, dvl, hl, tau_t), ftb_dev(vu, dvu, hu, tau_t)] + (extra or [])
+        h = torch.stack(rows).cpu().numpy()
+        a = np.minimum(1.0, np.minimum(h[0], h[1]))
+        return (a, *h[2:]) if extra else a
 
     def filter_ok(b, theta_t, phi_t):
         return all(not (theta_t >= th_f and phi_t >= ph_f) for th_f, ph_f in filt[b])
@@ -914,8 +922,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     # ---- the filter line search with second-order corrections (all instances in `want`) ---------
     def line_search(want, dy, dlam, rhs_top, c_cur, dl, du, theta, phi, grad_phi, tau_t, mu_t):
         """Per instance in `want`: (accepted, alpha, y_trial, dy_used, dlam_used, backtracks, socs)."""
-        alpha = np.minimum(ftb(dl, dy, hl, tau_t), ftb(du, -dy, hu, tau_t))
-        gphi_d = (grad_phi * dy).sum(1).cpu().numpy()
+        alpha, gphi_d = ftb2(dl, dy, du, -dy, tau_t, extra=[(grad_phi * dy).sum(1)])
         alpha_min = opts.alpha_min_frac * np.where(
             gphi_d < 0, np.minimum(opts.gamma_theta, opts.gamma_phi * theta / np.maximum(-gphi_d, 1e-300)),
             opts.gamma_theta)
@@ -1003,7 +1010,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 sel = dev_b(upd)[:, None] > 0
                 dys = torch.where(sel, sol[:, :ny], dys)
                 dlam_s = torch.where(sel, sol[:, ny:], dlam_s)
-                a_new = np.minimum(ftb(dl, dys, hl, tau_t), ftb(du, -dys, hu, tau_t))
+                a_new = ftb2(dl, dys, du, -dys, tau_t)
                 a_s = np.where(upd, a_new, a_s)
                 in_soc |= upd
                 # a non-finite correction: plain backtracking
@@ -1044,7 +1051,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             fin = torch.isfinite(sol).all(1).cpu().numpy()
             live &= fin
             dyv = torch.where(torch.isfinite(sol[:, :ny]), sol[:, :ny], torch.zeros_like(sol[:, :ny]))
-            a = np.minimum(ftb(dlv, dyv, hl, dev_b(tau)), ftb(duv, -dyv, hu, dev_b(tau)))
+            a = ftb2(dlv, dyv, duv, -dyv, dev_b(tau))
             searching = live.copy()
             a_acc = np.zeros(B)
             for _bt in range(30):
@@ -1113,8 +1120,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
         grad_phi = grad_y(grad) - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
             torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y)) + opts.kappa_d * mu_d[:, None] * damp_dir
-        theta = c.abs().sum(1).cpu().numpy()
-        phi = barrier_phi(f, y, mu_d).cpu().numpy()
+        theta, phi = torch.stack([c.abs().sum(1), barrier_phi(f, y, mu_d)]).cpu().numpy()
         rhs_top = -(grad_phi + A_T_lam(jv, lam))
         rhs = torch.cat([rhs_top, -c], 1)
         pending = active.copy()
@@ -1164,7 +1170,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             sel = dev_b(acc_all)[:, None] > 0
             dzl = torch.where(hl, mu_d[:, None] / dl - zl - zl / dl * dy_new, torch.zeros_like(y))
             dzu = torch.where(hu, mu_d[:, None] / du - zu + zu / du * dy_new, torch.zeros_like(y))
-            alpha_z = np.minimum(ftb(zl, dzl, hl, tau_d), ftb(zu, dzu, hu, tau_d))
+            alpha_z = ftb2(zl, dzl, zu, dzu, tau_d)
             az = dev_b(np.where(acc_all, alpha_z, 0.0))[:, None]
             y = torch.where(sel, y_new, y)
             lam = lam + dev_b(np.where(acc_all, alpha_acc, 0.0))[:, None] * dlam_new
