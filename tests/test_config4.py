@@ -75,12 +75,14 @@ def test_config4_shard_at_stated_shape_fan_vs_chain(gpu):
     assert np.allclose(fan["period_s"], chain["period_s"], rtol=1e-2)
 
 
-def test_config4_hardest_shard_converges_with_rising_power(gpu):
+def test_config4_far_shard_converges_with_rising_power(gpu):
     """Rank 7's shard of config 4 -- points 56..63 of linspace(5, 8, 64), u_ref 7.62..8.0 m/s, the
-    far end of the power curve from the homotopy's standard initial guess -- at the example's N=20
-    d=4 in fan mode: the homotopy of the shard's first point and the batched warm start of the
-    other seven converge, and the power rises with u_ref (profiles/r04/config4_full.jsonl holds all
-    eight shards)."""
+    far end of the power curve from the homotopy's standard initial guess, every optimum on the
+    t_f bound -- at the example's N=20 d=4 in fan mode: the homotopy of the shard's first point and
+    the batched warm start of the other seven converge, and the power rises with u_ref (49 s on
+    MI355X). The shard with the most iterations, shard 6 (896 in its homotopy, 142 s), exceeds a
+    test's time limit; it runs with the other seven in tools/config4_full.py
+    (profiles/r04/config4/config4_full.jsonl)."""
     u = np.linspace(5.0, 8.0, 64)[56:64]
     res = _sweep(u, n_k=20, mode="fan")
     print("shard 7", res["avg_power_W"], res["period_s"], res["iterations"], res["wall_s"])
