@@ -30,6 +30,7 @@ What is left out: IPOPT's full restoration-phase NLP, the watchdog, and quasi-Ne
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -291,6 +292,10 @@ def _dense_A(nlp, jv, N0, K):
     K[scol, srow] = -1.0
 
 
+# interval blocks up to which the inertia pass runs beside the factorisation (StructuredKKT.factor):
+# above it the LU kernel alone fills the GPU and the overlap only adds contention
+EARLY_INERTIA_MAX_BLOCKS = int(os.environ.get("AWE_EARLY_INERTIA_MAX_BLOCKS", "512"))
+
 ZERO_PIVOT = 1e-30   # relative zero-pivot threshold of the inertia count: KKT pivots legitimately span
                      # 1e-10 .. 1e10 at small mu, so only exactly singular columns count as zero
 
@@ -427,12 +432,20 @@ class StructuredKKT:
                 self.btd = None                                 # not stage-structured: dense S
         self.int_flat = torch.tensor(owner[int_p] * nI + loc[int_p], device=dev)
         self.sep_p = torch.tensor(sep, device=dev)
+        self._cI = None                                         # interval-block counts in flight (factor)
 
     # ---------------------------------------------------------------------------------------
-    def factor(self, hv, diag, jv, delta_c, mI):
+    def factor(self, hv, diag, jv, delta_c, mI, early_inertia=False):
         """Factorise K for every instance: hv [B, nH] Hessian values, diag [B, ny] (Sigma +
-        delta_w), jv [B, nJ] Jacobian values, delta_c float or [B] (1-D inputs: one instance)."""
+        delta_w), jv [B, nJ] Jacobian values, delta_c float or [B] (1-D inputs: one instance).
+
+        ``early_inertia`` (the caller will ask for inertia()): the Bunch-Kaufman counts of the
+        interval blocks start on a side stream as soon as the blocks are assembled and run beside
+        their LU, the Schur complement and the separator sweep -- with few instances each of those
+        kernels fills a few dozen of the 256 CUs, and the inertia pass (one workgroup per block,
+        ~2.3 ms at AP2 N=40 B=1) was the largest single kernel of the sweep's homotopy."""
         f64 = dict(dtype=torch.float64, device=self.dev)
+        self._cI = None
         self.squeeze = hv.dim() == 1
         hv, diag, jv = (t.unsqueeze(0) if t.dim() == 1 else t for t in (hv, diag, jv))
         B = hv.shape[0]
@@ -448,6 +461,8 @@ class StructuredKKT:
         KII[:, self.pad_flat] = 1.0
         KII = KII.view(B * n_k, nI, nI)
         self.KII = KII
+        if early_inertia and KII.is_cuda and B * n_k <= EARLY_INERTIA_MAX_BLOCKS:
+            self._interval_inertia_async(KII)
         KIS = self.sc[1].add_into(torch.zeros(B, n_k * nI * L, **f64), vals[:, self.sel_is]).view(B * n_k, nI, L)
         self.awelu = self.lu_backend == "awelu" and KII.is_cuda   # the CPU test harness uses LAPACK
         if self.awelu:
@@ -473,6 +488,34 @@ class StructuredKKT:
         self.S = S
         self.LU_S, self.piv_S = torch.linalg.lu_factor(S)
 
+    def _interval_inertia_async(self, KII):
+        from .batched_lu import sym_inertia
+        side = getattr(self, "_side", None)
+        if side is None:
+            side = self._side = torch.cuda.Stream(device=KII.device)
+        main = torch.cuda.current_stream(KII.device)
+        side.wait_stream(main)                          # KII assembled
+        with torch.cuda.stream(side):
+            self._cI = sym_inertia(KII, ztol=ZERO_PIVOT)
+        KII.record_stream(side)                         # not reused before the side stream is done
+        self._cI_done = torch.cuda.Event()
+        self._cI_done.record(side)
+
+    def _interval_inertia(self):
+        """[B, 3] counts of the interval blocks (padding rows excluded)."""
+        from .batched_lu import sym_inertia, sym_inertia_host
+        if self._cI is not None:
+            main = torch.cuda.current_stream(self.KII.device)
+            main.wait_event(self._cI_done)
+            cI = self._cI
+            cI.record_stream(main)
+        else:
+            f = sym_inertia if self.KII.is_cuda else sym_inertia_host
+            cI = f(self.KII, ztol=ZERO_PIVOT)
+        c = cI.to(torch.int64).view(self.B, self.n_k, 3).sum(1)
+        c[:, 0] -= self.n_pad
+        return c
+
     def inertia(self):
         """(positive, negative, zero) eigenvalue counts of K per instance, int64 [B, 3] (a tuple for
         a one-instance factor()), by Haynsworth's additivity In(K) = sum_k In(K_II^k) + In(S):
@@ -481,9 +524,7 @@ class StructuredKKT:
         pivot blocks and the border (btd.BorderedBtd)."""
         from .batched_lu import sym_inertia, sym_inertia_host
         f = sym_inertia if self.KII.is_cuda else sym_inertia_host
-        B = self.B
-        c = f(self.KII, ztol=ZERO_PIVOT).to(torch.int64).view(B, self.n_k, 3).sum(1)
-        c[:, 0] -= self.n_pad
+        c = self._interval_inertia()
         if self.use_btd:
             c = c + self.btd.inertia()
         else:
@@ -865,7 +906,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         dw_used = np.zeros(B)
         for attempt in range(60):
             with _Phase("kkt_factor"):
-                skkt.factor(hv, sigma + dev_b(delta_w)[:, None], jv, dev_b(delta_c), mI)
+                skkt.factor(hv, sigma + dev_b(delta_w)[:, None], jv, dev_b(delta_c), mI, early_inertia=exact_inertia)
             grow = ~done.copy()
             if exact_inertia:
                 with _Phase("inertia"):
