@@ -26,6 +26,8 @@ def load_library(path: str = _PATH):
         lib.awelu_btd_solve_batched.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p] * 4
         lib.awelu_sym_inertia_batched.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_double,
                                                   ctypes.c_void_p, ctypes.c_void_p]
+        lib.awelu_gather_sum.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_longlong] + \
+            [ctypes.c_void_p] * 2 + [ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
         lib.awelu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
@@ -119,6 +121,25 @@ def btd_dense(T):
             if 0 <= k + dk < nb:
                 A[:, k * m:(k + 1) * m, (k + dk) * m:(k + dk + 1) * m] = T[:, k, s_]
     return A
+
+
+def gather_sum(lsrc, lw, ldst, vals, out, rows, x=None, cols=None):
+    """out[r][ldst] += the lane lists' sums of vals[r][lsrc] (times x[r][cols[lsrc]] with x), for
+    r < rows: ipm._ScatterSum's fixed-order sums in one launch (awelu_gather_sum).  All device
+    tensors: lsrc / ldst int32, lw uint8 (one entry per lane), vals / out / x float64 contiguous
+    with ``rows`` leading rows, cols int32."""
+    import torch
+    L = lsrc.numel()
+    if L == 0 or rows == 0:
+        return out
+    lib = load_library()
+    s = torch.cuda.current_stream(out.device).cuda_stream
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+    rc = lib.awelu_gather_sum(L, rows, ptr(lsrc), ptr(lw), ptr(ldst), ptr(vals), vals.shape[-1], ptr(x), ptr(cols),
+                              x.shape[-1] if x is not None else 0, ptr(out), out.shape[-1], ctypes.c_void_p(s))
+    if rc != 0:
+        raise RuntimeError(f"awelu_gather_sum: {lib.awelu_last_error().decode()}")
+    return out
 
 
 def sym_inertia(A, ztol=1e-13):

@@ -1011,6 +1011,41 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_kernel(int n, int nb, do
 
 }  // namespace
 
+// Fixed-order gather-sums of ipm._ScatterSum (the KKT assembly, the KKT and Jacobian products):
+// out[r][dst[u]] += sum over the source list of destination u of v(r, s), v = vals[r][s] or
+// vals[r][s] * x[r][cols[s]].  The lists are padded to a power-of-two width w <= 64 and laid out
+// in lanes, each list on w consecutive lanes aligned to w (widest first), so one butterfly of
+// shuffles with offsets 1, 2, .., w / 2 adds every list as the adjacent-pair tree
+// ((v0 + v1) + (v2 + v3)) + ..: the order torch's sum over a row of <= 64 float64 entries uses on
+// this GPU (tools/torch_sum_order_probe.py), so this one launch returns bitwise what the gather /
+// sum / index-put chain it replaces returned (tests/test_gather_sum_gpu.py).  No contraction: the
+// product and the sums round as the separate torch operations did.
+__global__ __launch_bounds__(256) void gather_sum_kernel(int L, const int* __restrict__ lsrc,
+                                                         const unsigned char* __restrict__ lw,
+                                                         const int* __restrict__ ldst, const double* __restrict__ vals,
+                                                         long long ldv, const double* __restrict__ x,
+                                                         const int* __restrict__ cols, long long ldx,
+                                                         double* __restrict__ out, long long ldo) {
+#pragma clang fp contract(off)
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    const long long r = blockIdx.y;
+    const int li = l < L ? l : L - 1;                         // every lane takes part in the shuffles
+    const int s = lsrc[li];
+    const int w = lw[li];
+    double v = 0.0;
+    if (l < L && s >= 0) {
+        v = vals[r * ldv + s];
+        if (x) v = v * x[r * ldx + cols[s]];
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_xor(v, o);
+        if (o < w) v = v + u;
+    }
+    const int d = ldst[li];
+    if (l < L && d >= 0) out[r * ldo + d] = out[r * ldo + d] + v;
+}
+
 extern "C" {
 
 const char* awelu_last_error(void) { return g_err.c_str(); }
@@ -1126,6 +1161,26 @@ int awelu_sym_inertia_batched(int n, int batch, double* A, double ztol, int* cou
     else
         sym_inertia_kernel<<<dim3((unsigned)batch), kThreads, sizeof(double) * (size_t)nb * n, (hipStream_t)stream>>>(
             n, nb, A, ztol, counts);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// Gather-sums for `rows` rows (see gather_sum_kernel): L lanes of (source, width, destination);
+// x and cols NULL for plain sums.  Asynchronous on `stream`.
+int awelu_gather_sum(int L, int rows, const int* lsrc, const unsigned char* lw, const int* ldst, const double* vals,
+                     long long ldv, const double* x, const int* cols, long long ldx, double* out, long long ldo,
+                     void* stream) {
+    if (L < 0 || rows < 0 || rows > 65535 || (L > 0 && (!lsrc || !lw || !ldst || !vals || !out)) || (x && !cols)) {
+        g_err = "need L >= 0, 0 <= rows <= 65535 and device pointers (cols with x)";
+        return 1;
+    }
+    if (L == 0 || rows == 0) return 0;
+    gather_sum_kernel<<<dim3((unsigned)((L + 255) / 256), (unsigned)rows), 256, 0, (hipStream_t)stream>>>(
+        L, lsrc, lw, ldst, vals, ldv, x, cols, ldx, out, ldo);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

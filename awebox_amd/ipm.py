@@ -217,17 +217,27 @@ class DeviceNlp:
 class _ScatterSum:
     """out[..., dst[i]] += vals[..., i] for a fixed index pattern, deterministically and without
     atomics: the duplicates of every destination are pre-grouped on the host into gather tables
-    (one per power-of-two bucket of the multiplicity, padding -> a zero slot), so a few gathers,
-    row sums and plain indexed stores replace index_put_(accumulate=True) / index_add_, whose
+    (one per power-of-two bucket of the multiplicity, padding -> a zero slot), and each table row is
+    summed as one fixed-order reduction instead of index_put_(accumulate=True) / index_add_, whose
     atomics add duplicates in a run-dependent order (the homotopy path is
-    sensitive to that roundoff).  Leading (batch) dimensions of ``out`` and ``vals`` are kept."""
+    sensitive to that roundoff).  Leading (batch) dimensions of ``out`` and ``vals`` are kept.
+
+    On the GPU every bucket up to width 64 goes through one launch of libawelu's gather-sum
+    kernel (awelu_gather_sum: lists in lanes, adjacent-pair shuffle trees -- bitwise the gather,
+    row sum and indexed add that torch performs per bucket, ~5 launches each); wider buckets (the
+    few long rows, e.g. t_f's column of J) keep the torch reduction, whose order over more than 64
+    entries the kernel does not reproduce."""
+
+    NATIVE_MAX_W = 64
 
     def __init__(self, dst, dev):
         dst = np.asarray(dst, dtype=np.int64).reshape(-1)
         self.n_src = len(dst)
+        self.dev = torch.device(dev)
         order = np.argsort(dst, kind="stable")
         uniq, start, count = np.unique(dst[order], return_index=True, return_counts=True)
-        self.buckets = []
+        self.buckets = []                                       # (dst, table) on the device, all widths
+        narrow = []                                             # host tables of width <= 64
         lo, width = 0, 1
         while lo < (count.max() if len(count) else 0):
             sel = np.where((count > lo) & (count <= width))[0]
@@ -237,12 +247,89 @@ class _ScatterSum:
                     has = count[sel] > w
                     table[has, w] = order[start[sel][has] + w]
                 self.buckets.append((torch.tensor(uniq[sel], device=dev), torch.tensor(table, device=dev)))
+                if width <= self.NATIVE_MAX_W:
+                    narrow.append((uniq[sel], table))
             lo, width = width, 2 * width
+        self.wide = [(d, t) for d, t in self.buckets if t.shape[1] > self.NATIVE_MAX_W]
+        # AWE_NATIVE_GATHER_SUM=0: the torch reduction everywhere (A/B measurements)
+        self.native = self.dev.type == "cuda" and os.environ.get("AWE_NATIVE_GATHER_SUM", "1") != "0"
+        self._sel_lanes = {}
+        self.lanes_host = self.build_lanes(narrow, len(dst))
+        if self.native:
+            lsrc, lw, ldst = self.lanes_host
+            self.lsrc = torch.tensor(lsrc.astype(np.int32), device=dev)
+            self.lw = torch.tensor(lw, device=dev)
+            self.ldst = torch.tensor(ldst.astype(np.int32), device=dev)
+
+    @staticmethod
+    def build_lanes(narrow, n_src):
+        """(lsrc, lw, ldst) host arrays of awelu_gather_sum for the buckets [(dst, table)] of width
+        <= 64: widest bucket first, so every list starts at a multiple of its width; padding
+        (table entry n_src) -> source -1; the destination on a list's first lane."""
+        lsrc, lw, ldst = [np.zeros(0, np.int64)], [np.zeros(0, np.uint8)], [np.zeros(0, np.int64)]
+        for d, table in sorted(narrow, key=lambda b: -b[1].shape[1]):
+            n_u, w = table.shape
+            lsrc.append(np.where(table == n_src, -1, table).reshape(-1))
+            lw.append(np.full(n_u * w, w, dtype=np.uint8))
+            dd = np.full((n_u, w), -1, dtype=np.int64)
+            dd[:, 0] = d
+            ldst.append(dd.reshape(-1))
+        return np.concatenate(lsrc), np.concatenate(lw), np.concatenate(ldst)
+
+    # --- the torch reduction (host tensors, and the buckets wider than 64) ------------------------
+    def _torch_buckets(self, out, vals, buckets):
+        ext = torch.cat([vals, vals.new_zeros(vals.shape[:-1] + (1,))], dim=-1)
+        for d, table in buckets:
+            out[..., d] += ext[..., table].sum(dim=-1)
+        return out
+
+    def _native_ok(self, out, vals, x=None):
+        """The kernel's contract: float64 device tensors, ``out`` contiguous (written in place),
+        the same leading shape everywhere, at most 65,535 rows (vals and x are made contiguous by
+        an exact copy where needed)."""
+        return (self.native and out.is_cuda and out.dtype == torch.float64 and vals.dtype == torch.float64
+                and out.is_contiguous() and out.shape[:-1] == vals.shape[:-1] and out.numel() // max(1, out.shape[-1]) <= 65535
+                and (x is None or (x.dtype == torch.float64 and x.shape[:-1] == out.shape[:-1])))
+
+    def _launch(self, out, vals, lsrc, x=None, cols=None):
+        from .batched_lu import gather_sum
+        rows = out.numel() // max(1, out.shape[-1]) if out.dim() > 1 else 1
+        gather_sum(lsrc, self.lw, self.ldst, vals.contiguous(), out, rows,
+                   x=x.contiguous() if x is not None else None, cols=cols)
 
     def add_into(self, out, vals):
-        ext = torch.cat([vals, vals.new_zeros(vals.shape[:-1] + (1,))], dim=-1)
-        for d, table in self.buckets:
-            out[..., d] += ext[..., table].sum(dim=-1)
+        if not self._native_ok(out, vals):
+            return self._torch_buckets(out, vals, self.buckets)
+        self._launch(out, vals, self.lsrc)
+        if self.wide:
+            self._torch_buckets(out, vals, self.wide)
+        return out
+
+    def add_into_sel(self, out, vals, sel):
+        """add_into(out, vals[..., sel]) without forming vals[..., sel] (sel: a fixed device index
+        tensor; its composition with the lanes is cached)."""
+        if not self._native_ok(out, vals):
+            return self.add_into(out, vals[..., sel])
+        key = (sel.data_ptr(), sel.numel())
+        ent = self._sel_lanes.get(key)
+        if ent is None:
+            s_h = sel.cpu().numpy()
+            lsrc = self.lanes_host[0]
+            comp = np.where(lsrc >= 0, s_h[np.clip(lsrc, 0, None)], -1)
+            ent = self._sel_lanes[key] = (sel, torch.tensor(comp.astype(np.int32), device=self.dev))
+        self._launch(out, vals, ent[1])
+        if self.wide:
+            self._torch_buckets(out, vals[..., sel], self.wide)
+        return out
+
+    def add_products(self, out, vals, x, cols, cols32):
+        """add_into(out, vals * x[..., cols]) without forming the products (cols: int64 device
+        indices, cols32 the same as int32)."""
+        if not self._native_ok(out, vals, x):
+            return self.add_into(out, vals * x[..., cols])
+        self._launch(out, vals, self.lsrc, x=x, cols=cols32)
+        if self.wide:
+            self._torch_buckets(out, vals * x[..., cols], self.wide)
         return out
 
 
@@ -272,12 +359,13 @@ class _GatherMv:
 
     def __init__(self, rows, cols, shape, dev):
         self.cols = torch.tensor(np.asarray(cols, dtype=np.int64), device=dev)
+        self.cols32 = self.cols.to(torch.int32)
         self.sum = scatter_sum(rows, dev)
         self.shape = shape
 
     def mv(self, vals, x):
         out = x.new_zeros(x.shape[:-1] + (self.shape[0],))
-        return self.sum.add_into(out, vals * x[..., self.cols])
+        return self.sum.add_products(out, vals, x, self.cols, self.cols32)
 
 
 def _dense_A(nlp, jv, N0, K):
@@ -292,9 +380,10 @@ def _dense_A(nlp, jv, N0, K):
     K[scol, srow] = -1.0
 
 
-# interval blocks up to which the inertia pass runs beside the factorisation (StructuredKKT.factor):
-# above it the LU kernel alone fills the GPU and the overlap only adds contention
-EARLY_INERTIA_MAX_BLOCKS = int(os.environ.get("AWE_EARLY_INERTIA_MAX_BLOCKS", "512"))
+# interval blocks up to which the inertia pass runs beside the factorisation (StructuredKKT.factor);
+# measured in one session (tools/gpu_solver_ab.sh): AP2 sweep +10-14 %, config-4 shard +15 % (fan) and
+# +20 % (chain), converged MPC (1,280 blocks) 107 ms against 110-115 ms per sampling time: no limit
+EARLY_INERTIA_MAX_BLOCKS = int(os.environ.get("AWE_EARLY_INERTIA_MAX_BLOCKS", "1000000000"))
 
 ZERO_PIVOT = 1e-30   # relative zero-pivot threshold of the inertia count: KKT pivots legitimately span
                      # 1e-10 .. 1e10 at small mu, so only exactly singular columns count as zero
@@ -363,6 +452,7 @@ class StructuredKKT:
         Q_ = np.concatenate([hc, hr[off], np.arange(ny), jc, ny + jr, sc, ny + sr, ny + np.arange(m)])
         self.off_mask = torch.tensor(off, device=dev)
         self.P_, self.Q_ = torch.tensor(P_, device=dev), torch.tensor(Q_, device=dev)
+        self.Q32 = self.Q_.to(torch.int32)
         self.n_solve = self.n_dense = 0
         oP, oQ = owner[P_], owner[Q_]
         ii = (oP >= 0) & (oP == oQ)
@@ -457,13 +547,13 @@ class StructuredKKT:
         self.vals = vals
         self.k_norm = self._mv(vals.abs(), torch.ones(B, self.N, **f64)).amax(dim=1)     # [B]
         nI, L, nS, n_k = self.nI, self.L, self.nS, self.n_k
-        KII = self.sc[0].add_into(torch.zeros(B, n_k * nI * nI, **f64), vals[:, self.sel_ii])
+        KII = self.sc[0].add_into_sel(torch.zeros(B, n_k * nI * nI, **f64), vals, self.sel_ii)
         KII[:, self.pad_flat] = 1.0
         KII = KII.view(B * n_k, nI, nI)
         self.KII = KII
         if early_inertia and KII.is_cuda and B * n_k <= EARLY_INERTIA_MAX_BLOCKS:
             self._interval_inertia_async(KII)
-        KIS = self.sc[1].add_into(torch.zeros(B, n_k * nI * L, **f64), vals[:, self.sel_is]).view(B * n_k, nI, L)
+        KIS = self.sc[1].add_into_sel(torch.zeros(B, n_k * nI * L, **f64), vals, self.sel_is).view(B * n_k, nI, L)
         self.awelu = self.lu_backend == "awelu" and KII.is_cuda   # the CPU test harness uses LAPACK
         if self.awelu:
             from .batched_lu import lu_factor
@@ -479,7 +569,7 @@ class StructuredKKT:
             return
         self.use_btd = False
         S = torch.zeros(B, (nS + 1) * (nS + 1), **f64)
-        self.sc[2].add_into(S, vals[:, self.sel_ss])
+        self.sc[2].add_into_sel(S, vals, self.sel_ss)
         self.sc[3].add_into(S, -T)
         S = S.view(B, nS + 1, nS + 1)
         S[:, nS, :] = 0.0
@@ -537,8 +627,8 @@ class StructuredKKT:
 
     def _mv(self, vals, x):
         """K(vals) x for every instance: a fixed-order gather-sum."""
-        return self.sc_mv.add_into(torch.zeros(x.shape[0], self.N, dtype=torch.float64, device=self.dev),
-                                   vals * x[:, self.Q_])
+        return self.sc_mv.add_products(torch.zeros(x.shape[0], self.N, dtype=torch.float64, device=self.dev),
+                                       vals, x, self.Q_, self.Q32)
 
     def matvec(self, x):
         return self._mv(self.vals, x)

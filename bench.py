@@ -270,6 +270,8 @@ def main():
     ap.add_argument("--dual-sweep-points", type=int, default=8,
                     help="dual-kite u_ref sweep points per GPU (config 4: 8 of linspace(5, 8, 64), example "
                          "discretization N=20; 0: skip)")
+    ap.add_argument("--sweep-mode", choices=["fan", "batch", "chain"], default="fan",
+                    help="AP2 sweep mode (awebox_amd/sweep.py run_sweep)")
     ap.add_argument("--sweep-points", type=int, default=8,
                     help="u_ref sweep points solved per GPU for the sweep block, as one batched homotopy (0: skip)")
     args = ap.parse_args()
@@ -369,7 +371,7 @@ def main():
             mpc["converged"] = pmpc_block(k3.build_constants(), args.pmpc_loops, dev, dist, world)
     sweep = None
     if args.sweep_points > 0:
-        sweep = sweep_block(args.sweep_points, world, dist, dev, consts)
+        sweep = sweep_block(args.sweep_points, world, dist, dev, consts, mode=args.sweep_mode)
     dual_sweep = None
     if args.dual_sweep_points > 0:
         dual_sweep = dual_sweep_block(args.dual_sweep_points, world, dist, dev, with_chain=not args.no_dual_chain)
@@ -755,7 +757,7 @@ def _grid_points(per_gpu, world):
     return np.linspace(5.0, 8.0, n_pts)
 
 
-def sweep_block(per_gpu, world, dist, dev, consts):
+def sweep_block(per_gpu, world, dist, dev, consts, mode="fan"):
     """Second half of the headline metric: wind-speed sweep trials/s on config 4's recipe (points of
     u_ref = linspace(5, 8, 64), contiguous blocks of `per_gpu` per GPU, template broadcast / seed
     scatter / solution gather over RCCL), the AP2 N=40 d=4 trial.  Per shard (weak scaling): the
@@ -773,10 +775,10 @@ def sweep_block(per_gpu, world, dist, dev, consts):
         dist.barrier()
     torch.cuda.synchronize()
     res = run_sweep(u, n_k=consts.cfg.n_k, d=consts.cfg.d, make_evaluator=lambda c, b=1: Ap2Evaluator(c, batch=b),
-                    dist=dist, device=str(dev), opts=IpmOptions(max_iter=1000), mode="fan")
+                    dist=dist, device=str(dev), opts=IpmOptions(max_iter=1000), mode=mode)
     if res is None:
         return None
-    return {"metric": "sweep trials/sec, AP2 N=40 d=4 power curve", "value": res["trials_per_s"],
+    return {"metric": "sweep trials/sec, AP2 N=40 d=4 power curve", "value": res["trials_per_s"], "mode": mode,
             "unit": "trials/s", "points": len(u), "points_per_gpu": per_gpu, "wall_s": res["wall_s"],
             "u_ref": [round(x, 4) for x in res["u_ref"]],
             "all_converged": bool(all(res["ok"])), "iterations": res["iterations"],

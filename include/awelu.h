@@ -41,6 +41,16 @@ int awelu_btd_solve_batched(int nb, int m, int nrhs, int batch, const double* T,
  * MA27/MA57 inertia) for the structured KKT of awebox_amd/ipm.py. */
 int awelu_sym_inertia_batched(int n, int batch, double* A, double ztol, int* counts, void* stream);
 
+/* Fixed-order gather-sums of the solver's KKT assembly and sparse products (ipm._ScatterSum,
+ * ipm._GatherMv): for every row r < rows, out[r * ldo + dst] += the sum of v(r, s) over a
+ * destination's source list, v = vals[r * ldv + s] (x NULL) or vals[r * ldv + s] * x[r * ldx + cols[s]].
+ * The lists occupy L lanes: lsrc[l] a source (-1 = padding), lw[l] the list's power-of-two width
+ * (<= 64; lists aligned to their width), ldst[l] the destination on a list's first lane, -1
+ * elsewhere.  The lists are summed as adjacent-pair trees, the order of torch's row sums. */
+int awelu_gather_sum(int L, int rows, const int* lsrc, const unsigned char* lw, const int* ldst, const double* vals,
+                     long long ldv, const double* x, const int* cols, long long ldx, double* out, long long ldo,
+                     void* stream);
+
 /* Message of the last failed call on this thread. */
 const char* awelu_last_error(void);
 

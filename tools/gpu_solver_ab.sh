@@ -21,6 +21,10 @@ for l in open(f"gpurun_out/solver_ab_{tag}.log"):
               round(m.get("realtime_factor", 0), 3), flush=True)
 PY
 }
+if [ -n "$AB_VAR" ]; then           # AB_VAR=NAME: NAME=0 against NAME=1, twice
+    run off $AB_VAR=0 && run on $AB_VAR=1 && run off2 $AB_VAR=0 && run on2 $AB_VAR=1
+    exit $?
+fi
 run base AWE_EARLY_INERTIA_MAX_BLOCKS=0
 run side AWE_EARLY_INERTIA_MAX_BLOCKS=512
 run all AWE_EARLY_INERTIA_MAX_BLOCKS=100000
