@@ -89,7 +89,7 @@ class BorderedBtd:
                  (C, self.src_gg, self.dst_gg))
         for i, (out, src, dst) in enumerate(parts):
             if self.sc is not None:
-                self.sc[i].add_into(out, v[:, src])
+                self.sc[i].add_into_sel(out, v, src)
             else:
                 out.index_add_(1, dst, v[:, src])
         T = T.view(B, nb, 3, m, m)

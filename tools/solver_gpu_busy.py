@@ -81,6 +81,22 @@ def sweep(steps):
     return _profile(one, steps)
 
 
+def dual_sweep(steps):
+    import numpy as np
+
+    from awebox_amd.ipm import IpmOptions
+    from awebox_amd.sweep import run_sweep
+    from awebox_amd.dual_homotopy import make_evaluator
+    u = np.linspace(5.0, 8.0, 64)[:8]                 # rank 0's shard of config 4
+    state = {}
+
+    def one():
+        state["r"] = run_sweep(u, n_k=20, d=4, make_evaluator=lambda c, b=1: make_evaluator(c, device="cuda", batch=b),
+                               device="cuda",
+                               opts=IpmOptions(max_iter=3000), arch="dual", mode="fan")
+    return _profile(one, steps)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="both")
@@ -94,6 +110,9 @@ def main():
     if args.what in ("sweep", "both"):
         out["ap2_sweep_8"] = sweep(1)
         print(json.dumps({k: v for k, v in out["ap2_sweep_8"].items() if k != "top"}), flush=True)
+    if args.what == "dual":
+        out["dual_sweep_8"] = dual_sweep(1)
+        print(json.dumps({k: v for k, v in out["dual_sweep_8"].items() if k != "top"}), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(out, open(args.out, "w"), indent=1)
     print("wrote", args.out)
