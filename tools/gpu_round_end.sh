@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-end check of the generated evaluation path: GPU suite, smoke, default bench, rocprof kernel
-# statistics of the bench's AP2 block alone (node + gather kernels), and the PMC passes of the two
-# kernels (tools/gpu_pmc_gen.sh).  A failure ends the script.
+# Round-end records in one GPU session: GPU suite, smoke, default bench, rocprof kernel statistics
+# of the bench's AP2 block alone (the instance-minor path's kernels), the PMC passes of those kernels
+# (tools/gpu_pmc_soa.sh) and of the config-3 / config-5 kernels (tools/gpu_pmc_configs.sh).  A
+# failure ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -18,4 +19,5 @@ step 600 bench.log python bench.py
 step 300 rocprof_ap2.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ap2 -o run --output-format csv -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --sweep-points 0 --dual-sweep-points 0 --no-hessian --no-latency
 find gpurun_out/prof_ap2 -name '*_trace.csv' -size +4M -delete
 step 500 pmc_soa.log bash tools/gpu_pmc_soa.sh
+step 400 pmc_configs.log bash tools/gpu_pmc_configs.sh
 echo ROUND_END_DONE
