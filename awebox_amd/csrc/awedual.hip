@@ -579,7 +579,7 @@ __global__ __launch_bounds__(kBlock, ADL_MIN_BLOCKS) void dual_interval_kernel(D
             if (kind == kKindTang) val = tang[idx];
             else if (kind == kKindTangPoly) val = tang[idx] * (C[rr * NN + n] * ihtf);
             else val = a.kconst[idx];
-            jac[sl[u]] = val;
+            __builtin_nontemporal_store(val, &jac[sl[u]]);   // written once (as the AP2 path's J_g)
         }
     }
 }

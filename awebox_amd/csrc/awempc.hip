@@ -269,7 +269,7 @@ __global__ __launch_bounds__(64 * waves_for<D>(), 3) void mpc_interval_kernel(MA
         else if (kind == kKindTangPoly) val = tang[idx] * (C[rr * NN + n] * inv_h_tf);
         else if (kind == kKindOne) val = 1.0;
         else val = -Dc[rr];
-        jac[a.gslot[e]] = val;
+        __builtin_nontemporal_store(val, &jac[a.gslot[e]]);  // written once (as the AP2 path's J_g)
     }
 }
 
