@@ -664,10 +664,11 @@ class StructuredKKT:
             scale = self.k_norm * x.abs().amax(dim=1) + b_norm
             done = done | (err <= rtol * scale)
             bad = ~torch.isfinite(err)
-            if bool((done | bad).all().item()) or it == refine:
+            db = torch.stack([done, bad]).cpu().numpy()          # one transfer: the test and the fallback list
+            if (db[0] | db[1]).all() or it == refine:
                 break
             x = torch.where(done[:, None], x, x + self._solve(r))
-        todo = (~done).nonzero().flatten().cpu().tolist()
+        todo = np.where(~db[0])[0].tolist()
         for b in todo:                      # ill-conditioned interior pivots: dense LU of that K
             self.n_dense += 1
             K = self.sc_dense.add_into(torch.zeros(self.N * self.N, dtype=torch.float64, device=self.dev),
@@ -922,7 +923,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     gl0 = torch.tensor(nlp.yl0[n:], **f64)
     gu0 = torch.tensor(nlp.yu0[n:], **f64)
 
-    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_t, damped=False, unscaled=False):
+    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_t, damped=False, unscaled=False, dev_only=False):
         """IPOPT's scaled optimality error per instance (host [B] arrays): total, dual, primal,
         complementarity at barrier parameter mu_t ([B] tensor); ``damped`` adds the kappa_d term
         (the barrier problem's error).  With ``unscaled`` also the unscaled dual infeasibility,
@@ -956,6 +957,8 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                                    torch.where(torch.isfinite(gl0), gl0 - gI, torch.zeros_like(gI)))
                 u_pr = torch.maximum(u_pr, torch.clamp(vI, min=0.0).amax(1))
             parts += [u_dual, u_pr, compl / osc]
+        if dev_only:
+            return parts
         e = torch.stack(parts).cpu().numpy()
         return tuple(e)
 
@@ -1217,8 +1220,16 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     it = 0
     while it < opts.max_iter:
         c = nlp.constraints(g, y[:, n:])
-        kkt_err, e_d, e_p, e_c, u_d, u_p, u_c = errors(grad, jv, c, y, lam, zl, zu,
-                                                       torch.full((B,), opts.mu_target, **f64), unscaled=True)
+        # one transfer for the loop head: the convergence errors, the barrier problem's error at the
+        # current mu (the first pass of the barrier update below) and theta / phi at the current mu
+        # (the line search's reference values, unless mu changes)
+        mu_head = dev_b(mu)
+        head = torch.stack(errors(grad, jv, c, y, lam, zl, zu, torch.full((B,), opts.mu_target, **f64),
+                                  unscaled=True, dev_only=True) +
+                           [errors(grad, jv, c, y, lam, zl, zu, mu_head, damped=True, dev_only=True)[0],
+                            c.abs().sum(1), barrier_phi(f, y, mu_head)]).cpu().numpy()
+        kkt_err, e_d, e_p, e_c, u_d, u_p, u_c = head[:7]
+        e_mu_head, theta_head, phi_head = head[7], head[8], head[9]
         # IPOPT's OptimalityErrorConvergenceCheck: the scaled error and the unscaled tests
         conv = active & (kkt_err <= opts.tol) & (u_d <= opts.dual_inf_tol) & (u_p <= opts.constr_viol_tol) & \
             (u_c <= opts.compl_inf_tol)
@@ -1234,11 +1245,13 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         if not active.any():
             break
         # barrier update (monotone), per instance
-        for _ in range(50):
-            e_mu = errors(grad, jv, c, y, lam, zl, zu, dev_b(mu), damped=True)[0]
+        mu_changed = False
+        for pass_ in range(50):
+            e_mu = e_mu_head if pass_ == 0 else errors(grad, jv, c, y, lam, zl, zu, dev_b(mu), damped=True)[0]
             upd = active & (e_mu <= opts.kappa_eps * mu) & (mu > mu_floor * 1.0000001)
             if not upd.any():
                 break
+            mu_changed = True
             mu = np.where(upd, np.maximum(mu_floor, np.minimum(opts.kappa_mu * mu, mu ** opts.theta_mu)), mu)
             tau = np.maximum(opts.tau_min, 1.0 - mu)
             for b in np.where(upd)[0]:
@@ -1251,7 +1264,10 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
         grad_phi = grad_y(grad) - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
             torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y)) + opts.kappa_d * mu_d[:, None] * damp_dir
-        theta, phi = torch.stack([c.abs().sum(1), barrier_phi(f, y, mu_d)]).cpu().numpy()
+        if mu_changed:
+            theta, phi = torch.stack([c.abs().sum(1), barrier_phi(f, y, mu_d)]).cpu().numpy()
+        else:
+            theta, phi = theta_head, phi_head
         rhs_top = -(grad_phi + A_T_lam(jv, lam))
         rhs = torch.cat([rhs_top, -c], 1)
         pending = active.copy()
@@ -1301,14 +1317,17 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             sel = dev_b(acc_all)[:, None] > 0
             dzl = torch.where(hl, mu_d[:, None] / dl - zl - zl / dl * dy_new, torch.zeros_like(y))
             dzu = torch.where(hu, mu_d[:, None] / du - zu + zu / du * dy_new, torch.zeros_like(y))
-            alpha_z = ftb2(zl, dzl, zu, dzu, tau_d)
-            az = dev_b(np.where(acc_all, alpha_z, 0.0))[:, None]
+            # the bound multipliers' step on the device (min(1, steps to the bounds), exact like the
+            # host minimum); its host copy only for the log, with f below
+            az_dev = torch.minimum(torch.minimum(ftb_dev(zl, dzl, hl, tau_d), ftb_dev(zu, dzu, hu, tau_d)),
+                                   torch.ones(B, **f64))
+            az = torch.where(dev_b(acc_all) > 0, az_dev, torch.zeros_like(az_dev))[:, None]
             y = torch.where(sel, y_new, y)
             lam = lam + dev_b(np.where(acc_all, alpha_acc, 0.0))[:, None] * dlam_new
             zl = zl + az * dzl
             zu = zu + az * dzu
         else:
-            alpha_z = np.zeros(B)
+            az_dev = torch.zeros(B, **f64)
         # kappa_sigma safeguard
         dl, du = gaps(y)
         zl = torch.where(hl, torch.clamp(zl, min=mu_d[:, None] / (opts.kappa_sigma * dl),
@@ -1328,7 +1347,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         it += 1
         stepped = acc_all | rest_ok
         iters += stepped
-        f_host = (f / nlp.obj_scale).cpu().numpy()
+        f_host, alpha_z = torch.stack([f / nlp.obj_scale, az_dev]).cpu().numpy()
         for b in np.where(stepped)[0]:
             rec = dict(it=int(iters[b]), f=float(f_host[b]), inf_pr=float(e_p[b]), inf_du=float(e_d[b]), mu=float(mu[b]),
                        alpha=float(alpha_acc[b]) if acc_all[b] else 0.0,
