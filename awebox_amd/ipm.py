@@ -664,17 +664,22 @@ class StructuredKKT:
             scale = self.k_norm * x.abs().amax(dim=1) + b_norm
             done = done | (err <= rtol * scale)
             bad = ~torch.isfinite(err)
-            db = torch.stack([done, bad]).cpu().numpy()          # one transfer: the test and the fallback list
+            # one transfer: the test, the fallback list and whether each solution is finite (the
+            # callers' check, self.last_finite)
+            db = torch.stack([done, bad, torch.isfinite(x).all(1)]).cpu().numpy()
             if (db[0] | db[1]).all() or it == refine:
                 break
             x = torch.where(done[:, None], x, x + self._solve(r))
         todo = np.where(~db[0])[0].tolist()
+        self.last_finite = db[2].copy()
         for b in todo:                      # ill-conditioned interior pivots: dense LU of that K
             self.n_dense += 1
             K = self.sc_dense.add_into(torch.zeros(self.N * self.N, dtype=torch.float64, device=self.dev),
                                        self.vals[b])
             xb, info = torch.linalg.solve_ex(K.view(self.N, self.N), rhs[b])
             x[b] = torch.where(info == 0, xb, torch.full_like(xb, float("nan")))
+        if todo:
+            self.last_finite = torch.isfinite(x).all(1).cpu().numpy()
         return x[0] if one else x
 
     def _block_solve(self, B):
@@ -1017,7 +1022,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             if good.any():
                 with _Phase("kkt_solve"):
                     sol = skkt.solve(rhs, active=good)
-                fin = torch.isfinite(sol).all(1).cpu().numpy()
+                fin = skkt.last_finite                        # isfinite(sol), from the solve's last copy
                 if not exact_inertia:
                     dy = sol[:, :ny]
                     Wd = h_op.mv(torch.cat([hv, hv[:, nlp.h_offdiag]], 1), dy)
@@ -1056,10 +1061,13 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     # ---- the filter line search with second-order corrections (all instances in `want`) ---------
     def line_search(want, dy, dlam, rhs_top, c_cur, dl, du, theta, phi, grad_phi, tau_t, mu_t):
         """Per instance in `want`: (accepted, alpha, y_trial, dy_used, dlam_used, backtracks, socs)."""
-        alpha, gphi_d = ftb2(dl, dy, du, -dy, tau_t, extra=[(grad_phi * dy).sum(1)])
-        alpha_min = opts.alpha_min_frac * np.where(
-            gphi_d < 0, np.minimum(opts.gamma_theta, opts.gamma_phi * theta / np.maximum(-gphi_d, 1e-300)),
-            opts.gamma_theta)
+        # the fraction-to-the-boundary step and grad phi . dy stay on the device for the first trial
+        # and come back with its theta / phi in one copy (the host minimum and the device minimum
+        # are the same exact operation)
+        alpha_dev = torch.minimum(torch.minimum(ftb_dev(dl, dy, hl, tau_t), ftb_dev(du, -dy, hu, tau_t)),
+                                  torch.ones(B, **f64))
+        gphi_dev = (grad_phi * dy).sum(1)
+        alpha = gphi_d = alpha_min = None
         live = want.copy()
         acc = np.zeros(B, dtype=bool)
         a_out = np.zeros(B)
@@ -1092,14 +1100,24 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         for _round in range(opts.max_backtracks * (opts.max_soc + 1) + 1):
             if not live.any():
                 break
-            a_t = dev_b(np.where(in_soc, a_s, alpha))[:, None]
-            yt = y + a_t * torch.where(dev_b(in_soc)[:, None] > 0, dys, dy)
+            if alpha is None:                                 # first trial: alpha on the device
+                yt = y + alpha_dev[:, None] * dy
+            else:
+                a_t = dev_b(np.where(in_soc, a_s, alpha))[:, None]
+                yt = y + a_t * torch.where(dev_b(in_soc)[:, None] > 0, dys, dy)
             with _Phase("eval_fg"):
                 ft, gt = nlp.eval_fg(yt[:, :n])
             ct = nlp.constraints(gt, yt[:, n:])
             theta_t = ct.abs().sum(1)
             phi_t = barrier_phi(ft, yt, dev_b(mu_t))
-            tp = torch.stack([theta_t, phi_t]).cpu().numpy()
+            if alpha is None:
+                tp4 = torch.stack([theta_t, phi_t, alpha_dev, gphi_dev]).cpu().numpy()
+                tp, alpha, gphi_d = tp4[:2], tp4[2].copy(), tp4[3].copy()
+                alpha_min = opts.alpha_min_frac * np.where(
+                    gphi_d < 0, np.minimum(opts.gamma_theta, opts.gamma_phi * theta / np.maximum(-gphi_d, 1e-300)),
+                    opts.gamma_theta)
+            else:
+                tp = torch.stack([theta_t, phi_t]).cpu().numpy()
             start_soc = np.zeros(B, dtype=bool)
             cont_soc = np.zeros(B, dtype=bool)
             for b in np.where(live)[0]:
@@ -1139,7 +1157,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                                     torch.where(ctn, dev_b(a_s)[:, None] * c_soc + ct, c_soc))
                 with _Phase("kkt_solve"):
                     sol = skkt.solve(torch.cat([rhs_top, -c_soc], 1), active=start_soc | cont_soc)
-                fin = torch.isfinite(sol).all(1).cpu().numpy()
+                fin = skkt.last_finite                        # isfinite(sol), from the solve's last copy
                 upd = (start_soc | cont_soc) & fin
                 sel = dev_b(upd)[:, None] > 0
                 dys = torch.where(sel, sol[:, :ny], dys)
@@ -1182,7 +1200,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             sig = torch.where(hl, 1.0 / dlv ** 2, torch.zeros_like(yv)) + torch.where(hu, 1.0 / duv ** 2, torch.zeros_like(yv))
             skkt.factor(hv_zero, sig + 1e-8, jv_c, 0.0, mI)
             sol = skkt.solve(-torch.cat([torch.zeros(B, ny, **f64), cv], 1), active=live)
-            fin = torch.isfinite(sol).all(1).cpu().numpy()
+            fin = skkt.last_finite                            # isfinite(sol), from the solve's last copy
             live &= fin
             dyv = torch.where(torch.isfinite(sol[:, :ny]), sol[:, :ny], torch.zeros_like(sol[:, :ny]))
             a = ftb2(dlv, dyv, duv, -dyv, dev_b(tau))
