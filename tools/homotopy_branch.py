@@ -1,5 +1,5 @@
 """Sensitivity of the default AP2 N=40 homotopy's end point to roundoff-level changes: the full
-homotopy on the generated and on the colour evaluation path, and on the colour path from initial
+homotopy on the generated, the colour and the instance-minor evaluation path, and on the colour path from initial
 guesses perturbed by a relative 1e-13 / 1e-10 (seeded).  Prints one JSON line per run: steps,
 iterations, final objective, average power and period.
 
@@ -26,7 +26,8 @@ def main():
     v0 = initial_guess(consts, lay)
     rng = np.random.default_rng(7)
     noise = rng.standard_normal(v0.shape)
-    runs = [("generated", 0.0), ("colour", 0.0), ("colour", 1e-13), ("colour", 1e-10), ("generated", 1e-13)]
+    runs = [("generated", 0.0), ("colour", 0.0), ("colour", 1e-13), ("colour", 1e-10), ("generated", 1e-13),
+            ("soa", 0.0)]
     for path, eps in runs:
         ev = Ap2Evaluator(consts, batch=1)
         ev.path = path
