@@ -454,8 +454,11 @@ def main():
     if fp64:
         line["fp64"] = fp64
     if rec is not None:
-        line["roofline"]["measured_limiter"] = measured_limiter(rec, line["roofline"]["frac"],
-                                                                fp64.get("issued", {}).get("frac"))
+        # FP64: the issued fraction from the PMC record when it has the FP64 counters, else the
+        # algorithmic one (the instance-minor record carries no TRANS_F64 count)
+        line["roofline"]["measured_limiter"] = measured_limiter(
+            rec, line["roofline"]["frac"],
+            fp64.get("issued", {}).get("frac", fp64.get("algorithmic", {}).get("frac")))
     if dual is not None:
         line["dual"] = dual
     if mpc is not None:
