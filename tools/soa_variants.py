@@ -3,8 +3,10 @@ bench's AP2 block: B = 2048 instances of N=40 d=4, J_g instance-minor; HIP-event
 input transpose, the node kernels, the interval kernel and the finalize kernel; output checksums so
 that variants which change the arithmetic show up).
 
-usage: python tools/soa_variants.py lib1.so lib2.so ...
+usage: python tools/soa_variants.py lib1.so lib2.so[:VAR=VAL,VAR2=VAL2] ...
+(an optional suffix sets environment variables for that variant's subprocess)
 """
+import os
 import json
 import subprocess
 import sys
@@ -39,6 +41,13 @@ print(json.dumps({"lib": sys.argv[1], "total_ms": tot, "evals_per_s": B / tot * 
 
 if __name__ == "__main__":
     for rep in range(2):
-        for lib in sys.argv[1:]:
-            r = subprocess.run([sys.executable, "-c", CHILD, lib], capture_output=True, text=True, timeout=240)
-            print(r.stdout.strip() or json.dumps({"lib": lib, "error": r.stderr[-800:]}), flush=True)
+        for spec in sys.argv[1:]:
+            lib, _, envs = spec.partition(":")
+            env = dict(os.environ)
+            for kv in filter(None, envs.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
+            r = subprocess.run([sys.executable, "-c", CHILD, lib], capture_output=True, text=True, timeout=240, env=env)
+            out = r.stdout.strip()
+            print((out[:-1] + f', "variant": "{spec}"}}') if out.endswith("}") else
+                  json.dumps({"lib": spec, "error": r.stderr[-800:]}), flush=True)
