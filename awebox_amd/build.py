@@ -29,13 +29,18 @@ GEN_HEADER = os.path.join(CSRC, "ap2_nodejac.gen.hpp")
 GEN_SOURCES = [os.path.join(CSRC, "gen", f) for f in ("ap2_jacgen.cpp", "sym.hpp")] + [
     os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
     os.path.join(INCLUDE, "awegpu.h"), os.path.join(HERE, "problem.py")]
+# the node-Hessian code (forward-over-reverse, csrc/gen/ap2_hessgen.cpp)
+HESS_HEADER = os.path.join(CSRC, "ap2_nodehess.gen.hpp")
+HESS_SOURCES = [os.path.join(CSRC, "gen", "ap2_hessgen.cpp")] + GEN_SOURCES[1:]
+# (header, generator source, inputs hashed into the header's first line)
+GENERATORS = [(GEN_HEADER, "ap2_jacgen.cpp", GEN_SOURCES), (HESS_HEADER, "ap2_hessgen.cpp", HESS_SOURCES)]
 # content hash of GEN_SOURCES recorded in the generated header's first line: the header is stale
 # when the hash differs (file times do not survive a checkout or the copy to the GPU box)
 _HASH_TAG = "// inputs-sha1: "
 _COMMON = [os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
     os.path.join(INCLUDE, "awegpu.h")]
 TARGETS = {
-    LIB: ([os.path.join(CSRC, "awegpu.hip")], _COMMON + [GEN_HEADER]),
+    LIB: ([os.path.join(CSRC, "awegpu.hip")], _COMMON + [GEN_HEADER, HESS_HEADER]),
     LIB_MPC: ([os.path.join(CSRC, "awempc.hip")],
               _COMMON + [os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp")]
               + [os.path.join(INCLUDE, "awempc.h")]),
@@ -69,39 +74,46 @@ def build_one(lib: str, force: bool = False, verbose: bool = False) -> str:
     return lib
 
 
-def gen_inputs_hash() -> str:
+def gen_inputs_hash(sources=None) -> str:
     import hashlib
     h = hashlib.sha1()
-    for p in GEN_SOURCES:
+    for p in (GEN_SOURCES if sources is None else sources):
         with open(p, "rb") as fh:
             h.update(os.path.basename(p).encode() + b"\0" + fh.read())
     return h.hexdigest()
 
 
-def _header_hash() -> str | None:
-    if not os.path.exists(GEN_HEADER):
+def _header_hash(header=GEN_HEADER) -> str | None:
+    if not os.path.exists(header):
         return None
-    with open(GEN_HEADER) as fh:
+    with open(header) as fh:
         first = fh.readline()
     return first[len(_HASH_TAG):].strip() if first.startswith(_HASH_TAG) else None
 
 
 def generate(force: bool = False, verbose: bool = False) -> str:
-    """Regenerate csrc/ap2_nodejac.gen.hpp when the model, the generator or the default constants
-    changed (content hash of GEN_SOURCES against the one recorded in the header); the file is
-    rewritten only if its content differs, so an unchanged model does not trigger a rebuild.  Without
-    a host C++ compiler the committed header is kept (it is checked against the model by
-    tests/test_codegen.py wherever g++ exists)."""
+    """Regenerate the generated headers (csrc/ap2_nodejac.gen.hpp: node Jacobians;
+    csrc/ap2_nodehess.gen.hpp: node Hessians) when the model, a generator or the default constants
+    changed (content hash of the generator's inputs against the one recorded in the header); a file
+    is rewritten only if its content differs, so an unchanged model does not trigger a rebuild.
+    Without a host C++ compiler the committed headers are kept (tests/test_codegen.py checks them
+    against the model wherever g++ exists)."""
+    for header, gen, sources in GENERATORS:
+        _generate_one(header, gen, sources, force, verbose)
+    return GEN_HEADER
+
+
+def _generate_one(header, gen, sources, force, verbose):
     import shutil
-    want = gen_inputs_hash()
-    if not force and _header_hash() == want:
-        return GEN_HEADER
+    want = gen_inputs_hash(sources)
+    if not force and _header_hash(header) == want:
+        return header
     cxx = os.environ.get("CXX", "g++")
     if shutil.which(cxx) is None:
-        if os.path.exists(GEN_HEADER):
+        if os.path.exists(header):
             if verbose:
-                print(f"{cxx} not found: keeping the committed {os.path.basename(GEN_HEADER)}", file=sys.stderr)
-            return GEN_HEADER
+                print(f"{cxx} not found: keeping the committed {os.path.basename(header)}", file=sys.stderr)
+            return header
         raise RuntimeError(f"{cxx} not found and no generated header to fall back to")
     import tempfile
 
@@ -110,9 +122,8 @@ def generate(force: bool = False, verbose: bool = False) -> str:
     from . import problem as pb
     consts = pb.build_constants(pb.Ap2Config())
     with tempfile.TemporaryDirectory() as tmp:
-        exe = os.path.join(tmp, "ap2_jacgen")
-        cmd = [cxx, "-O1", "-std=c++17", os.path.join(CSRC, "gen", "ap2_jacgen.cpp"),
-               "-o", exe]
+        exe = os.path.join(tmp, os.path.splitext(gen)[0])
+        cmd = [cxx, "-O1", "-std=c++17", os.path.join(CSRC, "gen", gen), "-o", exe]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
@@ -123,12 +134,12 @@ def generate(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(r.stdout.strip(), file=sys.stderr)
         new = _HASH_TAG + want + "\n" + open(out).read()
-    old = open(GEN_HEADER).read() if os.path.exists(GEN_HEADER) else None
+    old = open(header).read() if os.path.exists(header) else None
     if new != old:
-        with open(GEN_HEADER + ".tmp", "w") as fh:
+        with open(header + ".tmp", "w") as fh:
             fh.write(new)
-        os.replace(GEN_HEADER + ".tmp", GEN_HEADER)
-    return GEN_HEADER
+        os.replace(header + ".tmp", header)
+    return header
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

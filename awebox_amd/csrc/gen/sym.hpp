@@ -139,6 +139,7 @@ class Tape {
     }
 
     int group = -1;   // current emission group (set by forward_grads)
+    bool extra_call = false;   // emit extra leaves as ex(i) (an accessor) instead of variables ex<i>
 
   private:
     struct Key {
@@ -572,7 +573,9 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
             case Op::Input: e = opq("in(" + std::to_string(s.idx) + ")"); st.loads++; break;
             case Op::Th: e = opq("th[" + std::to_string(s.idx) + "]"); st.loads++; break;
             case Op::Cs: e = opq("cst[" + std::to_string(s.idx) + "]"); st.loads++; break;
-            case Op::Extra: e = opq("ex" + std::to_string(s.idx)); break;
+            case Op::Extra:
+                e = opq(t.extra_call ? "ex(" + std::to_string(s.idx) + ")" : "ex" + std::to_string(s.idx));
+                break;
             case Op::Add:
             case Op::Sub:
                 if (fz[v].m >= 0) {

@@ -80,6 +80,9 @@ def load_library(path: str = _LIB_PATH):
     lib.awe_set_eval_path.argtypes = [h, ctypes.c_int]
     lib.awe_get_eval_path.argtypes = [h, ip]
     lib.awe_last_kernel_ms_gen.argtypes = [h, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.awe_eval_hess_im.argtypes = [h] + [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p]
+    lib.awe_set_hess_path.argtypes = [h, ctypes.c_int]
+    lib.awe_get_hess_path.argtypes = [h, ip]
     _LIB = lib
     return lib
 
@@ -255,6 +258,40 @@ class Ap2Evaluator:
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         self._check(self._lib.awe_eval_hess(self._h, V.data_ptr(), P.data_ptr(), sigma.data_ptr(),
                                             lam_g.data_ptr(), H.data_ptr(), ctypes.c_void_p(s)))
+
+    def eval_hess_device_im(self, V, P, sigma, lam_g, H, stream=None):
+        """As eval_hess_device with H instance-minor: the transposed view ``x.t()`` of a contiguous
+        [nnz_h, ld] tensor, ld >= B (awe_eval_hess_im; ``alloc_hess``)."""
+        import torch
+        for t, n in ((V, self.n_v), (P, self.n_p), (sigma, 1), (lam_g, self.n_g)):
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
+                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+        if H.dtype != torch.float64 or not H.is_cuda or tuple(H.shape) != (self.batch, self.nnz_h) or \
+                H.stride(0) != 1 or H.stride(1) < self.batch:
+            raise ValueError("H must be an instance-minor [batch, nnz_h] float64 view (strides (1, ld))")
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(self._lib.awe_eval_hess_im(self._h, V.data_ptr(), P.data_ptr(), sigma.data_ptr(),
+                                               lam_g.data_ptr(), H.data_ptr(), int(H.stride(1)), ctypes.c_void_p(s)))
+
+    def alloc_hess(self, device="cuda", instance_minor=True):
+        """A Hessian value tensor [B, nnz_h], instance-minor unless asked otherwise."""
+        import torch
+        if instance_minor:
+            return torch.zeros(self.nnz_h, self.batch, dtype=torch.float64, device=device).t()
+        return torch.zeros(self.batch, self.nnz_h, dtype=torch.float64, device=device)
+
+    HESS_PATHS = {"hyperdual": 0, "generated": 1, "follow": 2}
+
+    @property
+    def hess_path(self):
+        """'generated' or 'hyperdual': the Hessian kernel the next call runs (include/awegpu.h)."""
+        p = ctypes.c_int()
+        self._check(self._lib.awe_get_hess_path(self._h, ctypes.byref(p)))
+        return {0: "hyperdual", 1: "generated"}[p.value]
+
+    @hess_path.setter
+    def hess_path(self, name):
+        self._check(self._lib.awe_set_hess_path(self._h, self.HESS_PATHS[name]))
 
     def eval_hess(self, V, P, sigma, lam_g):
         """Host arrays in, host array out: H [B, nnz_h] (upper triangle, CCS)."""

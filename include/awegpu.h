@@ -27,6 +27,8 @@
 #ifndef AWEGPU_H
 #define AWEGPU_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -154,6 +156,24 @@ int awe_eval_hess_host(awe_handle h, const double* V, const double* P, const dou
                        const double* lam_g, double* H);
 /* Kernel time of the last awe_eval_hess call (HIP events), milliseconds. */
 int awe_last_hess_ms(awe_handle h, float* ms);
+/* nlp_hess_l with H instance-minor: the value of CCS entry i of instance b at H[i * ldh + b]
+ * (ldh >= batch; with batch = 1 and ldh = 1 it is awe_eval_hess's layout). */
+int awe_eval_hess_im(awe_handle h, const double* V, const double* P, const double* sigma, const double* lam_g,
+                     double* H, size_t ldh, void* stream);
+/* Hessian path.  AWE_HESS_GENERATED: straight-line direction-pair Hessians of the node Lagrangian
+ * generated at build time from the node model (csrc/gen/ap2_hessgen.cpp: a symbolic reverse sweep,
+ * then sparse forward mode over it -- what CasADi's SX Hessian of the reference's nlp_hess_l
+ * evaluates, opti/preparation.py:366-400), one wavefront per collocation node for 64 instances, and
+ * an assembly kernel, one lane per instance; AWE_HESS_HYPERDUAL: the compressed hyper-dual kernel,
+ * one (node, colour pair) per lane; AWE_HESS_FOLLOW (default): the generated Hessian with the
+ * generated and instance-minor evaluation paths, the hyper-dual one with the colour path.  Both
+ * agree to rounding.  AWE_HESS_PATH=generated|hyperdual selects it at awe_create; awe_get_hess_path
+ * returns the path the next call takes. */
+#define AWE_HESS_HYPERDUAL 0
+#define AWE_HESS_GENERATED 1
+#define AWE_HESS_FOLLOW 2
+int awe_set_hess_path(awe_handle h, int path);
+int awe_get_hess_path(awe_handle h, int* path);
 
 /* nlp_grad_f + nlp_jac_g fused, with J_g and grad f instance-minor: the value of CCS entry i of
  * instance b at jac[i * ldj + b], gradient entry i at grad_f[i * ldj + b] (ldj >= batch; V, P, g and f

@@ -174,14 +174,21 @@ def _close_hess(Hk, Ho, what="H"):
     assert not bad.any(), f"{what}: {bad.sum()} entries off, worst {D.data[bad].max():.3e}"
 
 
-@pytest.mark.parametrize("n_k,d,member", [(40, 4, 3), (5, 3, 1), (3, 2, 2)])
-def test_hessian_matches_oracle(gpu, n_k, d, member):
+@pytest.mark.parametrize("n_k,d,member,hess", [(40, 4, 3, "hyperdual"), (5, 3, 1, "hyperdual"),
+                                                (3, 2, 2, "hyperdual"), (40, 4, 3, "generated"),
+                                                (5, 3, 1, "generated"), (3, 2, 2, "generated"),
+                                                (4, 5, 0, "generated")])
+def test_hessian_matches_oracle(gpu, n_k, d, member, hess):
+    """nlp_hess_l of one instance on both Hessian kernels: the hyper-dual colour-pair kernel and the
+    generated forward-over-reverse node code + assembly kernel."""
     from awebox_amd.evaluator import Ap2Evaluator
     consts, lay, v0, orc = _setup(n_k, d)
     V = batch_member(v0, lay, member)
     P = pb.pack_p(lay, consts, v0, u_ref=7.0)
     lam = np.random.default_rng(7).standard_normal(lay.n_g)       # SURVEY 8(d): sigma 1, lam ~ N(0,1)
     ev = Ap2Evaluator(consts, batch=1)
+    ev.hess_path = hess
+    assert ev.hess_path == hess
     H = ev.hess_csc(ev.eval_hess(V, P, 1.0, lam)[0])
     Ho = orc.nlp_hess_l(V, P, 1.0, lam, lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES)
     _close_hess(H, Ho)
@@ -206,4 +213,41 @@ def test_hessian_batch_sigma_lambda_and_determinism(gpu):
     ev.eval_hess_device(dev(Vs), dev(Ps), dev(sig), dev(lams), Hd)
     torch.cuda.synchronize()
     assert np.array_equal(Hd.cpu().numpy(), Hh)
+    assert ev.last_hess_ms() > 0
+
+
+def test_generated_hessian_batch_matches_hyperdual_and_oracle(gpu):
+    """130 instances (two full blocks of 64 and a partial one) with different V, u_ref, sigma and
+    multipliers: the generated Hessian against the hyper-dual kernel for every instance and the oracle
+    for three; the instance-minor output (awe_eval_hess_im) equals the per-instance one bitwise, and
+    repeats bitwise."""
+    torch = gpu
+    from awebox_amd.evaluator import Ap2Evaluator
+    consts, lay, v0, orc = _setup()
+    B = 130
+    rng = np.random.default_rng(5)
+    Vs = np.stack([batch_member(v0, lay, b) for b in range(B)])
+    Ps = np.stack([pb.pack_p(lay, consts, v0, u_ref=u) for u in np.linspace(5, 8, B)])
+    sig = rng.uniform(0.0, 2.0, B)
+    lams = rng.standard_normal((B, lay.n_g))
+    ev = Ap2Evaluator(consts, batch=B)
+    assert ev.hess_path == "generated"                 # follows the instance-minor evaluation path
+    Hg = ev.eval_hess(Vs, Ps, sig, lams)
+    ev.hess_path = "hyperdual"
+    Hh = ev.eval_hess(Vs, Ps, sig, lams)
+    scale = np.abs(Hh).max(axis=1, keepdims=True)
+    assert np.all(np.abs(Hg - Hh) <= RTOL * np.abs(Hh) + ATOL_REL * scale)
+    for b in (0, 64, 129):
+        Ho = orc.nlp_hess_l(Vs[b], Ps[b], sig[b], lams[b], lay, pb.THETA0_OFF, pb.COST_NAMES, pb.PHI_NAMES)
+        _close_hess(ev.hess_csc(Hg[b]), Ho, f"H[{b}]")
+    ev.hess_path = "generated"
+    dev = lambda a: torch.tensor(a, device="cuda")
+    Him = ev.alloc_hess()
+    args = (dev(Vs), dev(Ps), dev(sig), dev(lams))
+    ev.eval_hess_device_im(*args, Him)
+    H1 = Him.clone()
+    ev.eval_hess_device_im(*args, Him)
+    torch.cuda.synchronize()
+    assert torch.equal(Him, H1)
+    assert np.array_equal(Him.cpu().numpy(), Hg)
     assert ev.last_hess_ms() > 0
