@@ -58,3 +58,46 @@ def test_generated_jacobian_matches_dual_model(checker, k, seed):
         assert r["value_rel"] < 1e-14, (kind, r)
         assert r["tangent_rel"] < 1e-12, (kind, r)
         assert r["tangent_max"] > 1.0
+
+
+@pytest.fixture(scope="module")
+def hess_checker(tmp_path_factory):
+    tmp = tmp_path_factory.mktemp("hgen")
+    exe = str(tmp / "check_hess")
+    subprocess.run(["g++", "-O1", "-std=c++17", os.path.join(CSRC, "gen", "check_ap2_hess.cpp"), "-o", exe],
+                   check=True)
+    return tmp, exe
+
+
+def test_committed_hessian_header_is_current():
+    """ap2_nodehess.gen.hpp in the tree is what gen/ap2_hessgen.cpp writes for the current model."""
+    before = open(B.HESS_HEADER).read()
+    B.generate(force=True)
+    assert open(B.HESS_HEADER).read() == before, "ap2_nodehess.gen.hpp is stale: run python -m awebox_amd.build"
+
+
+@pytest.mark.parametrize("k,seed", [(0, 0), (13, 1), (39, 2)])
+def test_generated_hessian_matches_hyperdual_model(hess_checker, k, seed):
+    """Every direction pair of the node Hessian pattern (and dL/dxdot at a Radau node) against one
+    hyper-dual evaluation of the node Lagrangian per pair (csrc/gen/check_ap2_hess.cpp)."""
+    tmp, exe = hess_checker
+    consts = pb.build_constants(pb.Ap2Config(n_k=40, d=4))
+    lay = pb.NlpLayout(40, 4)
+    v0 = initial_guess(consts, lay)
+    P = pb.pack_p(lay, consts, v0)
+    th = P[lay.n_v + pb.NW + pb.NCOST:]
+    rng = np.random.default_rng(seed)
+    w = np.concatenate([v0[lay.x(k)], v0[lay.xdot(k)], v0[lay.u(k)], v0[lay.z(k)], v0[lay.theta()],
+                        v0[lay.phi()][:1], [0.5]])                      # last: phi.psi
+    w = w * (1 + 0.05 * rng.standard_normal(w.shape)) + 0.01 * rng.standard_normal(w.shape)
+    for name, arr in (("consts", consts.consts), ("th", th), ("w", w)):
+        np.savetxt(str(tmp / f"{name}.txt"), arr)
+    cxx, inv_tf = 2.0 + rng.random(), 1.0 / (20.0 + 30.0 * rng.random())
+    out = subprocess.run([exe, str(tmp / "consts.txt"), str(tmp / "th.txt"), str(tmp / "w.txt"), repr(cxx),
+                          repr(inv_tf), "0.37", "-1.9"], check=True, capture_output=True, text=True)
+    rec = json.loads(out.stdout)
+    for kind in ("shooting", "radau"):
+        r = rec[kind]
+        assert r["hess_rel"] < 1e-12, (kind, r)
+        assert r["grad_rel"] < 1e-12, (kind, r)
+        assert r["hess_max"] > 1.0 and r["nonzero"] > 150, (kind, r)
