@@ -176,7 +176,10 @@ class DeviceNlp:
         # J_g in the evaluator's instance-minor layout where it has one (the AP2 evaluator writes it
         # with coalesced stores, awe_eval_nlp_im); a [B, nnz] view either way
         self.jac = ev.alloc_jac(device) if hasattr(ev, "alloc_jac") else torch.zeros(B, ev.nnz, **f64)
-        self.H = torch.zeros(B, ev.nnz_h, **f64)
+        # H instance-minor where the evaluator's Hessian kernel writes it that way (the generated
+        # Hessian, awe_eval_hess_im); per instance for the hyper-dual kernels
+        self.h_im = getattr(ev, "hess_path", None) == "generated" and hasattr(ev, "alloc_hess")
+        self.H = ev.alloc_hess(device) if self.h_im else torch.zeros(B, ev.nnz_h, **f64)
         self.sig = torch.ones(B, **f64)
         self.free_t = torch.tensor(self.free, device=device)
         self.ineq_t = torch.tensor(self.ineq, device=device)
@@ -204,7 +207,10 @@ class DeviceNlp:
         """Hessian of obj_scale f + (c_scale lam)^T g, reduced upper values [B, nH]."""
         lam_unscaled = (lam * self.c_scale).contiguous()
         self.sig.copy_(self.obj_scale)
-        self.ev.eval_hess_device(self.full_x(x), self.P, self.sig, lam_unscaled, self.H)
+        if self.h_im:
+            self.ev.eval_hess_device_im(self.full_x(x), self.P, self.sig, lam_unscaled, self.H)
+        else:
+            self.ev.eval_hess_device(self.full_x(x), self.P, self.sig, lam_unscaled, self.H)
         return self.H[:, self.h_keep]
 
     def constraints(self, g, s):

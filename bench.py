@@ -164,8 +164,9 @@ def measured_limiter(rec, hbm_frac, fp64_frac):
         return None
     wait = max(v["wait_frac"] for v in per.values())
     fp = fp64_frac if fp64_frac is not None else 0.0
-    bound = ("latency (waves waiting on memory / LDS while HBM is at {:.0%} and FP64 at {:.0%} of peak)".format(
-        hbm_frac, fp) if wait > 0.5 and hbm_frac < 0.6 and fp < 0.6 else "hbm" if hbm_frac >= fp else "fp64")
+    fp_txt = "FP64 at {:.1%} of peak".format(fp64_frac) if fp64_frac is not None else "FP64 not measured"
+    bound = ("latency (waves waiting on memory / LDS while HBM is at {:.0%} of peak and {})".format(
+        hbm_frac, fp_txt) if wait > 0.5 and hbm_frac < 0.6 and fp < 0.6 else "hbm" if hbm_frac >= fp else "fp64")
     return {"bound": bound, "kernels": per}
 
 
@@ -473,6 +474,8 @@ def main():
         line["latency_batch1"] = latency_block(consts, lay, v0, with_cpu=not args.no_cpu_baseline)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(consts, lay, v0, args.cpu_seconds)
+    if rank == 0:
+        line["casadi_probe"] = casadi_probe()
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
@@ -843,29 +846,69 @@ def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4, with_chain=True):
             "chain": chain, "utilisation": sweep_profile("dual")}
 
 
+def hess_gen_counts():
+    """Algorithmic work of one node Hessian from the generated code (csrc/ap2_nodehess.gen.hpp:
+    kFlops = adds / muls / reciprocals, kTranscendental = sqrt / exp / log / sin / cos calls, per
+    node kind: 0 shooting, 1 Radau)."""
+    import re
+    txt = open(os.path.join(ROOT, "awebox_amd", "csrc", "ap2_nodehess.gen.hpp")).read()
+    get = lambda name: [int(x) for x in re.search(r"%s\[2\] = \{(\d+), (\d+)\}" % name, txt).groups()]  # noqa: E731
+    return get("kFlops"), get("kTranscendental")
+
+
 def hessian_block(ev, V, P, B, lay, dev, steps=10):
     """nlp_hess_l throughput (sigma = 1, lam ~ N(0,1) seed 7), reported beside the
-    headline metric; kernel time from the library's HIP events."""
+    headline metric; kernel time from the library's HIP events.  The default Hessian at this batch is
+    the generated one (awe_eval_hess_im, H instance-minor as the solver reads it); the hyper-dual
+    colour-pair kernel is timed beside it (3 calls)."""
     import numpy as np
     import torch
     sig = torch.ones(B, dtype=torch.float64, device=dev)
     lam = torch.tensor(np.random.default_rng(7).standard_normal((B, lay.n_g)), device=dev)
-    H = torch.empty(B, ev.nnz_h, dtype=torch.float64, device=dev)
-    ev.eval_hess_device(V, P, sig, lam, H)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    kms = []
-    for _ in range(steps):
-        ev.eval_hess_device(V, P, sig, lam, H)
-        kms.append(ev.last_hess_ms())
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    out = {"metric": "nlp_hess_l evals/sec", "value": B / dt, "unit": "evals/s", "ms_per_step": dt * 1e3,
-           "kernel_ms": float(np.mean(kms)), "nnz_h": ev.nnz_h, "batch": B,
-           "finite": bool(torch.isfinite(H).all().item())}
-    rl = hess_roofline(B, float(np.mean(kms)))
-    if rl is not None:
-        out["roofline"] = rl
+    out = {}
+    for path, n in (("generated", steps), ("hyperdual", 3)):
+        ev.hess_path = path
+        if path == "generated":
+            H = ev.alloc_hess(dev)
+            call = lambda: ev.eval_hess_device_im(V, P, sig, lam, H)  # noqa: E731
+        else:
+            H = torch.empty(B, ev.nnz_h, dtype=torch.float64, device=dev)
+            call = lambda: ev.eval_hess_device(V, P, sig, lam, H)  # noqa: E731
+        call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        kms = []
+        for _ in range(n):
+            call()
+            kms.append(ev.last_hess_ms())
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        rec = {"metric": "nlp_hess_l evals/sec", "value": B / dt, "unit": "evals/s", "ms_per_step": dt * 1e3,
+               "kernel_ms": float(np.mean(kms)), "nnz_h": ev.nnz_h, "batch": B,
+               "finite": bool(torch.isfinite(H).all().item())}
+        if path == "generated":
+            out.update(rec)
+            out["path"] = "generated (ap2_hgen_*: forward-over-reverse node code + assembly, H instance-minor)"
+            (f0, f1), (t0_, t1_) = hess_gen_counts()
+            d = lay.d
+            flops = lay.n_k * ((f0 + t0_) + d * (f1 + t1_))       # node code per instance; transcendentals as 1
+            byts = 8.0 * (lay.n_v + lay.n_p + lay.n_g + 1 + ev.nnz_h)   # V, P, lam, sigma in; H out
+            kms_mean = float(np.mean(kms)) * 1e-3
+            out["roofline"] = {
+                "bound": "fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+                "flops_per_eval": flops, "achieved": flops * B / kms_mean / 1e12,
+                "frac": flops * B / kms_mean / 1e12 / FP64_PEAK_TFLOPS,
+                "hbm": {"bytes_per_eval": byts, "achieved_GBps": byts * B / kms_mean / 1e9,
+                        "frac": byts * B / kms_mean / 1e9 / HBM_PEAK_GBS},
+                "note": "algorithmic: the generated node code's operations (kFlops + kTranscendental of "
+                        "csrc/ap2_nodehess.gen.hpp) per node, assembly not counted; bytes = V, P, lam, sigma in "
+                        "and H out once"}
+        else:
+            out["hyperdual"] = rec
+            rl = hess_roofline(B, float(np.mean(kms)))
+            if rl is not None:
+                out["hyperdual"]["roofline"] = rl
+    ev.hess_path = "follow"
     return out
 
 
@@ -895,6 +938,18 @@ def hess_roofline(B, kernel_ms):
             "hbm_GBps": hbm, "pmc_record": "profiles/pmc_hess.json"}
 
 
+def casadi_probe():
+    """BASELINE.md's CPU-baseline rule: probe `import casadi` on the box; the reference's CasADi +
+    IPOPT path is the CPU baseline only if it imports (it never has: no casadi wheel in the image),
+    otherwise the C++ CPU port is (cpu_baseline.kind = "port").  A child process, so a failing import
+    cannot disturb this one."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import casadi; print(casadi.__version__)"], capture_output=True,
+                       text=True, timeout=120)
+    return {"importable": r.returncode == 0,
+            "detail": (r.stdout.strip() if r.returncode == 0 else (r.stderr.strip().splitlines() or [""])[-1])[:200]}
+
+
 def latency_block(consts, lay, v0, with_cpu=True, reps=50):
     """Config 2's drop-in case: IPOPT on the host calls one NLP evaluation at a time through the
     CasADi Callback.  Host round-trip latency (host arrays in and out, one instance) of the C-ABI's
@@ -918,9 +973,16 @@ def latency_block(consts, lay, v0, with_cpu=True, reps=50):
             ts.append(time.perf_counter() - t0)
         return float(np.median(ts)) * 1e3
 
+    lam = np.random.default_rng(7).standard_normal((1, lay.n_g))
     out = {"unit": "ms", "instances": 1,
            "nlp_f_host": med(lambda: ev.eval_f(V, P)), "nlp_g_host": med(lambda: ev.eval_g(V, P)),
-           "nlp_f_g_grad_jac_host": med(lambda: ev.eval_nlp(V, P))}
+           "nlp_f_g_grad_jac_host": med(lambda: ev.eval_nlp(V, P)),
+           # nlp_hess_l: once per IPOPT iteration through the Callback; default at batch 1 the
+           # hyper-dual kernel (follows the colour evaluation path), the generated one beside it
+           "nlp_hess_l_host": med(lambda: ev.eval_hess(V, P, 1.0, lam))}
+    ev.hess_path = "generated"
+    out["nlp_hess_l_host_generated"] = med(lambda: ev.eval_hess(V, P, 1.0, lam))
+    ev.hess_path = "follow"
     if with_cpu:
         from oracle.cpu_port import CpuPort
         port = CpuPort(consts)

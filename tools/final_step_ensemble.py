@@ -34,7 +34,9 @@ def main():
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--eps", type=float, default=1e-13)
     ap.add_argument("--seed", type=int, default=11)
-    ap.add_argument("--path", default="generated", choices=["generated", "colour", "cpu"])
+    ap.add_argument("--path", default="generated", choices=["generated", "colour", "soa", "cpu"])
+    ap.add_argument("--hess", default="follow", choices=["follow", "generated", "hyperdual"],
+                    help="Hessian kernel (default: the one the evaluation path selects)")
     ap.add_argument("--variants", default="[{}]", help="JSON list of IpmOptions overrides")
     ap.add_argument("--cache", default=os.path.join(ROOT, "gpurun_out", "power1_{path}.npz"))
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "final_step_ensemble.jsonl"))
@@ -56,13 +58,15 @@ def main():
         from awebox_amd.evaluator import Ap2Evaluator
         ev = Ap2Evaluator(consts, batch=batch)
         ev.path = args.path
+        ev.hess_path = args.hess
         return ev, "cuda"
 
-    cache = args.cache.format(path=args.path)
+    cache = args.cache.format(path=f"{args.path}_{args.hess}")
     if not os.path.exists(cache):
         ev1, dev = make_ev(1)
         t0 = time.perf_counter()
-        _, summ, _, res = optimize(consts, ev1, IpmOptions(max_iter=2000), device=dev, final_step="power1")
+        _, summ, _, res = optimize(consts, ev1, IpmOptions(max_iter=2000), device=dev, final_step="power1",
+                                   eval_path=None)
         os.makedirs(os.path.dirname(cache), exist_ok=True)
         np.savez(cache, x=res.x, lam=res.lam_g, zl=res.zl, zu=res.zu)
         print(json.dumps({"power1": [s["iterations"] for s in summ], "seconds": time.perf_counter() - t0}), flush=True)
@@ -101,7 +105,7 @@ def main():
             hist[br] = hist.get(br, 0) + 1
             members.append({"status": r.status, "it": r.iterations, "T": round(out["period_s"], 3),
                             "P": round(out["avg_power_W"], 1), "f": r.f, "branch": br})
-        rec = {"variant": var, "path": args.path, "k": K, "eps": args.eps, "seconds": secs, "hist": hist,
+        rec = {"variant": var, "path": args.path, "hess": getattr(ev, "hess_path", "fd"), "k": K, "eps": args.eps, "seconds": secs, "hist": hist,
                "members": members}
         line = json.dumps(rec, default=float)
         print(line, flush=True)

@@ -31,8 +31,9 @@ def main():
     for path, eps in runs:
         ev = Ap2Evaluator(consts, batch=1)
         ev.path = path
-        V, summary, out, _ = optimize(consts, ev, IpmOptions(max_iter=2000), v_init=v0 * (1.0 + eps * noise))
-        print(json.dumps({"path": path, "perturbation": eps,
+        V, summary, out, _ = optimize(consts, ev, IpmOptions(max_iter=2000), v_init=v0 * (1.0 + eps * noise),
+                                      eval_path=None)
+        print(json.dumps({"path": path, "hess": ev.hess_path, "perturbation": eps,
                           "iterations": [r["iterations"] for r in summary],
                           "status": [r["status"] for r in summary], "f": summary[-1]["f"],
                           "avg_power_W": out["avg_power_W"], "period_s": out["period_s"]}, default=float), flush=True)
