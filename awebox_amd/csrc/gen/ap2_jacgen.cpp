@@ -54,13 +54,9 @@ struct KindOut {
 };
 
 std::vector<int> ko_dbp_dirs;   // directions of the Radau node's dbp entries, in order
-constexpr int kLookahead = 0;   // default leaf-load lookahead (statements)
 
 KindOut generate(int kind, const std::vector<double>& cst, const awt::ColorTabs& ct, int n_strips) {
     awe::Tape tape;
-    // leaf loads AWE_GEN_LOOKAHEAD statements ahead of their scheduled place (LDS latency overlap)
-    const char* la = std::getenv("AWE_GEN_LOOKAHEAD");
-    tape.lookahead = la ? std::atoi(la) : kLookahead;
     awe::active_tape() = &tape;
     std::vector<Sym> w(AWE_NW + 1), th(AWE_NTHETA0), cs(cst.size());
     for (int i = 0; i <= AWE_NW; ++i) w[i] = Sym::of(tape.leaf(Op::Input, i));

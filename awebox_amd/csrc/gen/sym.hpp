@@ -140,7 +140,6 @@ class Tape {
 
     int group = -1;   // current emission group (set by forward_grads)
     bool extra_call = false;   // emit extra leaves as ex(i) (an accessor) instead of variables ex<i>
-    int lookahead = 0;         // statements a leaf load is emitted ahead of its scheduled place
 
   private:
     struct Key {
@@ -490,28 +489,6 @@ inline std::string emit(Tape& t, std::vector<Store>& stores, EmitStats& st, bool
         order.swap(kept);
     }
     if (schedule) order = pressure_schedule(t, order, ops);
-    // load lookahead: every leaf load (input, parameter, constant) moves up to `lookahead` statements
-    // ahead of its place in the schedule, so that its latency (an LDS or scalar load) overlaps the
-    // statements in between; the scheduling fences would otherwise keep the compiler from hoisting it
-    if (t.lookahead > 0) {
-        std::vector<int> moved;
-        moved.reserve(order.size());
-        std::vector<std::pair<int, int>> pending;            // (target position, node) of leaves
-        for (size_t i = 0; i < order.size(); ++i) {
-            const Op op = t.n[order[i]].op;
-            const bool leaf = op == Op::Input || op == Op::Th || op == Op::Cs;
-            if (!leaf) continue;
-            pending.emplace_back(std::max(0, (int)i - t.lookahead), order[i]);
-        }
-        std::vector<std::vector<int>> at(order.size());
-        for (auto& pn : pending) at[pn.first].push_back(pn.second);
-        for (size_t i = 0; i < order.size(); ++i) {
-            for (int v : at[i]) moved.push_back(v);
-            const Op op = t.n[order[i]].op;
-            if (!(op == Op::Input || op == Op::Th || op == Op::Cs)) moved.push_back(order[i]);
-        }
-        order.swap(moved);
-    }
     std::vector<int> pos(N, -1);
     for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int)i;
     // stores of constant nodes (zero tangents) go first, the others after their node
