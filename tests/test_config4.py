@@ -90,3 +90,28 @@ def test_config4_far_shard_converges_with_rising_power(gpu):
     p = np.asarray(res["avg_power_W"])
     assert np.all(np.isfinite(p)) and p[0] > 1000.0 and np.all(np.diff(p) > 0), p
     assert np.allclose(res["u_ref"], u)
+
+
+# the reference-order curve: one chain over all 64 points (awebox/sweep.py:150-172),
+# tools/config4_full.py --global-chain, profiles/r05/config4/config4_global_chain.jsonl
+GLOBAL_CHAIN = {39: (6.857142857142857, 6921.33, 17.79), 40: (6.904761904761905, 6954.31, 17.9)}
+
+
+def test_config4_shard_boundary_matches_the_reference_order_chain(gpu):
+    """The shard 4 / shard 5 boundary of config 4 (points 39 | 40 of linspace(5, 8, 64), N=20 d=4):
+    shard 5's anchor -- the homotopy at point 40 from the standard initial guess, as rank 5 runs it --
+    and the continuation across the boundary to shard 4's last point (39, warm-started from 40) against
+    the reference-order global chain's solutions at those points.  Both land on the chain's interior
+    orbit family (period below the example's t_f bound of 20 s) with powers within 0.1 %.  (Shard 4's
+    own anchor at point 32 does not: its homotopy reaches a 17.7 s orbit where the chain has 16.9 s,
+    and its warm starts 33..39 go to the t_f-bound family, 2-8 % above the chain's power --
+    profiles/r05/config4/compare.json.)"""
+    u = np.linspace(5.0, 8.0, 64)
+    res = _sweep([u[40], u[39]], n_k=20, mode="chain")
+    print("boundary", res["avg_power_W"], res["period_s"], res["iterations"], res["wall_s"])
+    assert all(res["ok"]), res
+    for i, (uu, p, t) in zip((40, 39), zip(res["u_ref"], res["avg_power_W"], res["period_s"])):
+        ug, pg, tg = GLOBAL_CHAIN[i]
+        assert abs(uu - ug) < 1e-12
+        assert t < 19.99 and abs(t - tg) < 0.05, (i, t, tg)
+        assert abs(p - pg) / pg < 1e-3, (i, p, pg)
