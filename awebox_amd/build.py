@@ -32,8 +32,14 @@ GEN_SOURCES = [os.path.join(CSRC, "gen", f) for f in ("ap2_jacgen.cpp", "sym.hpp
 # the node-Hessian code (forward-over-reverse, csrc/gen/ap2_hessgen.cpp)
 HESS_HEADER = os.path.join(CSRC, "ap2_nodehess.gen.hpp")
 HESS_SOURCES = [os.path.join(CSRC, "gen", "ap2_hessgen.cpp")] + GEN_SOURCES[1:]
-# (header, generator source, inputs hashed into the header's first line)
-GENERATORS = [(GEN_HEADER, "ap2_jacgen.cpp", GEN_SOURCES), (HESS_HEADER, "ap2_hessgen.cpp", HESS_SOURCES)]
+# the tracking-MPC node-Jacobian code (csrc/gen/kite3_jacgen.cpp)
+K3_HEADER = os.path.join(CSRC, "kite3_nodejac.gen.hpp")
+K3_SOURCES = [os.path.join(CSRC, "gen", f) for f in ("kite3_jacgen.cpp", "sym.hpp")] + [
+    os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
+    os.path.join(INCLUDE, "awempc.h"), os.path.join(INCLUDE, "awegpu.h"), os.path.join(HERE, "kite3.py")]
+# (header, generator source, inputs hashed into the header's first line, default constants)
+GENERATORS = [(GEN_HEADER, "ap2_jacgen.cpp", GEN_SOURCES, "ap2"), (HESS_HEADER, "ap2_hessgen.cpp", HESS_SOURCES, "ap2"),
+              (K3_HEADER, "kite3_jacgen.cpp", K3_SOURCES, "kite3")]
 # content hash of GEN_SOURCES recorded in the generated header's first line: the header is stale
 # when the hash differs (file times do not survive a checkout or the copy to the GPU box)
 _HASH_TAG = "// inputs-sha1: "
@@ -42,8 +48,8 @@ _COMMON = [os.path.join(CSRC, f) for f in ("ap2_model.hpp", "ap2_tables.hpp", "s
 TARGETS = {
     LIB: ([os.path.join(CSRC, "awegpu.hip")], _COMMON + [GEN_HEADER, HESS_HEADER]),
     LIB_MPC: ([os.path.join(CSRC, "awempc.hip")],
-              _COMMON + [os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp")]
-              + [os.path.join(INCLUDE, "awempc.h")]),
+              _COMMON + [os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp", "im_layout.hpp")]
+              + [os.path.join(INCLUDE, "awempc.h"), K3_HEADER]),
     LIB_DUAL: ([os.path.join(CSRC, "awedual.hip")],
                _COMMON + [os.path.join(CSRC, f) for f in ("dual_model.hpp", "dual_tables.hpp")]
                + [os.path.join(INCLUDE, "awedual.h")]),
@@ -98,12 +104,20 @@ def generate(force: bool = False, verbose: bool = False) -> str:
     is rewritten only if its content differs, so an unchanged model does not trigger a rebuild.
     Without a host C++ compiler the committed headers are kept (tests/test_codegen.py checks them
     against the model wherever g++ exists)."""
-    for header, gen, sources in GENERATORS:
-        _generate_one(header, gen, sources, force, verbose)
+    for header, gen, sources, model in GENERATORS:
+        _generate_one(header, gen, sources, force, verbose, model)
     return GEN_HEADER
 
 
-def _generate_one(header, gen, sources, force, verbose):
+def _default_constants(model):
+    if model == "kite3":
+        from . import kite3
+        return kite3.build_constants().consts
+    from . import problem as pb
+    return pb.build_constants(pb.Ap2Config()).consts
+
+
+def _generate_one(header, gen, sources, force, verbose, model="ap2"):
     import shutil
     want = gen_inputs_hash(sources)
     if not force and _header_hash(header) == want:
@@ -119,8 +133,7 @@ def _generate_one(header, gen, sources, force, verbose):
 
     import numpy as np
 
-    from . import problem as pb
-    consts = pb.build_constants(pb.Ap2Config())
+    consts = _default_constants(model)
     with tempfile.TemporaryDirectory() as tmp:
         exe = os.path.join(tmp, os.path.splitext(gen)[0])
         cmd = [cxx, "-O1", "-std=c++17", os.path.join(CSRC, "gen", gen), "-o", exe]
@@ -128,7 +141,7 @@ def _generate_one(header, gen, sources, force, verbose):
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         cfile = os.path.join(tmp, "consts.txt")
-        np.savetxt(cfile, consts.consts)
+        np.savetxt(cfile, consts)
         out = os.path.join(tmp, "gen.hpp")
         r = subprocess.run([exe, cfile, out], check=True, capture_output=True, text=True)
         if verbose:

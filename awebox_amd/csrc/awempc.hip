@@ -22,7 +22,9 @@
 
 #include "../../include/awegpu.h"
 #include "../../include/awempc.h"
+#include "im_layout.hpp"
 #include "kite3_model.hpp"
+#include "kite3_nodejac.gen.hpp"
 #include "kite3_tables.hpp"
 
 namespace {
@@ -476,6 +478,272 @@ __global__ __launch_bounds__(64) void mpc_hess_finalize_kernel(HArgs ha) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Generated instance-minor path (awempc_eval_nlp_im): one lane per MPC instance.
+//   mpc_gen_in (im::transpose_in_kernel): V, p -> VT[i * ld + b], PT[i * ld + b]
+//   mpc_gen_shoot_kernel / mpc_gen_radau_kernel: lane = instance, one wavefront per node, the node
+//     in the straight-line code generated from kite3_node (kite3_nodejac.gen.hpp:
+//     the node's rows and the values of its J_g pattern entries, no dual numbers, no zero
+//     tangents); each tangent slot goes straight to its J_g entries (1, or the d polynomial columns
+//     X_r, r != n, of a Radau node's xdot direction, scaled by C[r][n] / (h t_f)) through the
+//     node's destination row staged in LDS.  The shooting node's wavefront also writes the interval's
+//     tracking-cost gradient and partial sum, continuity rows and constant J_g entries.
+//   mpc_gen_finalize_kernel: objective (fixed order), terminal cost, global gradient rows.
+// J_g and grad f leave instance-minor (jac[e * ldj + b]), every store one 512-byte row; g stays
+// per-instance (g[b * n_g + i]) as the solver reads it.
+// ---------------------------------------------------------------------------------------------
+constexpr int kGenMaxTan = 128;
+static_assert(awe_k3gen::kNTan[0] <= kGenMaxTan && awe_k3gen::kNTan[1] <= kGenMaxTan, "slot table too small");
+
+// destination count of every tangent slot (1, or d for the xdot directions of a Radau node) and its
+// first entry in the node's destination row; compile-time on the device (the generated code's slot
+// numbers are constants), built with the run-time d on the host
+struct GenSlotTab {
+    int first[2][kGenMaxTan];
+    int cnt[2][kGenMaxTan];
+    int total[2];
+    __host__ __device__ constexpr GenSlotTab(int d) : first(), cnt(), total() {
+        for (int kind = 0; kind < 2; ++kind) {
+            int dir_of[kGenMaxTan] = {};
+            for (int s = 0; s < kGenMaxTan; ++s) dir_of[s] = -1;
+            for (int r = 0; r < kRowsPerNode; ++r)
+                for (int l = 0; l < kLanes; ++l)
+                    if (awe_k3gen::kTanIdx[kind][r][l] >= 0) dir_of[awe_k3gen::kTanIdx[kind][r][l]] = l;
+            int f = 0;
+            for (int s = 0; s < awe_k3gen::kNTan[kind]; ++s) {
+                const bool xd = kind == 1 && dir_of[s] >= K3_NX && dir_of[s] < 2 * K3_NX;
+                first[kind][s] = f;
+                cnt[kind][s] = xd ? d : 1;
+                f += cnt[kind][s];
+            }
+            total[kind] = f;
+        }
+    }
+};
+template <int D>
+constexpr GenSlotTab kGenSlots{D};
+
+struct GenArgs {
+    awt::DevColl coll;
+    int n_k, batch, n_v, n_g, n_p, stride, v_int0, rows, nib, dstride;
+    unsigned ld8;                // bytes between VT / PT / fpart rows
+    unsigned ldj8;               // bytes between J_g / grad rows
+    double kconst[8];            // constant J_g values: 1, -D[0..d]
+};
+
+// node inputs of node n of interval k (first column c0) from VT; n = 0 the shooting node
+template <int D>
+struct GenIn {
+    const double* v;
+    unsigned ld8, lb;
+    int c0, n;
+    double inv_h_tf;
+    const double* C;
+    __device__ __forceinline__ double at(int col) const { return im::at(v, (unsigned)col, ld8, lb); }
+    __device__ __forceinline__ double operator()(int i) const {
+        constexpr int NN = D + 1;
+        constexpr int CO = 2 * K3_NX + K3_NU + K3_NZ;          // x, u, xdot, z of the interval
+        if (n > 0) {
+            const int xc = c0 + CO + (n - 1) * (K3_NX + K3_NZ);
+            if (i < K3_NX) return at(xc + i);
+            if (i < 2 * K3_NX) {                               // xdot from the collocation polynomial
+                const int s = i - K3_NX;
+                double acc = 0.0;
+#pragma unroll
+                for (int r = 0; r < NN; ++r)
+                    acc += C[r * NN + n] * at(r == 0 ? c0 + s : c0 + CO + (r - 1) * (K3_NX + K3_NZ) + s);
+                return acc * inv_h_tf;
+            }
+            if (i == 2 * K3_NX + K3_NU) return at(xc + K3_NX);
+        } else {
+            if (i < K3_NX) return at(c0 + i);
+            if (i < 2 * K3_NX) return at(c0 + K3_NX + K3_NU + (i - K3_NX));
+            if (i == 2 * K3_NX + K3_NU) return at(c0 + 2 * K3_NX + K3_NU);
+        }
+        if (i < 2 * K3_NX + K3_NU) return at(c0 + K3_NX + (i - 2 * K3_NX));   // u[k], zero-order hold
+        if (i < K3_NW) return at(i - (2 * K3_NX + K3_NU + K3_NZ));             // theta: diam_t, t_f
+        return at(K3_NTH + 0);                                                 // phi.gamma
+    }
+};
+
+// tan[s] = v  ->  the J_g entries of slot s (dt: the node's destination row in LDS, byte offsets)
+template <int D, int KIND>
+struct GenJSink {
+    double* jac;
+    unsigned lb;
+    const unsigned* dt;
+    const double* xs;
+    struct Ref {
+        const GenJSink* s;
+        int slot;
+        __device__ __forceinline__ void operator=(double v) const { s->put(slot, v); }
+    };
+    __device__ __forceinline__ Ref operator[](int slot) const { return Ref{this, slot}; }
+    __device__ __forceinline__ void put(int slot, double v) const {
+        const int f = kGenSlots<D>.first[KIND][slot], c = kGenSlots<D>.cnt[KIND][slot];
+        if (c == 1) {
+            __builtin_nontemporal_store(v, &im::at_byte(jac, dt[f] + lb));
+            return;
+        }
+#pragma unroll
+        for (int q = 0; q < D; ++q) __builtin_nontemporal_store(xs[q] * v, &im::at_byte(jac, dt[f + q] + lb));
+    }
+};
+
+// Radau nodes: one workgroup per (instance block, interval k), wavefront w runs nodes 1 + w, 1 + w + W, ..
+// (one wavefront per SIMD: the node code keeps ~150 values live, more than 256 VGPRs once scheduled)
+template <int D>
+constexpr int gen_radau_waves() { return D < 4 ? D : 4; }
+constexpr int kGenShootWaves = 4;
+
+template <int D>
+__global__ __launch_bounds__(64 * gen_radau_waves<D>()) __attribute__((amdgpu_waves_per_eu(1)))
+void mpc_gen_radau_kernel(const double* __restrict__ VT, const double* __restrict__ PT,
+                          const double* __restrict__ cst, const unsigned* __restrict__ dtab,
+                          double* __restrict__ g, double* __restrict__ jac, GenArgs a) {
+    constexpr int NN = D + 1;
+    constexpr int W = gen_radau_waves<D>();
+    constexpr int T0 = kGenSlots<D>.total[0], T1 = kGenSlots<D>.total[1];
+    __shared__ unsigned ldt[D * T1];
+    const int total = a.nib * a.n_k;
+    const int t = im::xcd_tile(total);
+    if (t >= total) return;
+    const int ib = t / a.n_k, k = t - ib * a.n_k;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int m = 1; m < NN; ++m)
+        im::stage_offsets<64 * W>(ldt + (m - 1) * T1, dtab + (size_t)(k * NN + m) * a.dstride, T1, a.ldj8, tid);
+    __syncthreads();
+    (void)T0;
+    const int b = ib * 64 + lane;
+    if (b >= a.batch) return;
+    const unsigned lb = 8u * (unsigned)b, ld8 = a.ld8;
+    const int c0 = a.v_int0 + k * a.stride;
+    const double* C = a.coll.C;
+    const double tf = im::at(VT, 1u, ld8, lb);
+    const double inv_h_tf = (double)a.n_k / tf;
+    const double u_ref = im::at(PT, (unsigned)(K3_NX + a.n_v), ld8, lb);
+    double* gb = g + (size_t)b * a.n_g + K3_NX + k * a.rows + K3_N_EQ + K3_N_INEQ;
+    for (int n = 1 + wave; n < NN; n += W) {
+        double xs[D];                                 // C[r][n] / (h t_f) of the columns X_r, r != n
+#pragma unroll
+        for (int q = 0; q < D; ++q) xs[q] = C[(q < n ? q : q + 1) * NN + n] * inv_h_tf;
+        GenIn<D> in{VT, ld8, lb, c0, n, inv_h_tf, C};
+        GenJSink<D, 1> js{jac, lb, ldt + (n - 1) * T1, xs};
+        awe_k3gen::k3_node_radau<1>(in, u_ref, C[n * NN + n] * inv_h_tf, 1.0 / tf, cst, gb + (n - 1) * K3_N_EQ, js);
+    }
+}
+
+// shooting nodes: one wavefront per interval (kGenShootWaves intervals of one instance block per
+// workgroup); after the node, the interval's tracking-cost gradient and partial sum, continuity rows,
+// initial conditions and constant J_g entries
+template <int D>
+__global__ __launch_bounds__(64 * kGenShootWaves) __attribute__((amdgpu_waves_per_eu(1)))
+void mpc_gen_shoot_kernel(const double* __restrict__ VT, const double* __restrict__ PT,
+                          const double* __restrict__ cst, const unsigned* __restrict__ dtab,
+                          const unsigned* __restrict__ ctab, const int* __restrict__ coff, double* __restrict__ g,
+                          double* __restrict__ grad, double* __restrict__ jac, double* __restrict__ fpart, GenArgs a) {
+    constexpr int NN = D + 1;
+    constexpr int T0 = kGenSlots<D>.total[0];
+    constexpr int STRIDE = K3_NX + K3_NU + K3_NX + K3_NZ + D * (K3_NX + K3_NZ);
+    __shared__ unsigned ldt[kGenShootWaves * T0];
+    const int nk4 = (a.n_k + kGenShootWaves - 1) / kGenShootWaves;
+    const int total = a.nib * nk4;
+    const int t = im::xcd_tile(total);
+    if (t >= total) return;
+    const int ib = t / nk4, k0 = (t - ib * nk4) * kGenShootWaves;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int w = 0; w < kGenShootWaves && k0 + w < a.n_k; ++w)
+        im::stage_offsets<64 * kGenShootWaves>(ldt + w * T0, dtab + (size_t)((k0 + w) * NN) * a.dstride, T0, a.ldj8,
+                                              tid);
+    __syncthreads();
+    const int k = k0 + wave;
+    const int b = ib * 64 + lane;
+    if (k >= a.n_k || b >= a.batch) return;
+    const unsigned lb = 8u * (unsigned)b, ld8 = a.ld8;
+    const int c0 = a.v_int0 + k * a.stride;
+    const double* C = a.coll.C;
+    const double tf = im::at(VT, 1u, ld8, lb);
+    const double inv_h_tf = (double)a.n_k / tf;
+    const double u_ref = im::at(PT, (unsigned)(K3_NX + a.n_v), ld8, lb);
+    double* gb = g + (size_t)b * a.n_g;
+    const int row0 = K3_NX + k * a.rows;
+    {
+        GenIn<D> in{VT, ld8, lb, c0, 0, inv_h_tf, C};
+        GenJSink<D, 0> js{jac, lb, ldt + wave * T0, nullptr};
+        awe_k3gen::k3_node_shoot<1>(in, u_ref, cst, gb + row0, js);
+    }
+    auto V = [&](int col) { return im::at(VT, (unsigned)col, ld8, lb); };
+    auto Pp = [&](int row) { return im::at(PT, (unsigned)row, ld8, lb); };
+    // tracking objective of the interval's columns (pmpc.py:304-358), as mpc_interval_kernel
+    const double* w = a.coll.w;
+    const double invN = 1.0 / a.n_k;
+    double sw = 0.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) sw += w[j];
+    const int pref = K3_NX + c0;                       // p.ref row of column c0
+    const int pq = K3_NX + a.n_v + 1;                  // Q, then R
+    double fs = 0.0;
+    for (int c = 0; c < STRIDE; ++c) {
+        double gr = 0.0, ft = 0.0;
+        if (c >= K3_NX && c < K3_NX + K3_NU) {
+            const int i = c - K3_NX;
+            const double e = V(c0 + c) - Pp(pref + c), W = Pp(pq + K3_NX + i);
+            gr = 2.0 * sw * W * e * invN;
+            ft = sw * W * e * e;
+        } else if (c >= 2 * K3_NX + K3_NU + K3_NZ) {
+            const int q = c - (2 * K3_NX + K3_NU + K3_NZ);
+            const int j = q / (K3_NX + K3_NZ), e_ = q % (K3_NX + K3_NZ);
+            const double e = V(c0 + c) - Pp(pref + c), W = e_ < K3_NX ? Pp(pq + e_) : 1.0;
+            gr = 2.0 * w[j] * W * e * invN;
+            ft = w[j] * W * e * e;
+        }
+        __builtin_nontemporal_store(gr, &im::at(grad, (unsigned)(c0 + c), a.ldj8, lb));
+        fs += ft;
+    }
+    im::at(fpart, (unsigned)k, ld8, lb) = fs * invN;
+    // continuity x[k+1] - sum_r D_r X_{k,r} (collocation.py:319-336) and the initial conditions
+    const int gc = row0 + K3_N_EQ + K3_N_INEQ + D * K3_N_EQ;
+    constexpr int CO = 2 * K3_NX + K3_NU + K3_NZ;
+    for (int i = 0; i < K3_NX; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < NN; ++r) s += a.coll.D[r] * V(r == 0 ? c0 + i : c0 + CO + (r - 1) * (K3_NX + K3_NZ) + i);
+        gb[gc + i] = V(c0 + a.stride + i) - s;
+    }
+    if (k == 0)
+        for (int i = 0; i < K3_NX; ++i) gb[i] = V(c0 + i) - Pp(i);
+    // the interval's constant J_g entries (initial-condition and continuity rows)
+    for (int q = coff[k]; q < coff[k + 1]; ++q) {
+        const unsigned e = ctab[q];
+        __builtin_nontemporal_store(a.kconst[e >> 24], &im::at(jac, e & 0xffffffu, a.ldj8, lb));
+    }
+}
+
+// one lane per instance: objective partials in a fixed order, terminal cost, global gradient rows
+__global__ __launch_bounds__(64) void mpc_gen_finalize_kernel(const double* __restrict__ VT,
+                                                             const double* __restrict__ PT,
+                                                             const double* __restrict__ fpart, double* __restrict__ f,
+                                                             double* __restrict__ grad, GenArgs a) {
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= a.batch) return;
+    const unsigned lb = 8u * (unsigned)b;
+    double s = 0.0;
+    for (int k = 0; k < a.n_k; ++k) s += im::at(fpart, (unsigned)k, a.ld8, lb);
+    const int xN = a.v_int0 + a.n_k * a.stride;
+    const int pP = K3_NX + a.n_v + 1 + K3_NX + K3_NU;
+    for (int i = 0; i < K3_NX; ++i) {
+        const double e = im::at(VT, (unsigned)(xN + i), a.ld8, lb) - im::at(PT, (unsigned)(K3_NX + xN + i), a.ld8, lb);
+        const double W = im::at(PT, (unsigned)(pP + i), a.ld8, lb);
+        im::at(grad, (unsigned)(xN + i), a.ldj8, lb) = 2.0 * W * e;
+        s += W * e * e;
+    }
+    for (int i = 0; i < a.v_int0; ++i) im::at(grad, (unsigned)i, a.ldj8, lb) = 0.0;   // theta, phi, xi
+    f[b] = s;
+}
+
 }  // namespace
 
 struct awempc_handle_s {
@@ -502,7 +770,87 @@ struct awempc_handle_s {
     double *d_hsig = nullptr, *d_hlam = nullptr, *d_H = nullptr;
     hipEvent_t hev[2] = {nullptr, nullptr};
     bool htimed = false;
+    // generated instance-minor path (awempc_eval_nlp_im)
+    bool gen_ok = false;
+    std::string gen_why;
+    int gen_dstride = 0;
+    size_t gen_ld = 0;                       // row length of VT / PT / fpart
+    unsigned *d_gdtab = nullptr, *d_gctab = nullptr;
+    int* d_gcoff = nullptr;
+    double *d_VT = nullptr, *d_PT = nullptr, *d_gfpart = nullptr;
+    double gen_kconst[8] = {};
+    hipEvent_t gev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool gtimed = false;
 };
+
+namespace {
+
+// destination tables of the generated path from the gather list of build_tables: per (interval k,
+// node n) a row of CCS positions in kGenSlots order (slot s of the node's generated code, then its
+// d polynomial columns for a Radau xdot direction), and per interval the constant entries
+// (position | value index << 24, values 1, -D[r])
+int build_gen(awempc_handle_s* h) {
+    const Tables& T = h->t;
+    const int n_k = T.lay.n_k, d = T.lay.d, NN = d + 1;
+    if ((int)h->consts[K3_C_N_ELEMENTS] != awe_k3gen::kNElements) {
+        h->gen_why = "the generated node code has " + std::to_string(awe_k3gen::kNElements) +
+                     " tether elements, the constants " + std::to_string((int)h->consts[K3_C_N_ELEMENTS]);
+        return AWE_OK;
+    }
+    if ((size_t)T.row.size() >= (1u << 24)) { h->gen_why = "J_g too large for the constant table"; return AWE_OK; }
+    const GenSlotTab st(d);
+    const int dstride = std::max(st.total[0], st.total[1]);
+    std::vector<unsigned> dtab((size_t)n_k * NN * dstride, 0xffffffffu);
+    std::vector<unsigned> ctab;
+    std::vector<int> coff(n_k + 1, 0);
+    for (int k = 0; k < n_k; ++k) {
+        for (int e = T.goff[k]; e < T.goff[k + 1]; ++e) {
+            const unsigned pos = (unsigned)T.gslot[e];
+            const uint32_t cd = T.gcode[e];
+            const uint32_t kind = cd >> 29;
+            const int rr = (cd >> 25) & 15, idx = (int)(cd & ((1u << 21) - 1u));
+            if (kind == kKindOne || kind == kKindMinusD) {
+                ctab.push_back(pos | ((kind == kKindOne ? 0u : 1u + (unsigned)rr) << 24));
+                continue;
+            }
+            const int n = idx / (kRowsPerNode * kLanes), r = (idx / kLanes) % kRowsPerNode, l = idx % kLanes;
+            const int kd = n > 0 ? 1 : 0;
+            const int s = awe_k3gen::kTanIdx[kd][r][l];
+            if (s < 0) return fail(AWE_ERR_ARG, "internal: J_g entry without a generated tangent");
+            int q = 0;
+            if (kind == kKindTangPoly) q = rr < n ? rr : rr - 1;
+            if (q >= st.cnt[kd][s]) return fail(AWE_ERR_ARG, "internal: destination count of a generated tangent");
+            unsigned& slot = dtab[(size_t)(k * NN + n) * dstride + st.first[kd][s] + q];
+            if (slot != 0xffffffffu) return fail(AWE_ERR_ARG, "internal: two J_g entries for one generated destination");
+            slot = pos;
+        }
+        coff[k + 1] = (int)ctab.size();
+        for (int n = 0; n < NN; ++n)
+            for (int i = 0; i < st.total[n > 0 ? 1 : 0]; ++i)
+                if (dtab[(size_t)(k * NN + n) * dstride + i] == 0xffffffffu)
+                    return fail(AWE_ERR_ARG, "internal: generated destination without a J_g entry");
+    }
+    if (ctab.empty()) ctab.push_back(0);
+    for (auto& x : dtab) if (x == 0xffffffffu) x = 0;   // padding of the shorter node kind
+    h->gen_kconst[0] = 1.0;
+    for (int r = 0; r < NN; ++r) h->gen_kconst[1 + r] = -h->t.coll.D[r];
+    h->gen_dstride = dstride;
+    h->gen_ld = (size_t)h->batch;
+    MPC_TRY(hipMalloc((void**)&h->d_gdtab, sizeof(unsigned) * dtab.size()));
+    MPC_TRY(hipMemcpy(h->d_gdtab, dtab.data(), sizeof(unsigned) * dtab.size(), hipMemcpyHostToDevice));
+    MPC_TRY(hipMalloc((void**)&h->d_gctab, sizeof(unsigned) * ctab.size()));
+    MPC_TRY(hipMemcpy(h->d_gctab, ctab.data(), sizeof(unsigned) * ctab.size(), hipMemcpyHostToDevice));
+    MPC_TRY(hipMalloc((void**)&h->d_gcoff, sizeof(int) * coff.size()));
+    MPC_TRY(hipMemcpy(h->d_gcoff, coff.data(), sizeof(int) * coff.size(), hipMemcpyHostToDevice));
+    MPC_TRY(hipMalloc((void**)&h->d_VT, sizeof(double) * h->gen_ld * T.lay.n_v));
+    MPC_TRY(hipMalloc((void**)&h->d_PT, sizeof(double) * h->gen_ld * T.lay.n_p));
+    MPC_TRY(hipMalloc((void**)&h->d_gfpart, sizeof(double) * h->gen_ld * n_k));
+    for (auto& e : h->gev) MPC_TRY(hipEventCreate(&e));
+    h->gen_ok = true;
+    return AWE_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -555,6 +903,10 @@ int awempc_create(int n_k, int d, const double* consts, int n_consts, int batch,
 #undef MPC_UPLOAD
     MPC_TRY(hipMalloc((void**)&h->d_fpart, sizeof(double) * (size_t)batch * n_k));
     for (auto& e : h->ev) MPC_TRY(hipEventCreate(&e));
+    if (int rc = build_gen(h)) {
+        awempc_destroy(h);
+        return rc;
+    }
     *out = h;
     return AWE_OK;
 }
@@ -564,12 +916,15 @@ int awempc_destroy(awempc_handle h) {
     void* bufs[] = {h->d_cst, h->d_coll, h->d_goff, h->d_gslot, h->d_gcode, h->d_fpart,
                     h->d_V, h->d_P, h->d_f, h->d_g, h->d_grad, h->d_jac,
                     h->d_task, h->d_slot0, h->d_nslot, h->d_ent_off, h->d_term_off, h->d_hgslot, h->d_xnslot,
-                    h->d_terms, h->d_gpart, h->d_hsig, h->d_hlam, h->d_H};
+                    h->d_terms, h->d_gpart, h->d_hsig, h->d_hlam, h->d_H,
+                    h->d_gdtab, h->d_gctab, h->d_gcoff, h->d_VT, h->d_PT, h->d_gfpart};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : h->hev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : h->gev)
         if (e) (void)hipEventDestroy(e);
     delete h;
     return AWE_OK;
@@ -613,6 +968,84 @@ int awempc_eval_nlp(awempc_handle h, const double* V, const double* p, double* f
     MPC_TRY(hipGetLastError());
     MPC_TRY(hipEventRecord(h->ev[2], s));
     h->timed = true;
+    return AWE_OK;
+}
+
+int awempc_gen_status(awempc_handle h, int* available) {
+    if (!h || !available) return fail(AWE_ERR_ARG, "null argument");
+    *available = h->gen_ok ? 1 : 0;
+    if (!h->gen_ok) g_err = h->gen_why;
+    return AWE_OK;
+}
+
+int awempc_eval_nlp_im(awempc_handle h, const double* V, const double* p, double* f, double* g, double* grad_f,
+                       double* jac, size_t ld, void* stream) {
+    if (!h || !V || !p || !f || !g || !grad_f || !jac) return fail(AWE_ERR_ARG, "null argument");
+    if (!h->gen_ok) return fail(AWE_ERR_ARG, "generated path unavailable: " + h->gen_why);
+    const Tables& T = h->t;
+    const int B = h->batch;
+    if (ld < (size_t)B) return fail(AWE_ERR_ARG, "ld must be >= batch");
+    const size_t nrows = std::max((size_t)T.row.size(), (size_t)T.lay.n_v);
+    if (nrows * ld * 8 >= ((size_t)1 << 32)) return fail(AWE_ERR_ARG, "instance-minor J_g must stay below 4 GiB");
+    if ((size_t)std::max(T.lay.n_v, T.lay.n_p) * h->gen_ld * 8 >= ((size_t)1 << 32))
+        return fail(AWE_ERR_ARG, "instance-minor inputs must stay below 4 GiB");
+    hipStream_t s = (hipStream_t)stream;
+    GenArgs a{};
+    const int NN = T.lay.d + 1;
+    for (int j = 0; j < NN; ++j) {
+        for (int r = 0; r < NN; ++r) a.coll.C[j * NN + r] = T.coll.C[j][r];
+        a.coll.D[j] = T.coll.D[j];
+    }
+    for (int j = 0; j < T.lay.d; ++j) a.coll.w[j] = T.coll.w[j];
+    a.n_k = T.lay.n_k;
+    a.batch = B;
+    a.n_v = T.lay.n_v;
+    a.n_g = T.lay.n_g;
+    a.n_p = T.lay.n_p;
+    a.stride = T.lay.stride;
+    a.v_int0 = T.lay.v_int0;
+    a.rows = T.lay.rows;
+    a.nib = (B + 63) / 64;
+    a.dstride = h->gen_dstride;
+    a.ld8 = (unsigned)(8 * h->gen_ld);
+    a.ldj8 = (unsigned)(8 * ld);
+    for (int i = 0; i < 8; ++i) a.kconst[i] = h->gen_kconst[i];
+    MPC_TRY(hipEventRecord(h->gev[0], s));
+    const dim3 tgrid((unsigned)((T.lay.n_v + T.lay.n_p + 63) / 64), (unsigned)a.nib);
+    im::transpose_in_kernel<<<tgrid, 256, 0, s>>>(V, p, h->d_VT, h->d_PT, B, T.lay.n_v, T.lay.n_p, (int)h->gen_ld);
+    MPC_TRY(hipGetLastError());
+    MPC_TRY(hipEventRecord(h->gev[1], s));
+    const dim3 rgrid((unsigned)im::xcd_grid(a.nib * a.n_k));
+    const dim3 sgrid((unsigned)im::xcd_grid(a.nib * ((a.n_k + kGenShootWaves - 1) / kGenShootWaves)));
+#define MPC_GEN_NODE(DD)                                                                                           \
+    mpc_gen_shoot_kernel<DD><<<sgrid, 64 * kGenShootWaves, 0, s>>>(h->d_VT, h->d_PT, h->d_cst, h->d_gdtab,         \
+                                                                    h->d_gctab, h->d_gcoff, g, grad_f, jac,          \
+                                                                    h->d_gfpart, a);                                 \
+    mpc_gen_radau_kernel<DD><<<rgrid, 64 * gen_radau_waves<DD>(), 0, s>>>(h->d_VT, h->d_PT, h->d_cst, h->d_gdtab, g, \
+                                                                          jac, a)
+    switch (T.lay.d) {
+        case 2: MPC_GEN_NODE(2); break;
+        case 3: MPC_GEN_NODE(3); break;
+        case 4: MPC_GEN_NODE(4); break;
+        case 5: MPC_GEN_NODE(5); break;
+        default: return fail(AWE_ERR_ARG, "unsupported d");
+    }
+#undef MPC_GEN_NODE
+    MPC_TRY(hipGetLastError());
+    MPC_TRY(hipEventRecord(h->gev[2], s));
+    mpc_gen_finalize_kernel<<<dim3((unsigned)a.nib), 64, 0, s>>>(h->d_VT, h->d_PT, h->d_gfpart, f, grad_f, a);
+    MPC_TRY(hipGetLastError());
+    MPC_TRY(hipEventRecord(h->gev[3], s));
+    h->gtimed = true;
+    return AWE_OK;
+}
+
+int awempc_last_kernel_ms_im(awempc_handle h, float* ms_in, float* ms_node, float* ms_fin) {
+    if (!h || !h->gtimed) return fail(AWE_ERR_ARG, "no timed instance-minor evaluation yet");
+    MPC_TRY(hipEventSynchronize(h->gev[3]));
+    if (ms_in) MPC_TRY(hipEventElapsedTime(ms_in, h->gev[0], h->gev[1]));
+    if (ms_node) MPC_TRY(hipEventElapsedTime(ms_node, h->gev[1], h->gev[2]));
+    if (ms_fin) MPC_TRY(hipEventElapsedTime(ms_fin, h->gev[2], h->gev[3]));
     return AWE_OK;
 }
 

@@ -53,27 +53,27 @@ template <class T>
 AWE_HD T k3_dot(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
 // ISA density (atmosphere.py:60-78)
-template <class T>
-AWE_HD T k3_density(const T& zz, const double* c) {
-    const double expo = c[K3_C_G] / c[K3_C_GAMMA_AIR] / c[K3_C_R_AIR] - 1.0;
+template <class T, class CT>
+AWE_HD T k3_density(const T& zz, const CT* c) {
+    const CT expo = c[K3_C_G] / c[K3_C_GAMMA_AIR] / c[K3_C_R_AIR] - 1.0;
     T ratio = 1.0 - zz * (c[K3_C_GAMMA_AIR] / c[K3_C_T_REF]);
     return c[K3_C_RHO_REF] * exp(expo * log(ratio));
 }
 
 // log wind u_ref log10(smooth_abs(zz, 1) / z0) / log10(z_ref / z0) (wind.py:184-208), written as
 // u_ref (0.5 log(zz^2 + 1) - log z0) / log(z_ref / z0)
-template <class T>
-AWE_HD T k3_wind(const T& zz, double u_ref, const double* c) {
-    const double lz0 = ::log(c[K3_C_Z0_AIR]);
-    const double scale = u_ref / (::log(c[K3_C_Z_REF]) - lz0);
+template <class T, class UT, class CT>
+AWE_HD T k3_wind(const T& zz, const UT& u_ref, const CT* c) {
+    const CT lz0 = log(c[K3_C_Z0_AIR]);
+    const auto scale = u_ref / (log(c[K3_C_Z_REF]) - lz0);
     return scale * (0.5 * log(zz * zz + 1.0) - lz0);
 }
 
 // 'multi' tether drag, element e of n_el on the main tether, lumped onto the kite node with the
 // reference's shape factor (element.py:60-104, segment.py:38-65); ground end at rest
-template <class T>
-AWE_HD void k3_tether_element(int e, int n_el, const T* q, const T* v, const T& diam, double u_ref,
-                              const double* c, T out[3]) {
+template <class T, class UT, class CT>
+AWE_HD void k3_tether_element(int e, int n_el, const T* q, const T* v, const T& diam, const UT& u_ref,
+                              const CT* c, T out[3]) {
     const double ds = 1.0 / n_el;
     const double s0 = 0.5 * ds, step = ((1.0 - 0.5 * ds) - s0) / (n_el - 1);
     const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
@@ -97,9 +97,9 @@ AWE_HD void k3_tether_element(int e, int n_el, const T* q, const T* v, const T& 
 // the main tether's drag summed over its elements, evaluated inside the node model (host
 // structure, CPU paths); the GPU kernel substitutes values + partials preaccumulated per node
 struct K3InlineDrag {
-    template <class T>
-    AWE_HD void operator()(const T* q, const T* v, const T& diam, double u_ref, const double* c, T D[3]) const {
-        const int n_el = (int)c[K3_C_N_ELEMENTS];
+    template <class T, class UT, class CT>
+    AWE_HD void operator()(const T* q, const T* v, const T& diam, const UT& u_ref, const CT* c, T D[3]) const {
+        const int n_el = structural(c[K3_C_N_ELEMENTS]);
         for (int i = 0; i < 3; ++i) D[i] = T(0.0);
         for (int e = 0; e < n_el; ++e) {
             T ce[3];
@@ -109,21 +109,23 @@ struct K3InlineDrag {
     }
 };
 
-template <class T, class In, class Sink, class Drag = K3InlineDrag>
-AWE_HD void kite3_node(const In& in, const T& gamma, double u_ref, const double* c, Sink& out, bool want_ineq,
+// u_ref and the constants c are doubles on the device and Sym leaves in the code generator
+// (gen/kite3_jacgen.cpp), which loads them at run time
+template <class T, class In, class Sink, class Drag = K3InlineDrag, class UT = double, class CT = double>
+AWE_HD void kite3_node(const In& in, const T& gamma, const UT& u_ref, const CT* c, Sink& out, bool want_ineq,
                        const Drag& drag = Drag()) {
     using namespace k3;
-    const double* s = c + K3_C_SCALING;
+    const CT* s = c + K3_C_SCALING;
     auto SI = [&](int i) -> T { return in(i) * s[i]; };
 
     // ---- trivial kinematics (lagr_dyn.py:141-169), sorted xdot names -------------------------
     for (int i = 0; i < 2; ++i)
-        out.eq_row(4 + i, (SI(XD_DCOEFF + i) - SI(U_DCOEFF + i)) / ::sqrt(s[U_DCOEFF + i] * s[XD_DCOEFF + i]));
-    out.eq_row(6, (SI(XD_DDDLT) - SI(U_DDDLT)) / ::sqrt(s[U_DDDLT] * s[XD_DDDLT]));
-    out.eq_row(7, (SI(XD_DDLT) - SI(DDLT)) / ::sqrt(s[DDLT] * s[XD_DDLT]));
-    out.eq_row(8, (SI(XD_DLT) - SI(DLT)) / ::sqrt(s[DLT] * s[XD_DLT]));
+        out.eq_row(4 + i, (SI(XD_DCOEFF + i) - SI(U_DCOEFF + i)) / sqrt(s[U_DCOEFF + i] * s[XD_DCOEFF + i]));
+    out.eq_row(6, (SI(XD_DDDLT) - SI(U_DDDLT)) / sqrt(s[U_DDDLT] * s[XD_DDDLT]));
+    out.eq_row(7, (SI(XD_DDLT) - SI(DDLT)) / sqrt(s[DDLT] * s[XD_DDLT]));
+    out.eq_row(8, (SI(XD_DLT) - SI(DLT)) / sqrt(s[DLT] * s[XD_DLT]));
     for (int i = 0; i < 3; ++i)
-        out.eq_row(9 + i, (SI(XD_DQ + i) - SI(DQ + i)) / ::sqrt(s[DQ + i] * s[XD_DQ + i]));
+        out.eq_row(9 + i, (SI(XD_DQ + i) - SI(DQ + i)) / sqrt(s[DQ + i] * s[XD_DQ + i]));
 
     T q[3], v[3];
     for (int i = 0; i < 3; ++i) q[i] = SI(Q + i);
@@ -165,17 +167,17 @@ AWE_HD void kite3_node(const In& in, const T& gamma, double u_ref, const double*
         T nq = sqrt(k3_dot(q, q));
         T diam = SI(TH_DIAM);
         T area = (k3::kPi * 0.25) * diam * diam;
-        const double ls = c[K3_C_LAMBDA_SCALING] * c[K3_C_SCALING_LENGTH];
-        const double char_tension = ::sqrt(ls * ls + 1e-16);    // smooth_abs
+        const CT ls = c[K3_C_LAMBDA_SCALING] * c[K3_C_SCALING_LENGTH];
+        const CT char_tension = sqrt(ls * ls + 1e-16);          // smooth_abs
         out.ineq_row(0, (SI(Z_LAMBDA) * nq - area * c[K3_C_STRESS_MAX]) / char_tension);
         T a[3];
         for (int i = 0; i < 3; ++i) a[i] = SI(XD_DDQ + i);
-        const double amax = c[K3_C_ACC_MAX];
+        const CT amax = c[K3_C_ACC_MAX];
         out.ineq_row(1, k3_dot(a, a) / (amax * amax) - 1.0);
     }
 
     // ---- translational Lagrangian dynamics (lagr_dyn.py:68-109, 174-204) ---------------------
-    const double g_grav = c[K3_C_G], m_k = c[K3_C_M_K], rho_t = c[K3_C_RHO_TETHER];
+    const CT g_grav = c[K3_C_G], m_k = c[K3_C_M_K], rho_t = c[K3_C_RHO_TETHER];
     T diam = SI(TH_DIAM);
     T D_tether[3];
     drag(q, v, diam, u_ref, c, D_tether);
@@ -198,9 +200,9 @@ AWE_HD void kite3_node(const In& in, const T& gamma, double u_ref, const double*
     T pq = g_grav * mu * (q[2] * inv_n) * 0.5;
     T pz = g_grav * mu * nq * 0.5 + g_grav * m_k;
     T mass_flow = mu * sv * inv_n;                                // d(m_t)/dt
-    const double sd = c[K3_C_SCALING_DIAM];
-    const double scaling_mass = (k3::kPi * 0.25) * sd * sd * rho_t * c[K3_C_SCALING_LENGTH];
-    const double inv_force_scaling = 1.0 / ((scaling_mass / 2.0 + m_k) * c[K3_C_G_SCALING] * 10.0);
+    const CT sd = c[K3_C_SCALING_DIAM];
+    const CT scaling_mass = (k3::kPi * 0.25) * sd * sd * rho_t * c[K3_C_SCALING_LENGTH];
+    const CT inv_force_scaling = 1.0 / ((scaling_mass / 2.0 + m_k) * c[K3_C_G_SCALING] * 10.0);
     for (int i = 0; i < 3; ++i) {
         T ddt = cv * v[i] + cq * q[i] + ca * a[i];
         T dLdq = kq * q[i] + kv * v[i] - pq * q[i] - lam * q[i];
@@ -214,8 +216,8 @@ AWE_HD void kite3_node(const In& in, const T& gamma, double u_ref, const double*
         T c0 = 0.5 * (qq - l_t * l_t);
         T c1 = sv - l_t * dl_t;
         T c2 = vv + qa - dl_t * dl_t - l_t * ddl_t;
-        const double kap = c[K3_C_KAPPA];
-        const double hscale = kap * kap * (c[K3_C_SCALING_LENGTH] * c[K3_C_Q_SCALING_MEAN]);
+        const CT kap = c[K3_C_KAPPA];
+        const CT hscale = kap * kap * (c[K3_C_SCALING_LENGTH] * c[K3_C_Q_SCALING_MEAN]);
         out.eq_row(3, (c2 + 2.0 * kap * c1 + kap * kap * c0) / hscale);
     }
 }

@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = ["awe_create", "awe_destroy", "awe_last_error", "awe_sizes", 
                     "awe_last_kernel_ms", "awe_device_count", "awe_hess_nnz", "awe_sparsity_hess",
                     "awe_sparsity_hess_static", "awe_eval_hess", "awe_eval_hess_host", "awe_last_hess_ms",
                     "awe_set_eval_path", "awe_get_eval_path", "awe_last_kernel_ms_gen", "awe_eval_nlp_im",
-                    "awe_last_kernel_ms_soa"]
+                    "awe_last_kernel_ms_soa", "awe_eval_hess_im", "awe_set_hess_path", "awe_get_hess_path"]
 
 PATH_COLOUR, PATH_GENERATED, PATH_SOA = 0, 1, 2
 

@@ -204,8 +204,9 @@ class BatchedRti:
         self.P = torch.zeros(B, self.ev.n_p, **f64)
         self.f = torch.zeros(B, **f64)
         self.g = torch.zeros(B, n_g, **f64)
-        self.grad = torch.zeros(B, n_v, **f64)
-        self.jac = torch.zeros(B, self.ev.nnz, **f64)
+        # the evaluator's preferred layout (instance-minor for the HIP MPC evaluator's generated path)
+        self.grad = self.ev.alloc_grad(self.dev) if hasattr(self.ev, "alloc_grad") else torch.zeros(B, n_v, **f64)
+        self.jac = self.ev.alloc_jac(self.dev) if hasattr(self.ev, "alloc_jac") else torch.zeros(B, self.ev.nnz, **f64)
         self.free_t, self.eq_t = t(self.free), t(self.eq)
         self.path_t = t(path)
         self.u0_idx = t(lay.u(0))

@@ -24,6 +24,8 @@
 #ifndef AWEMPC_H
 #define AWEMPC_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -92,6 +94,20 @@ int awempc_eval_nlp_host(awempc_handle h, const double* V, const double* p, doub
                          double* grad_f, double* jac);
 /* kernel time of the last awempc_eval_nlp (HIP events on its stream), ms */
 int awempc_last_kernel_ms(awempc_handle h, float* ms_main, float* ms_finalize);
+
+/* ---- generated instance-minor path ------------------------------------------------------------
+ * The same f, g, grad f and J_g values from straight-line node code generated from the model
+ * (csrc/gen/kite3_jacgen.cpp: the sparse Jacobian of each node, one lane per instance) instead of the
+ * dual-number kernel of awempc_eval_nlp.  grad_f and jac are instance-minor: grad_f[i * ld + b],
+ * jac[e * ld + b], ld >= batch (each J_g / gradient row of all instances contiguous, the layout the
+ * batched solvers read); V, p, f, g as above.  Device pointers, asynchronous on `stream`.
+ * awempc_gen_status sets *available = 0 (awempc_last_error() says why) when the model constants do
+ * not have the integer structure the code was generated for. */
+int awempc_gen_status(awempc_handle h, int* available);
+int awempc_eval_nlp_im(awempc_handle h, const double* V, const double* p, double* f, double* g, double* grad_f,
+                       double* jac, size_t ld, void* stream);
+/* kernel times of the last awempc_eval_nlp_im: input transposition, node kernel, finalize (ms) */
+int awempc_last_kernel_ms_im(awempc_handle h, float* ms_in, float* ms_node, float* ms_finalize);
 
 /* ---- nlp_hess_l ----------------------------------------------------------------------------------
  * Hessian of sigma f + lam^T g w.r.t. V, upper triangle (row <= col), CCS over the n_v columns:

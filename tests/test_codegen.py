@@ -101,3 +101,46 @@ def test_generated_hessian_matches_hyperdual_model(hess_checker, k, seed):
         assert r["hess_rel"] < 1e-12, (kind, r)
         assert r["grad_rel"] < 1e-12, (kind, r)
         assert r["hess_max"] > 1.0 and r["nonzero"] > 150, (kind, r)
+
+
+# ---- tracking MPC (3-DOF kite): csrc/gen/kite3_jacgen.cpp -> kite3_nodejac.gen.hpp ----------------
+@pytest.fixture(scope="module")
+def k3_checker(tmp_path_factory):
+    tmp = tmp_path_factory.mktemp("k3gen")
+    exe = str(tmp / "check_k3")
+    subprocess.run(["g++", "-O1", "-std=c++17", os.path.join(CSRC, "gen", "check_kite3_gen.cpp"), "-o", exe],
+                   check=True)
+    return tmp, exe
+
+
+def test_committed_kite3_header_is_current():
+    """kite3_nodejac.gen.hpp in the tree is what gen/kite3_jacgen.cpp writes for the current model."""
+    before = open(B.K3_HEADER).read()
+    B.generate(force=True)
+    assert open(B.K3_HEADER).read() == before, "kite3_nodejac.gen.hpp is stale: run python -m awebox_amd.build"
+
+
+@pytest.mark.parametrize("k,seed", [(0, 0), (9, 1), (19, 2)])
+def test_generated_kite3_jacobian_matches_dual_model(k3_checker, k, seed):
+    """Every entry of the MPC node Jacobian pattern (both node kinds) against one dual-number pass of
+    kite3_node per seed direction (csrc/gen/check_kite3_gen.cpp)."""
+    from awebox_amd import kite3 as k3
+    tmp, exe = k3_checker
+    c = k3.build_constants()
+    lay = k3.MpcLayout(20, 4)
+    V, p = k3.batch_instance(c, lay, k, 8)
+    rng = np.random.default_rng(seed)
+    w = np.concatenate([V[lay.x(k)], V[lay.xdot(k)], V[lay.u(k)], V[lay.z(k)], V[lay.theta()], V[lay.phi()][:1]])
+    w = w * (1 + 0.05 * rng.standard_normal(w.shape)) + 0.01 * rng.standard_normal(w.shape)
+    np.savetxt(str(tmp / "consts.txt"), c.consts)
+    np.savetxt(str(tmp / "w.txt"), w)
+    u_ref, cxx, inv_tf = 4.0 + 4.0 * rng.random(), 2.0 + rng.random(), 1.0 / (0.5 + rng.random())
+    out = subprocess.run([exe, str(tmp / "consts.txt"), str(tmp / "w.txt"), repr(u_ref), repr(cxx), repr(inv_tf)],
+                         check=True, capture_output=True, text=True)
+    rec = json.loads(out.stdout)
+    for kind in ("shooting", "radau"):
+        r = rec[kind]
+        assert r["entries"] == r["n_tan"], "every tangent slot is a pattern entry"
+        assert r["value_rel"] < 1e-14, (kind, r)
+        assert r["tangent_rel"] < 1e-12, (kind, r)
+        assert r["tangent_max"] > 1.0

@@ -225,6 +225,49 @@ def test_mpc_batch256_device_path_deterministic(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_k,d,batch", [(20, 4, 130), (3, 2, 70), (5, 3, 65), (4, 5, 3)])
+def test_mpc_generated_path_matches_oracle_and_dual_kernel(gpu, n_k, d, batch):
+    """awempc_eval_nlp_im (generated node code, instance-minor J_g and grad f; ragged last instance
+    block) against the oracle for three instances and against the dual-number kernel for all."""
+    from awebox_amd.mpc import MpcEvaluator
+    c, lay, orc = _setup(n_k, d)
+    inst = [k3.batch_instance(c, lay, i * 13, 64) for i in range(batch)]
+    V = np.stack([v for v, _ in inst])
+    P = np.stack([p for _, p in inst])
+    P[:, lay.p_u_ref] = np.linspace(4.0, 8.0, batch)
+    rng = np.random.default_rng(5)
+    P[:, lay.p_Q:lay.p_Q + 11] = rng.uniform(0.5, 2.0, (batch, 11))
+    ev = MpcEvaluator(c, batch=batch)
+    assert ev.generated_available
+    dev = torch.device("cuda", 0)
+    Vt, Pt = torch.tensor(V, device=dev), torch.tensor(P, device=dev)
+    out = {}
+    for im in (True, False):
+        f = torch.empty(batch, dtype=torch.float64, device=dev)
+        g = torch.full((batch, ev.n_g), float("nan"), dtype=torch.float64, device=dev)
+        gr, jac = ev.alloc_grad(dev, instance_minor=im), ev.alloc_jac(dev, instance_minor=im)
+        gr.fill_(float("nan"))
+        jac.fill_(float("nan"))
+        ev.eval_nlp_device(Vt, Pt, f, g, gr, jac)
+        torch.cuda.synchronize()
+        out[im] = [t.cpu().numpy() for t in (f, g, gr, jac)]
+    fi, gi, gri, ji = out[True]
+    assert np.isfinite(gi).all() and np.isfinite(gri).all() and np.isfinite(ji).all()
+    fd, gd, grd, jd = out[False]
+    assert np.allclose(fi, fd, rtol=1e-13, atol=0)
+    for b in range(batch):
+        _close(gi[b], gd[b], f"g[{b}] vs dual")
+        _close(gri[b], grd[b], f"grad_f[{b}] vs dual")
+        _close(ji[b], jd[b], f"jac[{b}] vs dual")
+    for b in sorted({0, batch // 2, batch - 1}):
+        _close(gi[b], orc.nlp_g(V[b], P[b], lay).numpy(), f"g[{b}]")
+        fo = float(orc.nlp_f(V[b], P[b], lay))
+        assert abs(fi[b] - fo) <= 1e-12 * abs(fo)
+        _close(gri[b], orc.nlp_grad_f(V[b], P[b], lay).numpy(), f"grad_f[{b}]")
+        _close_jac(ev.jac_csc(ji[b]), orc.nlp_jac_g(V[b], P[b], lay))
+
+
+@pytest.mark.gpu
 def test_mpc_nonfinite_is_an_error(gpu):
     from awebox_amd.evaluator import AwegpuError
     from awebox_amd.mpc import MpcEvaluator
