@@ -17,6 +17,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -591,33 +592,62 @@ struct GenJSink {
     }
 };
 
-// Radau nodes: one workgroup per (instance block, interval k), wavefront w runs nodes 1 + w, 1 + w + W, ..
-// (one wavefront per SIMD: the node code keeps ~150 values live, more than 256 VGPRs once scheduled)
+// node inputs preloaded into registers: every load of the node issued at once (one memory latency)
+// instead of at the generated code's first use of each input (one exposed latency per input)
 template <int D>
-constexpr int gen_radau_waves() { return D < 4 ? D : 4; }
-constexpr int kGenShootWaves = 4;
+struct GenInPre {
+    double w[K3_NW + 1];
+    __device__ __forceinline__ explicit GenInPre(const GenIn<D>& in) {
+#pragma unroll
+        for (int i = 0; i <= K3_NW; ++i) w[i] = in(i);
+    }
+    __device__ __forceinline__ double operator()(int i) const { return w[i]; }
+};
+
+#ifndef AWE_MPC_PRELOAD
+#define AWE_MPC_PRELOAD 1
+#endif
+#ifndef AWE_MPC_STRIP_WAVES
+#define AWE_MPC_STRIP_WAVES 1
+#endif
+
+// calls f(std::integral_constant<int, s>) for the direction strip s == sg of the generated code
+template <int S, int I = 0, class F>
+__device__ __forceinline__ void gen_strip(int sg, const F& f) {
+    if constexpr (I < S) {
+        if (sg == I) f(std::integral_constant<int, I>{});
+        else gen_strip<S, I + 1>(sg, f);
+    }
+}
+
+// Strip groups: with AWE_MPC_STRIP_WAVES the kNStrips direction strips of a node run in separate
+// workgroups side by side (each recomputes the values it needs: more, shorter wavefronts -- at the
+// config-5 batch of 256 instances one node per wavefront leaves most SIMDs idle and the kernel is the
+// latency of one wavefront); otherwise one wavefront runs the strips of its node in turn.
+constexpr int kGenStripGroups = AWE_MPC_STRIP_WAVES ? awe_k3gen::kNStrips : 1;
+constexpr int kGenNodeWaves = 4;
+constexpr int kGenShootWaves = kGenNodeWaves;
+template <int D>
+constexpr int gen_radau_waves() { return D < kGenNodeWaves ? D : kGenNodeWaves; }
 
 template <int D>
-__global__ __launch_bounds__(64 * gen_radau_waves<D>()) __attribute__((amdgpu_waves_per_eu(1)))
-void mpc_gen_radau_kernel(const double* __restrict__ VT, const double* __restrict__ PT,
-                          const double* __restrict__ cst, const unsigned* __restrict__ dtab,
-                          double* __restrict__ g, double* __restrict__ jac, GenArgs a) {
+__device__ __forceinline__ void gen_radau_tile(int t, unsigned* ldt, const double* __restrict__ VT,
+                                               const double* __restrict__ PT, const double* __restrict__ cst,
+                                               const unsigned* __restrict__ dtab, double* __restrict__ g,
+                                               double* __restrict__ jac, const GenArgs& a) {
     constexpr int NN = D + 1;
     constexpr int W = gen_radau_waves<D>();
-    constexpr int T0 = kGenSlots<D>.total[0], T1 = kGenSlots<D>.total[1];
-    __shared__ unsigned ldt[D * T1];
-    const int total = a.nib * a.n_k;
-    const int t = im::xcd_tile(total);
-    if (t >= total) return;
-    const int ib = t / a.n_k, k = t - ib * a.n_k;
+    constexpr int T1 = kGenSlots<D>.total[1];
+    const int sg = t % kGenStripGroups, tk = t / kGenStripGroups;
+    const int ib = tk / a.n_k, k = tk - ib * a.n_k;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int m = 1; m < NN; ++m)
-        im::stage_offsets<64 * W>(ldt + (m - 1) * T1, dtab + (size_t)(k * NN + m) * a.dstride, T1, a.ldj8, tid);
+        im::stage_offsets<64 * kGenNodeWaves>(ldt + (m - 1) * T1, dtab + (size_t)(k * NN + m) * a.dstride, T1,
+                                              a.ldj8, tid);
     __syncthreads();
-    (void)T0;
     const int b = ib * 64 + lane;
-    if (b >= a.batch) return;
+    if (wave >= W || b >= a.batch) return;
     const unsigned lb = 8u * (unsigned)b, ld8 = a.ld8;
     const int c0 = a.v_int0 + k * a.stride;
     const double* C = a.coll.C;
@@ -629,34 +659,58 @@ void mpc_gen_radau_kernel(const double* __restrict__ VT, const double* __restric
         double xs[D];                                 // C[r][n] / (h t_f) of the columns X_r, r != n
 #pragma unroll
         for (int q = 0; q < D; ++q) xs[q] = C[(q < n ? q : q + 1) * NN + n] * inv_h_tf;
-        GenIn<D> in{VT, ld8, lb, c0, n, inv_h_tf, C};
+        const GenIn<D> gin{VT, ld8, lb, c0, n, inv_h_tf, C};
+#if AWE_MPC_PRELOAD
+        const GenInPre<D> in(gin);
+#else
+        const GenIn<D>& in = gin;
+#endif
         GenJSink<D, 1> js{jac, lb, ldt + (n - 1) * T1, xs};
-        awe_k3gen::k3_node_radau<1>(in, u_ref, C[n * NN + n] * inv_h_tf, 1.0 / tf, cst, gb + (n - 1) * K3_N_EQ, js);
+        const double cxx = C[n * NN + n] * inv_h_tf, itf = 1.0 / tf;
+        auto run = [&](auto st) {
+            awe_k3gen::k3_node_radau<1, decltype(st)::value>(in, u_ref, cxx, itf, cst, gb + (n - 1) * K3_N_EQ, js);
+        };
+        if constexpr (kGenStripGroups > 1) {
+            gen_strip<awe_k3gen::kNStrips>(sg, run);
+        } else {
+            gen_strip<awe_k3gen::kNStrips>(0, run);
+            if constexpr (awe_k3gen::kNStrips > 1) gen_strip<awe_k3gen::kNStrips, 1>(1, run);
+            if constexpr (awe_k3gen::kNStrips > 2) gen_strip<awe_k3gen::kNStrips, 2>(2, run);
+            if constexpr (awe_k3gen::kNStrips > 3) gen_strip<awe_k3gen::kNStrips, 3>(3, run);
+            static_assert(awe_k3gen::kNStrips <= 4, "strip loop");
+        }
     }
 }
 
-// shooting nodes: one wavefront per interval (kGenShootWaves intervals of one instance block per
-// workgroup); after the node, the interval's tracking-cost gradient and partial sum, continuity rows,
-// initial conditions and constant J_g entries
+#ifndef AWE_MPC_EXTRA_TILES
+#define AWE_MPC_EXTRA_TILES 1
+#endif
 template <int D>
-__global__ __launch_bounds__(64 * kGenShootWaves) __attribute__((amdgpu_waves_per_eu(1)))
-void mpc_gen_shoot_kernel(const double* __restrict__ VT, const double* __restrict__ PT,
-                          const double* __restrict__ cst, const unsigned* __restrict__ dtab,
-                          const unsigned* __restrict__ ctab, const int* __restrict__ coff, double* __restrict__ g,
-                          double* __restrict__ grad, double* __restrict__ jac, double* __restrict__ fpart, GenArgs a) {
+__device__ __forceinline__ void gen_interval_extras(int k, int b, const double* __restrict__ VT,
+                                                    const double* __restrict__ PT, const unsigned* __restrict__ ctab,
+                                                    const int* __restrict__ coff, double* __restrict__ g,
+                                                    double* __restrict__ grad, double* __restrict__ jac,
+                                                    double* __restrict__ fpart, const GenArgs& a);
+
+// shooting nodes: one wavefront per interval (kGenShootWaves intervals of one instance block per
+// workgroup); strip group 0 then writes the interval's tracking-cost gradient and partial sum,
+// continuity rows, initial conditions and constant J_g entries
+template <int D>
+__device__ __forceinline__ void gen_shoot_tile(int t, unsigned* ldt, const double* __restrict__ VT,
+                                               const double* __restrict__ PT, const double* __restrict__ cst,
+                                               const unsigned* __restrict__ dtab, const unsigned* __restrict__ ctab,
+                                               const int* __restrict__ coff, double* __restrict__ g,
+                                               double* __restrict__ grad, double* __restrict__ jac,
+                                               double* __restrict__ fpart, const GenArgs& a) {
     constexpr int NN = D + 1;
     constexpr int T0 = kGenSlots<D>.total[0];
-    constexpr int STRIDE = K3_NX + K3_NU + K3_NX + K3_NZ + D * (K3_NX + K3_NZ);
-    __shared__ unsigned ldt[kGenShootWaves * T0];
     const int nk4 = (a.n_k + kGenShootWaves - 1) / kGenShootWaves;
-    const int total = a.nib * nk4;
-    const int t = im::xcd_tile(total);
-    if (t >= total) return;
-    const int ib = t / nk4, k0 = (t - ib * nk4) * kGenShootWaves;
+    const int sg = t % kGenStripGroups, tk = t / kGenStripGroups;
+    const int ib = tk / nk4, k0 = (tk - ib * nk4) * kGenShootWaves;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int w = 0; w < kGenShootWaves && k0 + w < a.n_k; ++w)
-        im::stage_offsets<64 * kGenShootWaves>(ldt + w * T0, dtab + (size_t)((k0 + w) * NN) * a.dstride, T0, a.ldj8,
+        im::stage_offsets<64 * kGenNodeWaves>(ldt + w * T0, dtab + (size_t)((k0 + w) * NN) * a.dstride, T0, a.ldj8,
                                               tid);
     __syncthreads();
     const int k = k0 + wave;
@@ -671,10 +725,41 @@ void mpc_gen_shoot_kernel(const double* __restrict__ VT, const double* __restric
     double* gb = g + (size_t)b * a.n_g;
     const int row0 = K3_NX + k * a.rows;
     {
-        GenIn<D> in{VT, ld8, lb, c0, 0, inv_h_tf, C};
+        const GenIn<D> gin{VT, ld8, lb, c0, 0, inv_h_tf, C};
+#if AWE_MPC_PRELOAD
+        const GenInPre<D> in(gin);
+#else
+        const GenIn<D>& in = gin;
+#endif
         GenJSink<D, 0> js{jac, lb, ldt + wave * T0, nullptr};
-        awe_k3gen::k3_node_shoot<1>(in, u_ref, cst, gb + row0, js);
+        auto run = [&](auto st) { awe_k3gen::k3_node_shoot<1, decltype(st)::value>(in, u_ref, cst, gb + row0, js); };
+        if constexpr (kGenStripGroups > 1) {
+            gen_strip<awe_k3gen::kNStrips>(sg, run);
+        } else {
+            gen_strip<awe_k3gen::kNStrips>(0, run);
+            if constexpr (awe_k3gen::kNStrips > 1) gen_strip<awe_k3gen::kNStrips, 1>(1, run);
+            if constexpr (awe_k3gen::kNStrips > 2) gen_strip<awe_k3gen::kNStrips, 2>(2, run);
+            if constexpr (awe_k3gen::kNStrips > 3) gen_strip<awe_k3gen::kNStrips, 3>(3, run);
+        }
     }
+    if (AWE_MPC_EXTRA_TILES || sg != 0) return;
+    gen_interval_extras<D>(k, b, VT, PT, ctab, coff, g, grad, jac, fpart, a);
+}
+
+// the interval's tracking-cost gradient and partial sum, continuity rows, initial conditions and
+// constant J_g entries (lane b = instance)
+template <int D>
+__device__ __forceinline__ void gen_interval_extras(int k, int b, const double* __restrict__ VT,
+                                                    const double* __restrict__ PT, const unsigned* __restrict__ ctab,
+                                                    const int* __restrict__ coff, double* __restrict__ g,
+                                                    double* __restrict__ grad, double* __restrict__ jac,
+                                                    double* __restrict__ fpart, const GenArgs& a) {
+    constexpr int NN = D + 1;
+    constexpr int STRIDE = K3_NX + K3_NU + K3_NX + K3_NZ + D * (K3_NX + K3_NZ);
+    const unsigned lb = 8u * (unsigned)b, ld8 = a.ld8;
+    const int c0 = a.v_int0 + k * a.stride;
+    double* gb = g + (size_t)b * a.n_g;
+    const int row0 = K3_NX + k * a.rows;
     auto V = [&](int col) { return im::at(VT, (unsigned)col, ld8, lb); };
     auto Pp = [&](int row) { return im::at(PT, (unsigned)row, ld8, lb); };
     // tracking objective of the interval's columns (pmpc.py:304-358), as mpc_interval_kernel
@@ -686,6 +771,7 @@ void mpc_gen_shoot_kernel(const double* __restrict__ VT, const double* __restric
     const int pref = K3_NX + c0;                       // p.ref row of column c0
     const int pq = K3_NX + a.n_v + 1;                  // Q, then R
     double fs = 0.0;
+#pragma unroll
     for (int c = 0; c < STRIDE; ++c) {
         double gr = 0.0, ft = 0.0;
         if (c >= K3_NX && c < K3_NX + K3_NU) {
@@ -707,6 +793,7 @@ void mpc_gen_shoot_kernel(const double* __restrict__ VT, const double* __restric
     // continuity x[k+1] - sum_r D_r X_{k,r} (collocation.py:319-336) and the initial conditions
     const int gc = row0 + K3_N_EQ + K3_N_INEQ + D * K3_N_EQ;
     constexpr int CO = 2 * K3_NX + K3_NU + K3_NZ;
+#pragma unroll
     for (int i = 0; i < K3_NX; ++i) {
         double s = 0.0;
 #pragma unroll
@@ -722,6 +809,37 @@ void mpc_gen_shoot_kernel(const double* __restrict__ VT, const double* __restric
     }
 }
 
+// The node kernel: the Radau tiles (instance block, interval, strip group) and the shooting tiles
+// (instance block, kGenShootWaves intervals, strip group) in one launch, so that the two node kinds
+// run side by side; one wavefront per SIMD (the node code keeps 100-150 values live)
+template <int D>
+constexpr int gen_radau_tiles(const GenArgs& a) { return a.nib * a.n_k * kGenStripGroups; }
+template <int D>
+__global__ __launch_bounds__(64 * kGenNodeWaves) __attribute__((amdgpu_waves_per_eu(1)))
+void mpc_gen_node_kernel(const double* __restrict__ VT, const double* __restrict__ PT,
+                         const double* __restrict__ cst, const unsigned* __restrict__ dtab,
+                         const unsigned* __restrict__ ctab, const int* __restrict__ coff, double* __restrict__ g,
+                         double* __restrict__ grad, double* __restrict__ jac, double* __restrict__ fpart, GenArgs a) {
+    constexpr int T0 = kGenSlots<D>.total[0], T1 = kGenSlots<D>.total[1];
+    constexpr int NLDT = D * T1 > kGenShootWaves * T0 ? D * T1 : kGenShootWaves * T0;
+    __shared__ unsigned ldt[NLDT];
+    const int nr = gen_radau_tiles<D>(a);
+    const int nk4 = (a.n_k + kGenShootWaves - 1) / kGenShootWaves;
+    const int ns = a.nib * nk4 * kGenStripGroups;
+    const int ne = AWE_MPC_EXTRA_TILES ? a.nib * nk4 : 0;
+    const int t = im::xcd_tile(ne + nr + ns);
+    if (t >= ne + nr + ns) return;
+    if (t < ne) {                        // first: the extras tiles are short and latency-bound
+        const int ib = t / nk4, k = (t - ib * nk4) * kGenShootWaves + (int)(threadIdx.x >> 6);
+        const int b = ib * 64 + (int)(threadIdx.x & 63);
+        if (k < a.n_k && b < a.batch) gen_interval_extras<D>(k, b, VT, PT, ctab, coff, g, grad, jac, fpart, a);
+    } else if (t < ne + nr) {
+        gen_radau_tile<D>(t - ne, ldt, VT, PT, cst, dtab, g, jac, a);
+    } else {
+        gen_shoot_tile<D>(t - ne - nr, ldt, VT, PT, cst, dtab, ctab, coff, g, grad, jac, fpart, a);
+    }
+}
+
 // one lane per instance: objective partials in a fixed order, terminal cost, global gradient rows
 __global__ __launch_bounds__(64) void mpc_gen_finalize_kernel(const double* __restrict__ VT,
                                                              const double* __restrict__ PT,
@@ -731,7 +849,15 @@ __global__ __launch_bounds__(64) void mpc_gen_finalize_kernel(const double* __re
     if (b >= a.batch) return;
     const unsigned lb = 8u * (unsigned)b;
     double s = 0.0;
-    for (int k = 0; k < a.n_k; ++k) s += im::at(fpart, (unsigned)k, a.ld8, lb);
+    int k = 0;
+    for (; k + 8 <= a.n_k; k += 8) {                   // 8 loads in flight, the sum in interval order
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = im::at(fpart, (unsigned)(k + u), a.ld8, lb);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    for (; k < a.n_k; ++k) s += im::at(fpart, (unsigned)k, a.ld8, lb);
     const int xN = a.v_int0 + a.n_k * a.stride;
     const int pP = K3_NX + a.n_v + 1 + K3_NX + K3_NU;
     for (int i = 0; i < K3_NX; ++i) {
@@ -1015,14 +1141,12 @@ int awempc_eval_nlp_im(awempc_handle h, const double* V, const double* p, double
     im::transpose_in_kernel<<<tgrid, 256, 0, s>>>(V, p, h->d_VT, h->d_PT, B, T.lay.n_v, T.lay.n_p, (int)h->gen_ld);
     MPC_TRY(hipGetLastError());
     MPC_TRY(hipEventRecord(h->gev[1], s));
-    const dim3 rgrid((unsigned)im::xcd_grid(a.nib * a.n_k));
-    const dim3 sgrid((unsigned)im::xcd_grid(a.nib * ((a.n_k + kGenShootWaves - 1) / kGenShootWaves)));
+    const int n_tiles = a.nib * (a.n_k + (a.n_k + kGenShootWaves - 1) / kGenShootWaves) * kGenStripGroups +
+                        (AWE_MPC_EXTRA_TILES ? a.nib * ((a.n_k + kGenShootWaves - 1) / kGenShootWaves) : 0);
+    const dim3 ngrid((unsigned)im::xcd_grid(n_tiles));
 #define MPC_GEN_NODE(DD)                                                                                           \
-    mpc_gen_shoot_kernel<DD><<<sgrid, 64 * kGenShootWaves, 0, s>>>(h->d_VT, h->d_PT, h->d_cst, h->d_gdtab,         \
-                                                                    h->d_gctab, h->d_gcoff, g, grad_f, jac,          \
-                                                                    h->d_gfpart, a);                                 \
-    mpc_gen_radau_kernel<DD><<<rgrid, 64 * gen_radau_waves<DD>(), 0, s>>>(h->d_VT, h->d_PT, h->d_cst, h->d_gdtab, g, \
-                                                                          jac, a)
+    mpc_gen_node_kernel<DD><<<ngrid, 64 * kGenNodeWaves, 0, s>>>(h->d_VT, h->d_PT, h->d_cst, h->d_gdtab, h->d_gctab, \
+                                                                 h->d_gcoff, g, grad_f, jac, h->d_gfpart, a)
     switch (T.lay.d) {
         case 2: MPC_GEN_NODE(2); break;
         case 3: MPC_GEN_NODE(3); break;

@@ -15,6 +15,7 @@
 //
 // The model constants and u_ref enter as run-time loads (cst[i], ex0); only the tether element count
 // is fixed at generation time and written out, so that awempc_create can check it.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -44,10 +45,16 @@ struct SymIn {
 };
 
 struct KindOut {
-    std::string body;
+    std::vector<std::string> body;   // one per direction strip
     awe::EmitStats st;
     std::vector<short> tan_idx;   // [kRowsPerNode][kLanes]
 };
+
+// direction strips: the node's tangents split into kStrips contiguous direction ranges of balanced
+// tangent counts; a strip is its own function body (STRIP template argument) that recomputes the
+// values it needs, so that kStrips wavefronts run one node side by side (strip 0 also stores the row
+// values).  AWE_K3_STRIPS overrides the count for experiments.
+constexpr int kStripsDefault = 1;
 
 // structural pattern of (row, direction) at a node of `kind` (build_tables' rules)
 bool in_pattern(int kind, uint32_t m, int dir) {
@@ -58,7 +65,7 @@ bool in_pattern(int kind, uint32_t m, int dir) {
     return (m >> dir) & 1u;
 }
 
-KindOut generate(int kind, const std::vector<double>& cst, const Tables& T) {
+KindOut generate(int kind, const std::vector<double>& cst, const Tables& T, int n_strips) {
     awe::Tape tape;
     awe::active_tape() = &tape;
     std::vector<Sym> w(kLanes), cs(cst.size());
@@ -104,11 +111,29 @@ KindOut generate(int kind, const std::vector<double>& cst, const Tables& T) {
         }
     }
     KindOut ko;
-    std::string body = awe::emit(tape, stores, ko.st, true, 32, false, 0);
-    ko.body = body;
+    std::vector<int> per_dir(kLanes, 0), strip_of(kLanes, 0);
+    int total = 0;
+    for (auto& s : stores) if (s.kind == 1) { per_dir[s.dir]++; total++; }
+    for (int dir = 0, acc = 0; dir < kLanes; ++dir) {
+        strip_of[dir] = std::min(n_strips - 1, (int)((long long)acc * n_strips / std::max(1, total)));
+        acc += per_dir[dir];
+    }
     ko.tan_idx.assign(kRowsPerNode * kLanes, -1);
-    for (auto& s : stores)
-        if (s.kind == 1) ko.tan_idx[s.row * kLanes + s.dir] = (short)s.slot;
+    int slot_base = 0;
+    for (int sidx = 0; sidx < n_strips; ++sidx) {
+        std::vector<awe::Store> part;
+        for (auto& s : stores)
+            if ((s.kind != 1 && sidx == 0) || (s.kind == 1 && strip_of[s.dir] == sidx)) part.push_back(s);
+        awe::EmitStats st;
+        const int before = slot_base;
+        ko.body.push_back(part.empty() ? std::string() : awe::emit(tape, part, st, true, 32, false, slot_base));
+        slot_base = before + st.n_tan;
+        ko.st.ops += st.ops; ko.st.flops += st.flops; ko.st.transcendental += st.transcendental;
+        ko.st.loads += st.loads; ko.st.n_tan += st.n_tan; ko.st.n_zero_tan += st.n_zero_tan;
+        ko.st.max_live = std::max(ko.st.max_live, st.max_live);
+        for (auto& s : part)
+            if (s.kind == 1) ko.tan_idx[s.row * kLanes + s.dir] = (short)s.slot;
+    }
     awe::active_tape() = nullptr;
     return ko;
 }
@@ -136,7 +161,16 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "tables: %s\n", err.c_str());
         return 1;
     }
-    KindOut ks = generate(0, cst, T), kr = generate(1, cst, T);
+    const char* ns = std::getenv("AWE_K3_STRIPS");
+    const int n_strips = ns ? std::max(1, std::atoi(ns)) : kStripsDefault;
+    KindOut ks = generate(0, cst, T, n_strips), kr = generate(1, cst, T, n_strips);
+    auto bodies = [&](const KindOut& k) {
+        std::string b;
+        for (int s = 0; s < n_strips; ++s)
+            b += std::string(s ? "    else " : "    ") + "if constexpr (STRIP == " + std::to_string(s) + ") {\n" +
+                 k.body[s] + "    }\n";
+        return b;
+    };
 
     std::ostringstream o;
     o << "// GENERATED by awebox_amd/csrc/gen/kite3_jacgen.cpp from kite3_model.hpp -- do not edit.\n"
@@ -147,6 +181,8 @@ int main(int argc, char** argv) {
          "#else\n#define AWE_GEN_FENCE() ((void)0)\n#endif\n\nnamespace awe_k3gen {\n\n";
     o << "// integer structure of the model constants the code was generated for (awempc_create checks it)\n";
     o << "constexpr int kNElements = " << (int)cst[K3_C_N_ELEMENTS] << ";\n";
+    o << "// direction strips: k3_node_*<TS, STRIP> stores the tangents of strip STRIP (strip 0 also the rows)\n";
+    o << "constexpr int kNStrips = " << n_strips << ";\n";
     o << "// tangent slots per node kind (0 shooting, 1 Radau): one per J_g pattern entry of the node's rows\n";
     o << "constexpr int kNTan[2] = {" << ks.st.n_tan << ", " << kr.st.n_tan << "};\n";
     o << "// algorithmic operations per node kind: adds/muls/reciprocals, transcendental calls\n";
@@ -166,13 +202,13 @@ int main(int argc, char** argv) {
     o << "};\n\n";
     o << "// shooting node: val[0..13] = 12 equalities + 2 path inequalities; ex0 = u_ref\n";
     o << "// in(i): node variable i (31 = phi.gamma); tan[s]: an accessor that sends slot s to its J_g entries\n";
-    o << "template <int TS, class In, class Val, class Tan>\nAWE_HD void k3_node_shoot(const In& in, const double ex0, "
-         "const double* __restrict__ cst, Val val, Tan tan) {\n";
-    o << ks.body << "}\n\n";
+    o << "template <int TS, int STRIP, class In, class Val, class Tan>\nAWE_HD void k3_node_shoot(const In& in, "
+         "const double ex0, const double* __restrict__ cst, Val val, Tan tan) {\n";
+    o << bodies(ks) << "}\n\n";
     o << "// Radau node: val[0..11] equalities; ex0 = u_ref, ex1 = C[n][n] / (h t_f), ex2 = 1 / t_f\n";
-    o << "template <int TS, class In, class Val, class Tan>\nAWE_HD void k3_node_radau(const In& in, const double ex0, "
-         "const double ex1, const double ex2, const double* __restrict__ cst, Val val, Tan tan) {\n";
-    o << kr.body << "}\n\n}  // namespace awe_k3gen\n";
+    o << "template <int TS, int STRIP, class In, class Val, class Tan>\nAWE_HD void k3_node_radau(const In& in, "
+         "const double ex0, const double ex1, const double ex2, const double* __restrict__ cst, Val val, Tan tan) {\n";
+    o << bodies(kr) << "}\n\n}  // namespace awe_k3gen\n";
 
     std::ofstream out(argv[2]);
     out << o.str();

@@ -639,7 +639,7 @@ def mpc_block(B, rank, dev, dist, world, steps=50, warmup=5):
             "finite": finite,
             "roofline": dict({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": achieved / HBM_PEAK_GBS,
-                              "kernel": ("mpc_gen_in + mpc_gen_shoot + mpc_gen_radau + mpc_gen_finalize (one evaluation)"
+                              "kernel": ("mpc_gen_in + mpc_gen_node (Radau, shooting and interval tiles) + mpc_gen_finalize (one evaluation)"
                                          if gen else "mpc_interval_kernel<4> + mpc_finalize_kernel"),
                               "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval, "traffic": None},
                              **({"kernel_ms_parts": dict(zip(("transpose_in", "node", "finalize"),
