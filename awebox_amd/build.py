@@ -8,9 +8,11 @@
 Plain ``hipcc -shared -fPIC`` (no JIT cache): the .so files live next to this file so that they
 travel with the repository snapshot to the GPU box.
 
-Before libawegpu.so is compiled, ``generate()`` refreshes ``csrc/ap2_nodejac.gen.hpp``: the node
-model is traced and differentiated by ``csrc/gen/ap2_jacgen.cpp`` (g++, host) for the default AP2
-constants, and the straight-line node-Jacobian code it writes is what ap2_node_kernel runs.
+Before the libraries are compiled, ``generate()`` refreshes the generated node code: each node model
+is traced and differentiated by its generator under ``csrc/gen/`` (g++, host) for the default
+constants -- ``ap2_nodejac.gen.hpp`` / ``ap2_nodehess.gen.hpp`` (AP2 Jacobian and Hessian),
+``kite3_nodejac.gen.hpp`` (tracking MPC), ``dual_nodejac.gen.hpp`` (dual kites) -- and the straight-line
+code they write is what the instance-minor kernels run.
 """
 from __future__ import annotations
 
@@ -37,9 +39,15 @@ K3_HEADER = os.path.join(CSRC, "kite3_nodejac.gen.hpp")
 K3_SOURCES = [os.path.join(CSRC, "gen", f) for f in ("kite3_jacgen.cpp", "sym.hpp")] + [
     os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp", "ap2_tables.hpp", "scalar.hpp")] + [
     os.path.join(INCLUDE, "awempc.h"), os.path.join(INCLUDE, "awegpu.h"), os.path.join(HERE, "kite3.py")]
+# the dual-kite node-Jacobian code (csrc/gen/dual_jacgen.cpp)
+DUAL_HEADER = os.path.join(CSRC, "dual_nodejac.gen.hpp")
+DUAL_SOURCES = [os.path.join(CSRC, "gen", f) for f in ("dual_jacgen.cpp", "sym.hpp")] + [
+    os.path.join(CSRC, f) for f in ("dual_model.hpp", "dual_tables.hpp", "ap2_model.hpp", "ap2_tables.hpp",
+                                    "scalar.hpp")] + [
+    os.path.join(INCLUDE, "awedual.h"), os.path.join(INCLUDE, "awegpu.h"), os.path.join(HERE, "dual.py")]
 # (header, generator source, inputs hashed into the header's first line, default constants)
 GENERATORS = [(GEN_HEADER, "ap2_jacgen.cpp", GEN_SOURCES, "ap2"), (HESS_HEADER, "ap2_hessgen.cpp", HESS_SOURCES, "ap2"),
-              (K3_HEADER, "kite3_jacgen.cpp", K3_SOURCES, "kite3")]
+              (K3_HEADER, "kite3_jacgen.cpp", K3_SOURCES, "kite3"), (DUAL_HEADER, "dual_jacgen.cpp", DUAL_SOURCES, "dual")]
 # content hash of GEN_SOURCES recorded in the generated header's first line: the header is stale
 # when the hash differs (file times do not survive a checkout or the copy to the GPU box)
 _HASH_TAG = "// inputs-sha1: "
@@ -50,9 +58,10 @@ TARGETS = {
     LIB_MPC: ([os.path.join(CSRC, "awempc.hip")],
               _COMMON + [os.path.join(CSRC, f) for f in ("kite3_model.hpp", "kite3_tables.hpp", "im_layout.hpp")]
               + [os.path.join(INCLUDE, "awempc.h"), K3_HEADER]),
-    LIB_DUAL: ([os.path.join(CSRC, "awedual.hip")],
-               _COMMON + [os.path.join(CSRC, f) for f in ("dual_model.hpp", "dual_tables.hpp")]
-               + [os.path.join(INCLUDE, "awedual.h")]),
+    LIB_DUAL: ([os.path.join(CSRC, "awedual.hip"), os.path.join(CSRC, "awedual_gen.hip")],
+               _COMMON + [os.path.join(CSRC, f) for f in ("dual_model.hpp", "dual_tables.hpp", "dual_hess_tables.hpp",
+                                                          "awedual_gen.hpp", "im_layout.hpp")]
+               + [os.path.join(INCLUDE, "awedual.h"), DUAL_HEADER]),
     LIB_LU: ([os.path.join(CSRC, "batched_lu.hip")], []),
 }
 ARCH = os.environ.get("AWE_OFFLOAD_ARCH", "gfx950")
@@ -72,10 +81,30 @@ def build_one(lib: str, force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale(lib, sources + headers):
         return lib
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *FLAGS, *sources, "-o", lib + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True, cwd=CSRC)
+    if len(sources) == 1:
+        cmd = [hipcc, *FLAGS, *sources, "-o", lib + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+    else:
+        # several translation units: compiled side by side into objects, then linked
+        import tempfile
+        with tempfile.TemporaryDirectory() as tmp:
+            objs = [os.path.join(tmp, os.path.splitext(os.path.basename(src))[0] + ".o") for src in sources]
+            cflags = [f for f in FLAGS if f != "-shared"] + ["-c"]
+            procs = []
+            for src, obj in zip(sources, objs):
+                cmd = [hipcc, *cflags, src, "-o", obj]
+                if verbose:
+                    print(" ".join(cmd), file=sys.stderr)
+                procs.append((cmd, subprocess.Popen(cmd, cwd=CSRC)))
+            for cmd, pr in procs:
+                if pr.wait() != 0:
+                    raise subprocess.CalledProcessError(pr.returncode, cmd)
+            cmd = [hipcc, *FLAGS, *objs, "-o", lib + ".tmp"]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(lib + ".tmp", lib)
     return lib
 
@@ -113,6 +142,9 @@ def _default_constants(model):
     if model == "kite3":
         from . import kite3
         return kite3.build_constants().consts
+    if model == "dual":
+        from . import dual
+        return dual.build_constants().consts
     from . import problem as pb
     return pb.build_constants(pb.Ap2Config()).consts
 
@@ -156,10 +188,13 @@ def _generate_one(header, gen, sources, force, verbose, model="ap2"):
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Build every library; returns the AP2 library path (the headline evaluator)."""
+    """Build every library (side by side: the dual-kite library's generated node kernel alone takes
+    ~9 minutes of hipcc); returns the AP2 library path (the headline evaluator)."""
+    from concurrent.futures import ThreadPoolExecutor
     generate(force=force, verbose=verbose)
-    for lib in TARGETS:
-        build_one(lib, force=force, verbose=verbose)
+    with ThreadPoolExecutor(max_workers=len(TARGETS)) as pool:
+        for fut in [pool.submit(build_one, lib, force, verbose) for lib in TARGETS]:
+            fut.result()
     return LIB
 
 

@@ -35,6 +35,7 @@
 #include "dual_model.hpp"
 #include "dual_tables.hpp"
 #include "dual_hess_tables.hpp"
+#include "awedual_gen.hpp"
 
 namespace {
 
@@ -54,11 +55,6 @@ int fail(int code, const std::string& msg) {
             return fail(AWE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
-constexpr int kNPart = 8;   // per interval: tracking, other, power integral A_k, d/d diam_t, t_f, l_s, diam_s
-constexpr int kCostTracking = 0, kCostURegularisation = 1, kCostXdotRegularisation = 2, kCostFictitious = 10,
-              kCostPower = 11, kCostTf = 13, kCostThetaRegularisation = 14, kCostBeta = 18;
-constexpr int kPhiCost[7] = {3, 6, 4, 5, 7, 8, 9};   // cost index of phi = [gamma tau iota psi eta nu upsilon]
-constexpr int kPhiPsi = 3;
 
 struct DArgs {
     const double* V;
@@ -638,13 +634,10 @@ __global__ __launch_bounds__(64) void dual_finalize_kernel(DArgs a) {
         }
     }
     // periodicity rows, sorted x names (operation.py:245-266)
-    constexpr int kOrder[ADL_NX] = {24, 25, 26, 45, 46, 47, 49, 3, 4, 5, 9, 10, 11, 30, 31, 32, 48,
-                                    12, 13, 14, 33, 34, 35, 0, 1, 2, 6, 7, 8, 27, 28, 29,
-                                    15, 16, 17, 18, 19, 20, 21, 22, 23, 36, 37, 38, 39, 40, 41, 42, 43, 44};
     const int gp = a.n_k * (ADL_N_EQ + ADL_N_INEQ + a.d * ADL_N_EQ + ADL_NX);
     const int x0 = a.v_int0;
     const int xT = a.v_int0 + (a.n_k - 1) * a.stride + 2 * ADL_NX + ADL_NU + ADL_NZ + (a.d - 1) * (ADL_NX + ADL_NZ);
-    for (int i = lane; i < ADL_NX; i += 64) g[gp + i] = V[x0 + kOrder[i]] - V[xT + kOrder[i]];
+    for (int i = lane; i < ADL_NX; i += 64) g[gp + i] = V[x0 + kPeriodicOrder[i]] - V[xT + kPeriodicOrder[i]];
 }
 
 // =========================================================================================
@@ -990,6 +983,9 @@ struct adl_handle_s {
     size_t hess_dyn = 0;
     hipEvent_t hev[2] = {nullptr, nullptr};
     bool htimed = false;
+    // generated instance-minor path (adl_eval_nlp_im, awedual_gen.hip)
+    dgen::Plan* gen = nullptr;
+    std::string gen_why;
 };
 
 static DArgs make_args(adl_handle h, const double* V, const double* P) {
@@ -1182,6 +1178,10 @@ int adl_create(int n_k, int d, const double* consts, int n_consts, int batch, ad
 #undef ADL_UPLOAD
     ADL_TRY(hipMalloc((void**)&h->d_part, sizeof(double) * (size_t)batch * n_k * kNPart));
     for (auto& e : h->ev) ADL_TRY(hipEventCreate(&e));
+    if (int rc = dgen::create(T, h->consts, batch, &h->gen, h->gen_why, err)) {
+        adl_destroy(h);
+        return fail(rc, err);
+    }
     *out = h;
     return AWE_OK;
 }
@@ -1200,7 +1200,37 @@ int adl_destroy(adl_handle h) {
     for (auto& e : h->hev)
         if (e) (void)hipEventDestroy(e);
     delete h->ht;
+    dgen::destroy(h->gen);
     delete h;
+    return AWE_OK;
+}
+
+int adl_gen_status(adl_handle h, int* available) {
+    if (!h || !available) return fail(AWE_ERR_ARG, "null argument");
+    *available = h->gen ? 1 : 0;
+    if (!h->gen) g_err = h->gen_why;
+    return AWE_OK;
+}
+
+int adl_eval_nlp_im(adl_handle h, const double* V, const double* P, double* f, double* g, double* grad_f, double* jac,
+                    size_t ld, void* stream) {
+    if (!h || !V || !P || !f || !g || !grad_f || !jac) return fail(AWE_ERR_ARG, "null argument");
+    if (!h->gen) return fail(AWE_ERR_ARG, "generated path unavailable: " + h->gen_why);
+    std::string err;
+    if (int rc = dgen::eval(h->gen, h->d_cst, V, P, f, g, grad_f, jac, ld, (hipStream_t)stream, err))
+        return fail(rc, err);
+    return AWE_OK;
+}
+
+int adl_last_kernel_ms_im(adl_handle h, float* ms_in, float* ms_node, float* ms_interval, float* ms_fin) {
+    if (!h || !h->gen) return fail(AWE_ERR_ARG, "no generated path");
+    float ms[4];
+    std::string err;
+    if (int rc = dgen::last_ms(h->gen, ms, err)) return fail(rc, err);
+    if (ms_in) *ms_in = ms[0];
+    if (ms_node) *ms_node = ms[1];
+    if (ms_interval) *ms_interval = ms[2];
+    if (ms_fin) *ms_fin = ms[3];
     return AWE_OK;
 }
 

@@ -1,6 +1,8 @@
 // Multi-kite node model: two 6-DOF Ampyx AP2 kites on secondary tethers below the layer node 1
 // (architecture {1: 0, 2: 1, 3: 1}, examples/dual_kites_power_curve.py), hand-written for CDNA4
-// and instantiated on double / Dual / Dep2 (scalar.hpp).
+// and instantiated on double / Dual / Dep2 (scalar.hpp), and on the tracing scalar of the
+// build-time code generator (gen/sym.hpp: the parameters th and the constants cst then enter as
+// symbols of their own types PT / CT, the integer structure through structural()).
 //
 // One call evaluates, at ONE node, the 53 model equalities (model.py:125; append order of
 // dynamics.py:89-148 and lagr_dyn.py:106-169), the 19 path inequalities (dynamics.py:122-148:
@@ -69,8 +71,8 @@ AWE_HD T element_height(int e, int n_el, const T& qbz, const T& qtz) {
 
 // wind speed and density at an element midpoint, evaluated in place
 struct InlineAtmosphere {
-    template <class T>
-    AWE_HD void operator()(int /*seg*/, int /*e*/, const T& zz, const double* th, T& uw, T& rho) const {
+    template <class T, class PT>
+    AWE_HD void operator()(int /*seg*/, int /*e*/, const T& zz, const PT* th, T& uw, T& rho) const {
         uw = wind_speed(zz, th);
         rho = isa_density(zz, th);
     }
@@ -79,9 +81,9 @@ struct InlineAtmosphere {
 // One element of the 'multi' drag model of a tether segment from (qb, vb) to (qt, vt)
 // (element.py:60-146, segment.py:38-65): the element's drag vector, not yet split.  `seg`
 // (0 main, 1 + k secondary of kite k) and `e` identify the element for the atmosphere provider.
-template <class T, class Atm = InlineAtmosphere>
+template <class T, class PT, class Atm = InlineAtmosphere>
 AWE_HD void segment_element_drag(int seg, int e, int n_el, const T* qb, const T* qt, const T* vb, const T* vt,
-                                 const T& diam, const double* th, T out[3], const Atm& atm = Atm()) {
+                                 const T& diam, const PT* th, T out[3], const Atm& atm = Atm()) {
     const double lo = (double)e / (double)n_el, up = (double)(e + 1) / (double)n_el;
     T qu[3], ql[3], vs[3], tv[3];
     for (int i = 0; i < 3; ++i) {
@@ -119,16 +121,16 @@ AWE_HD double element_upper_share(int e, int n_el) {
 // q_k, dq_k, diam_s: 13 inputs).  The default provider evaluates them inline; the GPU kernel
 // substitutes one that returns values and partial derivatives preaccumulated once per node.
 struct DualInlineSubmodels {
-    template <class T>
-    AWE_HD void kite_atmosphere(const T& qz, const double* th, T& uw, T& rho) const {
+    template <class T, class PT>
+    AWE_HD void kite_atmosphere(const T& qz, const PT* th, T& uw, T& rho) const {
         uw = wind_speed(qz, th);
         rho = isa_density(qz, th);
     }
     // main tether: ground -> node 1; only the upper share is kept (tether_aero.py:85-95)
-    template <class T, class Atm = InlineAtmosphere>
-    AWE_HD void main_drag(const T* q, const T* v, const T& diam, const double* th, const double* cst,
+    template <class T, class PT, class CT, class Atm = InlineAtmosphere>
+    AWE_HD void main_drag(const T* q, const T* v, const T& diam, const PT* th, const CT* cst,
                           T up[3], const Atm& atm = Atm()) const {
-        const int n_el = (int)cst[ADL_C_N_ELEMENTS];
+        const int n_el = structural(cst[ADL_C_N_ELEMENTS]);
         T z3[3] = {T(0.0), T(0.0), T(0.0)};
         for (int i = 0; i < 3; ++i) up[i] = T(0.0);
         for (int e = 0; e < n_el; ++e) {
@@ -139,10 +141,10 @@ struct DualInlineSubmodels {
         }
     }
     // secondary tether node 1 -> kite: upper share to the kite, lower share to node 1
-    template <class T, class Atm = InlineAtmosphere>
+    template <class T, class PT, class CT, class Atm = InlineAtmosphere>
     AWE_HD void sec_drag(int k, const T* qb, const T* vb, const T* qt, const T* vt, const T& diam,
-                         const double* th, const double* cst, T up[3], T lo[3], const Atm& atm = Atm()) const {
-        const int n_el = (int)cst[ADL_C_N_ELEMENTS];
+                         const PT* th, const CT* cst, T up[3], T lo[3], const Atm& atm = Atm()) const {
+        const int n_el = structural(cst[ADL_C_N_ELEMENTS]);
         for (int i = 0; i < 3; ++i) { up[i] = T(0.0); lo[i] = T(0.0); }
         for (int e = 0; e < n_el; ++e) {
             T c[3];
@@ -163,30 +165,35 @@ struct DualInlineSubmodels {
 // and holonomic rows) are evaluated in one loop body; only the node-1 accumulator (3 values)
 // crosses iterations.  Inputs are re-read through `in` where they are needed, keeping the
 // dual-number working set of one lane small.
-template <class T, class In, class Sink, class Sub = DualInlineSubmodels>
-AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const double* cst, Sink& out,
-                      bool want_ineq, const Sub& sub = Sub()) {
+//
+// first_kite = 1 evaluates kite 3 before kite 2 (only the order of node 1's two accumulations
+// changes): the code generator traces kite 3's rows that way, so that the values they share with
+// node 1 are formed next to their use.
+template <class T, class In, class Sink, class Sub = DualInlineSubmodels, class PT = double, class CT = double>
+AWE_HD void dual_node(const In& in, const T& gamma, const PT* th, const CT* cst, Sink& out,
+                      bool want_ineq, const Sub& sub = Sub(), int first_kite = 0) {
     using namespace dl;
-    const double* s = cst + ADL_C_SCALING;
+    const CT* s = cst + ADL_C_SCALING;
     auto SI = [&](int i) -> T { return in(i) * s[i]; };
     const double pi = 3.14159265358979323846;
-    const double g_grav = th[AWE_TH_G];
-    const double m_k = th[AWE_TH_M_K];
-    const double rho_t = th[AWE_TH_RHO_TETHER];
-    const double kap = th[AWE_TH_KAPPA];
-    const double gs10 = cst[ADL_C_G_SCALING] * 10.0;
-    const double sm_s = pi * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * rho_t *
+    const auto g_grav = th[AWE_TH_G];
+    const auto m_k = th[AWE_TH_M_K];
+    const auto rho_t = th[AWE_TH_RHO_TETHER];
+    const auto kap = th[AWE_TH_KAPPA];
+    const auto gs10 = cst[ADL_C_G_SCALING] * 10.0;
+    const auto sm_s = pi * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * (cst[ADL_C_SCALING_DIAM_S] / 2.0) * rho_t *
                         cst[ADL_C_SCALING_LENGTH_S];
 
     T acc1[3] = {T(0.0), T(0.0), T(0.0)};   // node 1: secondary-segment Lagrange terms - lower drag shares
 #pragma unroll 1
-    for (int k = 0; k < 2; ++k) {
+    for (int kk = 0; kk < 2; ++kk) {
+        const int k = first_kite ? 1 - kk : kk;
         // ---- DCM kinematics with orthonormality Baumgarte (lagr_dyn.py:236-254) ----------
         {
             T R[9], w[3];
             for (int i = 0; i < 9; ++i) R[i] = SI(r(k) + i);
             for (int i = 0; i < 3; ++i) w[i] = SI(om(k) + i);
-            const double kr2 = th[AWE_TH_KAPPA_R] / 2.0;
+            const auto kr2 = th[AWE_TH_KAPPA_R] / 2.0;
             for (int c = 0; c < 3; ++c) {
                 T A[3];
                 for (int rr = 0; rr < 3; ++rr) {
@@ -221,13 +228,13 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
             T x_comp = sqrt(ua_e1 * ua_e1 + 1e-16);
             T alpha = ua_e3 / x_comp;
             T beta = ua_e2 / x_comp;
-            const double b_ref = th[AWE_TH_B_REF], c_ref = th[AWE_TH_C_REF], s_ref = th[AWE_TH_S_REF];
+            const auto b_ref = th[AWE_TH_B_REF], c_ref = th[AWE_TH_C_REF], s_ref = th[AWE_TH_S_REF];
             T coeff[6];
             {
                 T inv2a = 1.0 / (2.0 * airspeed);
-                const double* sd = th + AWE_TH_STAB_DERIVS;
-                const double* sdl = cst + ADL_C_SD_LEN;
-                const double mf = th[AWE_TH_MOMENT_FACTOR];
+                const PT* sd = th + AWE_TH_STAB_DERIVS;
+                const CT* sdl = cst + ADL_C_SD_LEN;
+                const auto mf = th[AWE_TH_MOMENT_FACTOR];
                 T alpha2 = alpha * alpha;
                 for (int c = 0; c < 6; ++c) coeff[c] = T(0.0);
                 for (int i = 0; i < 9; ++i) {
@@ -243,14 +250,14 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
                     }
                     T ia = inp * alpha, ia2 = inp * alpha2;
                     for (int c = 0; c < 6; ++c) {
-                        const int n = (int)sdl[c * 9 + i];
+                        const int n = structural(sdl[c * 9 + i]);
                         if (n == 0) continue;
-                        const double* dv = sd + (c * 9 + i) * 3;
+                        const PT* dv = sd + (c * 9 + i) * 3;
                         T contrib = dv[0] * inp;
                         if (n > 1) contrib = contrib + dv[1] * ia;
                         if (n > 2) contrib = contrib + dv[2] * ia2;
-                        const double wgt = (c >= 3 && i >= 6) ? mf : 1.0;
-                        coeff[c] = coeff[c] + wgt * contrib;
+                        // (1.0 * contrib is contrib exactly: the unweighted terms skip the product)
+                        coeff[c] = coeff[c] + ((c >= 3 && i >= 6) ? mf * contrib : contrib);
                     }
                 }
             }
@@ -267,7 +274,7 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
                 M_body[0] = -(qs * (b_ref * coeff[3]));
                 M_body[1] = qs * (c_ref * coeff[4]);
                 M_body[2] = -(qs * (b_ref * coeff[5]));
-                const double* J = th + AWE_TH_J;
+                const PT* J = th + AWE_TH_J;
                 T w[3], Jw[3];
                 for (int i = 0; i < 3; ++i) w[i] = SI(om(k) + i);
                 for (int i = 0; i < 3; ++i) Jw[i] = J[i] * w[0] + J[3 + i] * w[1] + J[6 + i] * w[2];
@@ -275,7 +282,7 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
                 wxJw[0] = w[1] * Jw[2] - w[2] * Jw[1];
                 wxJw[1] = -(w[0] * Jw[2] - w[2] * Jw[0]);
                 wxJw[2] = w[0] * Jw[1] - w[1] * Jw[0];
-                const double inv_ms = 1.0 / cst[ADL_C_M_AERO_SCALING];
+                const auto inv_ms = 1.0 / cst[ADL_C_M_AERO_SCALING];
                 for (int i = 0; i < 3; ++i) {
                     const int xw = kXD + om(k);
                     T Jdw = J[i] * SI(xw) + J[3 + i] * SI(xw + 1) + J[6 + i] * SI(xw + 2);
@@ -289,20 +296,20 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
                 for (int i = 0; i < 3; ++i) dd[i] = SI(q(k) + i) - SI(kQ10 + i);
                 T nd = sqrt(dot3(dd, dd));
                 T tension = SI(lam(k)) * nd;                                   // dynamics.py:706-776
-                const double fscale = s[lam(k)] * cst[ADL_C_SCALING_LENGTH_S];
+                const auto fscale = s[lam(k)] * cst[ADL_C_SCALING_LENGTH_S];
                 out.ineq_row(irow_force(k), (tension - th[AWE_TH_FORCE_LIMITS + 1]) / fscale);
                 out.ineq_row(irow_force(k) + 1, (th[AWE_TH_FORCE_LIMITS + 0] - tension) / fscale);
-                const double u_ref = th[AWE_TH_U_REF];
+                const auto u_ref = th[AWE_TH_U_REF];
                 out.ineq_row(irow_airspeed(k), (airspeed - th[AWE_TH_AIRSPEED_LIMITS + 1]) / u_ref);
                 out.ineq_row(irow_airspeed(k) + 1, (th[AWE_TH_AIRSPEED_LIMITS + 0] - airspeed) / u_ref);
-                const double tight = cst[ADL_C_AERO_TIGHTNESS], aref = cst[ADL_C_AIRSPEED_REF];
-                const double amax = cst[ADL_C_ALPHA_MAX], amin = cst[ADL_C_ALPHA_MIN];
-                const double bmax = cst[ADL_C_BETA_MAX], bmin = cst[ADL_C_BETA_MIN];
-                out.ineq_row(irow_valid(k), (ua_e3 - ua_e1 * amax) * tight / aref / ::sqrt(amax * amax + 1e-16));
-                out.ineq_row(irow_valid(k) + 1, (-ua_e3 + ua_e1 * amin) * tight / aref / ::sqrt(amin * amin + 1e-16));
-                out.ineq_row(irow_valid(k) + 2, (ua_e2 - ua_e1 * bmax) * tight / aref / ::sqrt(bmax * bmax + 1e-16));
-                out.ineq_row(irow_valid(k) + 3, (-ua_e2 + ua_e1 * bmin) * tight / aref / ::sqrt(bmin * bmin + 1e-16));
-                const double cos_gmax = ::cos(th[AWE_TH_ROT_ANGLES + 2]);      // dynamics.py:1022-1052
+                const auto tight = cst[ADL_C_AERO_TIGHTNESS], aref = cst[ADL_C_AIRSPEED_REF];
+                const auto amax = cst[ADL_C_ALPHA_MAX], amin = cst[ADL_C_ALPHA_MIN];
+                const auto bmax = cst[ADL_C_BETA_MAX], bmin = cst[ADL_C_BETA_MIN];
+                out.ineq_row(irow_valid(k), (ua_e3 - ua_e1 * amax) * tight / aref / sqrt(amax * amax + 1e-16));
+                out.ineq_row(irow_valid(k) + 1, (-ua_e3 + ua_e1 * amin) * tight / aref / sqrt(amin * amin + 1e-16));
+                out.ineq_row(irow_valid(k) + 2, (ua_e2 - ua_e1 * bmax) * tight / aref / sqrt(bmax * bmax + 1e-16));
+                out.ineq_row(irow_valid(k) + 3, (-ua_e2 + ua_e1 * bmin) * tight / aref / sqrt(bmin * bmin + 1e-16));
+                const auto cos_gmax = cos(th[AWE_TH_ROT_ANGLES + 2]);      // dynamics.py:1022-1052
                 T yaw = (dd[0] * SI(r(k) + 6) + dd[1] * SI(r(k) + 7) + dd[2] * SI(r(k) + 8) - cos_gmax * nd) /
                         cst[ADL_C_SCALING_LENGTH_S];
                 out.ineq_row(irow_yaw(k), -1.0 * yaw);
@@ -338,7 +345,7 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
             T te = (mu / 6.0) * S * invL;                         // coefficient of d in dT/dq_k
             T lamk = SI(lam(k));
             T gm2 = g_grav * m * 0.5;
-            const double inv_fs = 1.0 / ((sm_s / 2.0 + m_k) * gs10);
+            const auto inv_fs = 1.0 / ((sm_s / 2.0 + m_k) * gs10);
             T c2a(0.0);
             for (int i = 0; i < 3; ++i) {
                 T ak = SI(kXD + dq(k) + i), a1 = SI(kDDQ10 + i);
@@ -358,7 +365,7 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
             T c0 = 0.5 * (dd - ls * ls);
             T c1 = dot3(d, wv);
             T c2 = dot3(wv, wv) + c2a;
-            const double hscale =
+            const auto hscale =
                 kap * kap * (cst[ADL_C_SCALING_LENGTH_S] * ((s[q(k)] + s[q(k) + 1] + s[q(k) + 2]) / 3.0));
             out.eq_row(row_hol(k), (c2 + 2.0 * kap * c1 + kap * kap * c0) / hscale);
         }
@@ -367,7 +374,7 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
     // ---- trivial kinematics, sorted names (lagr_dyn.py:141-169) -------------------------
     {
         auto triv = [&](int row, int ixd, int iu) {
-            out.eq_row(row, (SI(ixd) - SI(iu)) / ::sqrt(s[iu] * s[ixd]));
+            out.eq_row(row, (SI(ixd) - SI(iu)) / sqrt(s[iu] * s[ixd]));
         };
         for (int i = 0; i < 3; ++i) triv(kRowTriv + i, kXD + del(0) + i, ddel(0) + i);       // ddelta21
         for (int i = 0; i < 3; ++i) triv(kRowTriv + 3 + i, kXD + del(1) + i, ddel(1) + i);   // ddelta31
@@ -381,16 +388,16 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
     if (want_ineq) {
         T dd[3];
         for (int i = 0; i < 3; ++i) dd[i] = SI(q(0) + i) - SI(q(1) + i);
-        const double dmin = cst[ADL_C_ANTICOLLISION_DIST_MIN];
+        const auto dmin = cst[ADL_C_ANTICOLLISION_DIST_MIN];
         out.ineq_row(kIrowAnticollision, 1.0 - dot3(dd, dd) / (dmin * dmin));
     }
     out.power(SI(kLam10) * SI(kLT) * SI(kDLT) / cst[ADL_C_ENERGY_SCALING]);
 
     // ---- main tether segment (energy.py:59-97), node-1 translation, main holonomic --------
     {
-        const double sm_t = pi * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * rho_t *
-                            cst[ADL_C_SCALING_LENGTH_T];
-        const double inv_fs1 = 1.0 / ((sm_t / 2.0 + 2.0 * (sm_s / 2.0)) * gs10);   // mass.py:62-93
+        const auto sm_t = pi * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * (cst[ADL_C_SCALING_DIAM_T] / 2.0) * rho_t *
+                          cst[ADL_C_SCALING_LENGTH_T];
+        const auto inv_fs1 = 1.0 / ((sm_t / 2.0 + 2.0 * (sm_s / 2.0)) * gs10);   // mass.py:62-93
         T q1[3], v1[3], a1[3];
         for (int i = 0; i < 3; ++i) {
             q1[i] = SI(kQ10 + i);
@@ -427,7 +434,7 @@ AWE_HD void dual_node(const In& in, const T& gamma, const double* th, const doub
         T c0 = 0.5 * (qq - l_t * l_t);
         T c1 = sv - l_t * dl_t;
         T c2 = vv + qa - dl_t * dl_t - l_t * ldd;
-        const double hscale =
+        const auto hscale =
             kap * kap * (cst[ADL_C_SCALING_LENGTH_T] * ((s[kQ10] + s[kQ10 + 1] + s[kQ10 + 2]) / 3.0));
         out.eq_row(kRowHol1, (c2 + 2.0 * kap * c1 + kap * kap * c0) / hscale);
     }

@@ -38,6 +38,18 @@ constexpr int kNRows = kRowBeta0 + ADL_NKITES;     // 75
 constexpr int kGvalStride = 76;
 constexpr int kMaxConst = 16;
 
+// objective (objective.py): partial sums per interval -- tracking, other, power integral A_k,
+// d/d diam_t, t_f, l_s, diam_s -- and the cost-vector indices of P's cost entries
+constexpr int kNPart = 8;
+constexpr int kCostTracking = 0, kCostURegularisation = 1, kCostXdotRegularisation = 2, kCostFictitious = 10,
+              kCostPower = 11, kCostTf = 13, kCostThetaRegularisation = 14, kCostBeta = 18;
+constexpr int kPhiCost[7] = {3, 6, 4, 5, 7, 8, 9};   // cost index of phi = [gamma tau iota psi eta nu upsilon]
+constexpr int kPhiPsi = 3;
+// periodicity rows in the sorted order of the x names (operation.py:245-266): state index of each row
+constexpr int kPeriodicOrder[ADL_NX] = {24, 25, 26, 45, 46, 47, 49, 3,  4,  5,  9,  10, 11, 30, 31, 32, 48,
+                                        12, 13, 14, 33, 34, 35, 0,  1,  2,  6,  7,  8,  27, 28, 29,
+                                        15, 16, 17, 18, 19, 20, 21, 22, 23, 36, 37, 38, 39, 40, 41, 42, 43, 44};
+
 struct Mask {
     uint64_t lo = 0, hi = 0;
     bool has(int r) const { return r < 64 ? ((lo >> r) & 1u) : ((hi >> (r - 64)) & 1u); }

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <type_traits>
 #include <vector>
 
 #include "../kite3_nodejac.gen.hpp"
@@ -53,8 +54,18 @@ int main(int argc, char** argv) {
     for (int kind = 0; kind < 2; ++kind) {
         std::vector<double> val(k3t::kRowsPerNode, 0.0), tan(awe_k3gen::kNTan[kind], 0.0);
         PlainIn pin{w.data()};
-        if (kind == 0) awe_k3gen::k3_node_shoot<1>(pin, u_ref, cst.data(), val.data(), tan.data());
-        else awe_k3gen::k3_node_radau<1>(pin, u_ref, cxx, inv_tf, cst.data(), val.data(), tan.data());
+        auto strip = [&](auto st) {   // every direction strip of the generated code
+            constexpr int S = decltype(st)::value;
+            if constexpr (S < awe_k3gen::kNStrips) {
+                if (kind == 0) awe_k3gen::k3_node_shoot<1, S>(pin, u_ref, cst.data(), val.data(), tan.data());
+                else awe_k3gen::k3_node_radau<1, S>(pin, u_ref, cxx, inv_tf, cst.data(), val.data(), tan.data());
+            }
+        };
+        strip(std::integral_constant<int, 0>{});
+        strip(std::integral_constant<int, 1>{});
+        strip(std::integral_constant<int, 2>{});
+        strip(std::integral_constant<int, 3>{});
+        static_assert(awe_k3gen::kNStrips <= 4, "checker covers up to 4 strips");
         double dv = 0.0, dt = 0.0, tmax = 0.0;
         int covered = 0;
         const int nrows = kind == 0 ? k3t::kRowsPerNode : K3_N_EQ;

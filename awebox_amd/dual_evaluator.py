@@ -22,7 +22,8 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libawedual
 EXPORTED_SYMBOLS = ["adl_create", "adl_destroy", "adl_last_error", "adl_sizes", "adl_sparsity_jac",
                     "adl_sparsity_jac_static", "adl_colour_counts", "adl_eval_nlp", "adl_eval_nlp_host",
                     "adl_last_kernel_ms", "adl_node_eval_host", "adl_hess_nnz", "adl_sparsity_hess",
-                    "adl_sparsity_hess_static", "adl_eval_hess", "adl_eval_hess_host", "adl_last_hess_ms"]
+                    "adl_sparsity_hess_static", "adl_eval_hess", "adl_eval_hess_host", "adl_last_hess_ms",
+                    "adl_gen_status", "adl_eval_nlp_im", "adl_last_kernel_ms_im"]
 
 
 def load_library(path: str = _LIB_PATH):
@@ -52,6 +53,9 @@ def load_library(path: str = _LIB_PATH):
     lib.adl_eval_hess.argtypes = [h] + [ctypes.c_void_p] * 6
     lib.adl_eval_hess_host.argtypes = [h, dp, dp, dp, dp, dp]
     lib.adl_last_hess_ms.argtypes = [h, ctypes.POINTER(ctypes.c_float)]
+    lib.adl_gen_status.argtypes = [h, ip]
+    lib.adl_eval_nlp_im.argtypes = [h] + [ctypes.c_void_p] * 6 + [ctypes.c_size_t, ctypes.c_void_p]
+    lib.adl_last_kernel_ms_im.argtypes = [h] + [ctypes.POINTER(ctypes.c_float)] * 4
     _LIB = lib
     return lib
 
@@ -168,21 +172,64 @@ class DualEvaluator:
         import scipy.sparse as sp
         return sp.csc_matrix((np.asarray(values), self._row, self._colind), shape=(self.n_g, self.n_v))
 
+    @property
+    def generated_available(self) -> bool:
+        """Whether the generated instance-minor path (adl_eval_nlp_im) serves these constants."""
+        ok = ctypes.c_int()
+        self._check(self._lib.adl_gen_status(self._h, ctypes.byref(ok)))
+        return bool(ok.value)
+
     def eval_nlp_device(self, V, P, f, g, grad_f, jac, stream=None):
-        """f, g, grad f, J_g for all instances; contiguous float64 CUDA tensors [B, n_v], [B, n_p],
-        [B], [B, n_g], [B, n_v], [B, nnz]."""
+        """f, g, grad f, J_g for all instances; float64 CUDA tensors V [B, n_v], P [B, n_p], f [B],
+        g [B, n_g] (contiguous) and grad_f [B, n_v], jac [B, nnz]: both contiguous (adl_eval_nlp, the
+        colour kernel), or both instance-minor views ``x_t.t()`` of contiguous [n, ld] tensors with one
+        ld >= B (adl_eval_nlp_im, the generated node code; ``alloc_grad`` / ``alloc_jac``)."""
         import torch
-        for t, n in ((V, self.n_v), (P, self.n_p), (f, 1), (g, self.n_g), (grad_f, self.n_v), (jac, self.nnz)):
+        for t, n in ((V, self.n_v), (P, self.n_p), (f, 1), (g, self.n_g)):
             if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
                 raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+        for t, n in ((grad_f, self.n_v), (jac, self.nnz)):
+            if t.dtype != torch.float64 or not t.is_cuda or tuple(t.shape) != (self.batch, n):
+                raise ValueError("grad_f and jac must be float64 CUDA tensors [batch, n]")
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        self._check(self._lib.adl_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
-                                           grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
+        im = lambda t: t.stride(0) == 1 and t.stride(1) >= self.batch   # noqa: E731
+        if jac.is_contiguous() and grad_f.is_contiguous():
+            self._check(self._lib.adl_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
+                                               grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
+        elif im(jac) and im(grad_f) and jac.stride(1) == grad_f.stride(1):
+            self._check(self._lib.adl_eval_nlp_im(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
+                                                  grad_f.data_ptr(), jac.data_ptr(), int(jac.stride(1)),
+                                                  ctypes.c_void_p(s)))
+        else:
+            raise ValueError("jac and grad_f must both be contiguous or both instance-minor views "
+                             "(strides (1, ld), one ld)")
+
+    def alloc_jac(self, device="cuda", instance_minor=False):
+        """A J_g value tensor [B, nnz]: instance-minor (the transposed view of [nnz, B], written by the
+        generated path with coalesced stores) when asked for, per instance otherwise."""
+        import torch
+        if instance_minor:
+            return torch.zeros(self.nnz, self.batch, dtype=torch.float64, device=device).t()
+        return torch.zeros(self.batch, self.nnz, dtype=torch.float64, device=device)
+
+    def alloc_grad(self, device="cuda", instance_minor=False):
+        """A grad f tensor [B, n_v] in the layout of ``alloc_jac``."""
+        import torch
+        if instance_minor:
+            return torch.zeros(self.n_v, self.batch, dtype=torch.float64, device=device).t()
+        return torch.zeros(self.batch, self.n_v, dtype=torch.float64, device=device)
 
     def last_kernel_ms(self):
         a, b = ctypes.c_float(), ctypes.c_float()
         self._check(self._lib.adl_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def last_kernel_ms_im(self):
+        """(input transposition, node kernel, interval kernel, finalize) of the last instance-minor
+        evaluation, ms."""
+        v = [ctypes.c_float() for _ in range(4)]
+        self._check(self._lib.adl_last_kernel_ms_im(self._h, *(ctypes.byref(x) for x in v)))
+        return tuple(x.value for x in v)
 
     def eval_nlp(self, V, P):
         V = np.ascontiguousarray(np.asarray(V, dtype=np.float64).reshape(self.batch, self.n_v))

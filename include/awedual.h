@@ -28,6 +28,8 @@
 #ifndef AWEDUAL_H
 #define AWEDUAL_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -105,6 +107,20 @@ int adl_eval_nlp_host(adl_handle h, const double* V, const double* P, double* f,
                       double* jac);
 /* Kernel time of the last adl_eval_nlp (HIP events), milliseconds. */
 int adl_last_kernel_ms(adl_handle h, float* ms_main, float* ms_finalize);
+
+/* Generated instance-minor path (the node code generated from the model at build time,
+ * awebox_amd/csrc/gen/dual_jacgen.cpp; one lane per instance): *available = 1 when it serves the
+ * handle's constants (otherwise adl_last_error says why).  adl_eval_nlp_im returns the same f, g,
+ * grad f and J_g as adl_eval_nlp (to rounding) with grad_f and jac instance-minor,
+ * grad_f[i * ld + b], jac[e * ld + b] (ld >= batch); device pointers, asynchronous on `stream`.
+ * Replaces the same oracle surface (nlp_f / nlp_g / nlp_grad_f / nlp_jac_g of
+ * awebox/opti/preparation.py:366-400) for a batch of dual-kite NLPs. */
+int adl_gen_status(adl_handle h, int* available);
+int adl_eval_nlp_im(adl_handle h, const double* V, const double* P, double* f, double* g, double* grad_f,
+                    double* jac, size_t ld, void* stream);
+/* HIP-event times of the last adl_eval_nlp_im: input transposition, node kernel, interval kernel,
+ * finalize (ms). */
+int adl_last_kernel_ms_im(adl_handle h, float* ms_in, float* ms_node, float* ms_interval, float* ms_fin);
 
 /* Hessian of the Lagrangian sigma f + lam_g^T g (nlp_hess_l): values of its upper triangle
  * (row <= col) in the fixed CCS pattern of adl_sparsity_hess; sigma[b] and lam_g[b*n_g + i] per

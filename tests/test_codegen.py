@@ -144,3 +144,52 @@ def test_generated_kite3_jacobian_matches_dual_model(k3_checker, k, seed):
         assert r["value_rel"] < 1e-14, (kind, r)
         assert r["tangent_rel"] < 1e-12, (kind, r)
         assert r["tangent_max"] > 1.0
+
+
+# ---- dual kites: csrc/gen/dual_jacgen.cpp -> dual_nodejac.gen.hpp ---------------------------------
+@pytest.fixture(scope="module")
+def dual_checker(tmp_path_factory):
+    tmp = tmp_path_factory.mktemp("dgen")
+    exe = str(tmp / "check_dual")
+    subprocess.run(["g++", "-O1", "-std=c++17", os.path.join(CSRC, "gen", "check_dual_gen.cpp"), "-o", exe],
+                   check=True)
+    return tmp, exe
+
+
+def test_committed_dual_header_is_current():
+    """dual_nodejac.gen.hpp in the tree is what gen/dual_jacgen.cpp writes for the current model."""
+    before = open(B.DUAL_HEADER).read()
+    B.generate(force=True)
+    assert open(B.DUAL_HEADER).read() == before, "dual_nodejac.gen.hpp is stale: run python -m awebox_amd.build"
+
+
+@pytest.mark.parametrize("k,seed", [(0, 0), (41, 1), (59, 2)])
+def test_generated_dual_jacobian_matches_dual_model(dual_checker, k, seed):
+    """Every entry of the dual-kite node Jacobian pattern (both node kinds, all four wavefront roles),
+    the power / side-slip values and the objective terms' directional derivatives against one
+    dual-number pass of dual_node per seed direction (csrc/gen/check_dual_gen.cpp)."""
+    from awebox_amd import dual as du
+    tmp, exe = dual_checker
+    mc = du.build_constants(du.MultiConfig(n_k=60, d=4))
+    lay = du.layout_for(mc)
+    V = du.batch_member(du.initial_guess(mc, lay), lay, seed)
+    rng = np.random.default_rng(seed)
+    w = np.concatenate([V[lay.x(k)], V[lay.xdot(k)], V[lay.u(k)], V[lay.z(k)], V[lay.node_theta_index(k)],
+                        V[lay.phi()][:1]])
+    w = w * (1 + 0.05 * rng.standard_normal(w.shape)) + 0.01 * rng.standard_normal(w.shape)
+    assert w.size == 127
+    np.savetxt(str(tmp / "consts.txt"), mc.consts)
+    np.savetxt(str(tmp / "theta0.txt"), mc.theta0)
+    np.savetxt(str(tmp / "w.txt"), w)
+    cxx, inv_tf = 2.0 + rng.random(), 1.0 / (10.0 + 5.0 * rng.random())
+    ex2, ex3 = 0.1 + rng.random(), -(0.1 + rng.random())
+    out = subprocess.run([exe, str(tmp / "consts.txt"), str(tmp / "theta0.txt"), str(tmp / "w.txt"), repr(cxx),
+                          repr(inv_tf), repr(ex2), repr(ex3)], check=True, capture_output=True, text=True)
+    rec = json.loads(out.stdout)
+    for kind in ("shooting", "radau"):
+        r = rec[kind]
+        assert r["entries"] == r["n_tan"], "every tangent slot is a pattern entry"
+        assert r["value_rel"] < 1e-13, (kind, r)
+        assert r["tangent_rel"] < 1e-11, (kind, r)
+        assert r["tangent_max"] > 1.0
+    assert rec["radau"]["obv_rel"] < 1e-13 and rec["radau"]["dbp_rel"] < 1e-11, rec["radau"]

@@ -128,3 +128,52 @@ def test_dual_nonfinite_is_an_error(gpu):
     ev = DualEvaluator(mc, batch=1)
     with pytest.raises(AwegpuError):
         ev.eval_nlp(V, du.pack_p(lay, mc, V0))
+
+
+@pytest.mark.parametrize("n_k,batch", [(60, 130), (20, 8), (5, 3)])
+def test_dual_generated_path_matches_oracle_and_colour_kernel(gpu, n_k, batch):
+    """adl_eval_nlp_im (generated node code, four wavefront roles per node, instance-minor J_g and
+    grad f; ragged last instance block at B = 130) against the oracle for three instances and against
+    the colour kernel for all, with different u_ref and homotopy steps across the batch."""
+    torch = gpu
+    from awebox_amd.dual_evaluator import DualEvaluator
+    mc, lay, V0, o = _setup(n_k, 4)
+    steps = ("power1", "fictitious0", "final0")
+    Vs = np.stack([du.batch_member(V0, lay, b) for b in range(batch)])
+    Ps = np.stack([du.pack_p(lay, mc, V0, steps[b % 3], u_ref=5.0 + 3.0 * b / max(batch - 1, 1))
+                   for b in range(batch)])
+    ev = DualEvaluator(mc, batch=batch)
+    assert ev.generated_available
+    Vt, Pt = torch.tensor(Vs, device="cuda"), torch.tensor(Ps, device="cuda")
+    out = {}
+    for im in (True, False):
+        f = torch.full((batch,), float("nan"), dtype=torch.float64, device="cuda")
+        g = torch.full((batch, ev.n_g), float("nan"), dtype=torch.float64, device="cuda")
+        gr, jac = ev.alloc_grad("cuda", instance_minor=im), ev.alloc_jac("cuda", instance_minor=im)
+        gr.fill_(float("nan"))
+        jac.fill_(float("nan"))
+        ev.eval_nlp_device(Vt, Pt, f, g, gr, jac)
+        torch.cuda.synchronize()
+        out[im] = [t.cpu().numpy() for t in (f, g, gr, jac)]
+    fi, gi, gri, ji = out[True]
+    assert np.isfinite(fi).all() and np.isfinite(gi).all() and np.isfinite(gri).all() and np.isfinite(ji).all()
+    fc, gcol, grc, jc = out[False]
+    assert np.allclose(fi, fc, rtol=1e-12, atol=0)
+    for b in range(batch):
+        _close(gi[b], gcol[b], f"g[{b}] vs colour")
+        _close(gri[b], grc[b], f"grad_f[{b}] vs colour")
+        _close(ji[b], jc[b], f"jac[{b}] vs colour")
+    for b in sorted({0, batch // 2, batch - 1}):
+        f, g, grad, J = _oracle_all(o, lay, Vs[b], Ps[b], sparse=n_k >= 10)
+        assert abs(fi[b] - f) <= 1e-12 * max(abs(f), 1e-300)
+        _close(gi[b], g, f"g[{b}]")
+        _close(gri[b], grad, f"grad_f[{b}]")
+        _close_jac(ev.jac_csc(ji[b]), J, f"J[{b}]")
+    # deterministic: a second evaluation repeats every output bitwise
+    f2 = torch.empty(batch, dtype=torch.float64, device="cuda")
+    g2 = torch.empty(batch, ev.n_g, dtype=torch.float64, device="cuda")
+    gr2, jac2 = ev.alloc_grad("cuda", instance_minor=True), ev.alloc_jac("cuda", instance_minor=True)
+    ev.eval_nlp_device(Vt, Pt, f2, g2, gr2, jac2)
+    torch.cuda.synchronize()
+    for a, b in zip(out[True], (f2, g2, gr2, jac2)):
+        assert np.array_equal(a, b.cpu().numpy())

@@ -83,3 +83,26 @@ def test_awelu_exports_every_header_symbol():
                         "awelu_sym_inertia_batched", "awelu_gather_sum", "awelu_last_error"}
     out = subprocess.run(["nm", "-D", "--defined-only", LIB_LU], capture_output=True, text=True, check=True).stdout
     assert declared <= set(re.findall(r"\bT (awelu_\w+)", out))
+
+
+@pytest.mark.parametrize("lib_attr,header,prefix,module", [
+    ("LIB_DUAL", "awedual.h", "adl_", "awebox_amd.dual_evaluator"),
+    ("LIB_MPC", "awempc.h", "awempc_", "awebox_amd.mpc")])
+def test_model_libraries_export_every_header_symbol(lib_attr, header, prefix, module):
+    """libawedual.so / libawempc.so export what their headers declare, and the ctypes bindings bind
+    every declared entry point (no compute: this runs without a GPU)."""
+    import importlib
+
+    from awebox_amd import build as B
+    path = getattr(B, lib_attr)
+    B.build_one(path)
+    hdr = os.path.join(os.path.dirname(HEADER), header)
+    declared = set(re.findall(r"^(?:int|const char\*)\s+(" + prefix + r"\w+)\(", open(hdr).read(), re.M))
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    assert declared <= set(re.findall(r"\bT (" + prefix + r"\w+)", out))
+    mod = importlib.import_module(module)
+    lib = mod.load_library()
+    for name in declared:
+        assert getattr(lib, name) is not None
+    if hasattr(mod, "EXPORTED_SYMBOLS"):
+        assert declared == set(mod.EXPORTED_SYMBOLS)
