@@ -188,6 +188,8 @@ struct ImRef {
 // opens with a distinct empty asm statement: the roles' bodies all begin by loading the same node
 // inputs and theta0 entries, and without the marker the compiler hoists those loads above the branch,
 // where ~220 doubles then stay live through every role (3,000 VGPRs spilled to scratch)
+// diagnostics: -DDGEN_ONLY_ROLE=r (with -DDGEN_RADAU_ONLY) compiles one role of the Radau node alone,
+// to read its register use and scratch size (-Rpass-analysis=kernel-resource-usage)
 #ifndef DGEN_ONLY_ROLE
 #define DGEN_ONLY_ROLE -1
 #endif
@@ -539,16 +541,25 @@ __global__ __launch_bounds__(64) void dual_gen_finalize_kernel(const double* __r
     double tr = 0.0, ot = 0.0, e_end = 0.0, A0 = 0.0, A1 = 0.0, pdt = 0.0, pls = 0.0, pds = 0.0;
     double ptf0 = 0.0, ptf1 = 0.0;
     const double tf0 = V(1), tf1 = a.single ? V(2) : V(1);
-    for (int k = 0; k < a.n_k; ++k) {
-        double q[7];
+    constexpr int U = 4;                       // intervals whose partials are loaded together
+    for (int k0 = 0; k0 < a.n_k; k0 += U) {
+        double q[U][7];
 #pragma unroll
-        for (int e = 0; e < 7; ++e) q[e] = im::at(part, (unsigned)(k * kNPart + e), ld8, lb);
-        const bool ph1 = a.single && k >= a.nkr;
-        tr += q[0];
-        ot += q[1];
-        e_end += (ph1 ? tf1 : tf0) * q[2];
-        if (ph1) { A1 += q[2]; ptf1 += q[4]; } else { A0 += q[2]; ptf0 += q[4]; }
-        pdt += q[3]; pls += q[5]; pds += q[6];
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int e = 0; e < 7; ++e)
+                q[u][e] = im::at(part, (unsigned)(min(k0 + u, a.n_k - 1) * kNPart + e), ld8, lb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {          // summed in interval order
+            const int k = k0 + u;
+            if (k >= a.n_k) break;
+            const bool ph1 = a.single && k >= a.nkr;
+            tr += q[u][0];
+            ot += q[u][1];
+            e_end += (ph1 ? tf1 : tf0) * q[u][2];
+            if (ph1) { A1 += q[u][2]; ptf1 += q[u][4]; } else { A0 += q[u][2]; ptf0 += q[u][4]; }
+            pdt += q[u][3]; pls += q[u][5]; pds += q[u][6];
+        }
     }
     const double T = period(VT, a, lb);
     const double Tref = period(PT, a, lb);

@@ -66,7 +66,8 @@ struct KindOut {
 // anticollision, the power integrand).  Each group is its own function body that recomputes the
 // values it needs, so that three wavefronts evaluate one node side by side and each keeps about one
 // kite's working set in registers (one body for all rows peaks at ~490 live doubles).
-constexpr int kGroups = 5;
+constexpr int kGroups = 7;
+const bool kSplitKites = std::getenv("AWE_DUAL_SPLIT_KITES") != nullptr;
 int row_group(int r) {
     using namespace awe::dl;
     if (r < 0) return 2;
@@ -101,7 +102,7 @@ KindOut generate(int kind, const std::vector<double>& cst, const Tables& T, int 
     awe::dual_node<Sym>(SymIn{w.data()}, w[awe::dl::kGamma], th.data(), cs.data(), sink, kind == 0,
                         awe::DualInlineSubmodels(), first_kite);
     // the Radau node's objective terms, one per row group: ex2 beta_2^2, ex2 beta_3^2, ex3 p
-    int objt[kGroups] = {-1, -1, -1, -1, -1};
+    int objt[kGroups] = {-1, -1, -1, -1, -1, -1, -1};
     if (kind == 1) {
         const Sym cb = Sym::of(tape.leaf(Op::Extra, 2)), cpp = Sym::of(tape.leaf(Op::Extra, 3));
         for (int k = 0; k < ADL_NKITES; ++k) {
@@ -146,15 +147,22 @@ KindOut generate(int kind, const std::vector<double>& cst, const Tables& T, int 
     }
     std::vector<int> store_group;                  // row group of every store
     for (auto& st : stores) store_group.push_back(row_group(st.row));
-    {   // node 1's translation rows: tangents split in two direction ranges of equal counts
+    // tangents of a group split in two direction ranges of equal counts: node 1's translation rows
+    // (group 2 -> 2, 4), and with kSplitKites each kite's rows (0 -> 0, 5; 1 -> 1, 6)
+    auto split = [&](int from, int to) {
         std::vector<int> per_dir(kDirs, 0);
         int total = 0;
         for (size_t i = 0; i < stores.size(); ++i)
-            if (store_group[i] == 2 && stores[i].kind == 1) { per_dir[stores[i].dir]++; total++; }
+            if (store_group[i] == from && stores[i].kind == 1) { per_dir[stores[i].dir]++; total++; }
         std::vector<int> half(kDirs, 0);
         for (int dir = 0, acc = 0; dir < kDirs; ++dir) { half[dir] = 2 * acc >= total; acc += per_dir[dir]; }
         for (size_t i = 0; i < stores.size(); ++i)
-            if (store_group[i] == 2 && stores[i].kind == 1 && half[stores[i].dir]) store_group[i] = 4;
+            if (store_group[i] == from && stores[i].kind == 1 && half[stores[i].dir]) store_group[i] = to;
+    };
+    split(2, 4);
+    if (kSplitKites) {
+        split(0, 5);
+        split(1, 6);
     }
     if (kind == 1) {   // power and side slips (obv), tangents of the node's objective terms (dbp)
         stores.push_back({sink.rows[kRowPower], 3, 0, -1});
@@ -225,9 +233,11 @@ int main(int argc, char** argv) {
     // groups 0 and 2 from the trace in the model's order, group 1 (kite 3) from the trace with kite 3
     // first; slots numbered group after group, dbp entries kite 2, node 1, kite 3
     auto gen_kind = [&](int kind) {
-        KindOut a = generate(kind, cst, T, 0, {0}, 0);
-        KindOut c = generate(kind, cst, T, 1, {1}, a.group_stats[0].n_tan);
-        KindOut b = generate(kind, cst, T, 0, {2, 4, 3}, a.group_stats[0].n_tan + c.group_stats[1].n_tan);
+        KindOut a = generate(kind, cst, T, 0, {0, 5}, 0);
+        const int na = a.group_stats[0].n_tan + a.group_stats[5].n_tan;
+        KindOut c = generate(kind, cst, T, 1, {1, 6}, na);
+        const int nc = c.group_stats[1].n_tan + c.group_stats[6].n_tan;
+        KindOut b = generate(kind, cst, T, 0, {2, 4, 3}, na + nc);
         KindOut o = a;
         for (KindOut* x : {&c, &b})
             for (int g = 0; g < kGroups; ++g)
@@ -249,7 +259,9 @@ int main(int argc, char** argv) {
     // wavefront roles: kite 2's rows, kite 3's rows, node 1's translation rows along the first half
     // of their directions, then the second half and the remaining rows (groups 4 and 3, each in its
     // own scope: both come from one trace, so their statement names repeat)
-    const std::vector<std::vector<int>> role_groups = {{0}, {1}, {2}, {4, 3}};
+    const std::vector<std::vector<int>> role_groups =
+        kSplitKites ? std::vector<std::vector<int>>{{0}, {5}, {1}, {6}, {2}, {4, 3}}
+                    : std::vector<std::vector<int>>{{0}, {1}, {2}, {4, 3}};
     auto bodies = [&](const KindOut& k) {
         std::string b;
         for (size_t r = 0; r < role_groups.size(); ++r) {

@@ -32,6 +32,7 @@ from __future__ import annotations
 import math
 import os
 import time
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -318,11 +319,18 @@ class _ScatterSum:
             return self.add_into(out, vals[..., sel])
         key = (sel.data_ptr(), sel.numel())
         ent = self._sel_lanes.get(key)
+        if ent is not None and ent[0]() is not sel:          # the address of a freed sel, reused
+            ent = None
         if ent is None:
             s_h = sel.cpu().numpy()
             lsrc = self.lanes_host[0]
             comp = np.where(lsrc >= 0, s_h[np.clip(lsrc, 0, None)], -1)
-            ent = self._sel_lanes[key] = (sel, torch.tensor(comp.astype(np.int32), device=self.dev))
+            lanes = self._sel_lanes
+
+            def _drop(r, k=key):                              # the entry dies with its sel tensor
+                if lanes.get(k, (None,))[0] is r:
+                    del lanes[k]
+            ent = lanes[key] = (weakref.ref(sel, _drop), torch.tensor(comp.astype(np.int32), device=self.dev))
         self._launch(out, vals, ent[1])
         if self.wide:
             self._torch_buckets(out, vals[..., sel], self.wide)
@@ -346,7 +354,10 @@ def scatter_sum(dst, dev) -> _ScatterSum:
     """The _ScatterSum of a destination pattern, shared by every structure with the same pattern on
     the same device: the homotopy builds a StructuredKKT per step (and per sweep shard), and the
     host-side table construction was ~0.8 s of a 6-step AP2 homotopy (cProfile,
-    profiles/r02/solver_pstats_b8.txt).  The tables are read-only after construction."""
+    profiles/r02/solver_pstats_b8.txt).  The tables are read-only after construction, apart from
+    add_into_sel's lanes composed with a caller's index tensor: those entries are held through a
+    weak reference to that tensor and dropped when it is freed, so structures evicted from the
+    caches release their device tables."""
     import hashlib
     dst = np.ascontiguousarray(np.asarray(dst, dtype=np.int64).reshape(-1))
     key = (hashlib.sha1(dst.tobytes()).hexdigest(), dst.size, str(torch.device(dev)))

@@ -500,8 +500,10 @@ def dual_block(B, rank, dev, dist, world, steps=20, warmup=3, cpu_seconds=0.0):
     ev = DualEvaluator(c, batch=B)
     f = torch.empty(B, dtype=torch.float64, device=dev)
     g = torch.empty(B, ev.n_g, dtype=torch.float64, device=dev)
-    gr = torch.empty(B, ev.n_v, dtype=torch.float64, device=dev)
-    jac = torch.empty(B, ev.nnz, dtype=torch.float64, device=dev)
+    # the generated instance-minor path (adl_eval_nlp_im) when it serves these constants; the colour
+    # kernel (adl_eval_nlp, per-instance layout) is timed beside it for the record
+    gen = ev.generated_available
+    gr, jac = ev.alloc_grad(dev, instance_minor=gen), ev.alloc_jac(dev, instance_minor=gen)
     s = torch.cuda.current_stream(dev).cuda_stream
     for _ in range(warmup):
         ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
@@ -519,15 +521,31 @@ def dual_block(B, rank, dev, dist, world, steps=20, warmup=3, cpu_seconds=0.0):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kms, fms = [], []
+    kms, fms, parts = [], [], []
     for _ in range(10):
         ev.eval_nlp_device(V, P, f, g, gr, jac, stream=s)
-        a, b_ = ev.last_kernel_ms()
-        kms.append(a)
-        fms.append(b_)
+        if gen:
+            pt = ev.last_kernel_ms_im()
+            parts.append(pt)
+            kms.append(sum(pt[:3]))
+            fms.append(pt[3])
+        else:
+            a, b_ = ev.last_kernel_ms()
+            kms.append(a)
+            fms.append(b_)
+    finite = bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item())
+    colour_ms = None
+    if gen:
+        gr_c, jac_c = ev.alloc_grad(dev), ev.alloc_jac(dev)
+        cms = []
+        for _ in range(5):
+            ev.eval_nlp_device(V, P, f, g, gr_c, jac_c, stream=s)
+            cms.append(sum(ev.last_kernel_ms()))
+        colour_ms = float(np.mean(cms))
+        del gr_c, jac_c
     m = c.model
     bytes_per_eval = 8 * (lay.n_v + lay.n_v + pb_ntheta0() + m.nw + 20 + lay.n_g + lay.n_v + ev.nnz + 1)
-    kernel_ms = float(np.mean(kms))
+    kernel_ms = float(np.mean(kms)) + float(np.mean(fms))
     achieved = bytes_per_eval * B / (kernel_ms * 1e-3) / 1e9
     ncol = colour_counts(c)
     cpu = None
@@ -556,12 +574,18 @@ def dual_block(B, rank, dev, dist, world, steps=20, warmup=3, cpu_seconds=0.0):
             "value": B * steps * world / el, "unit": "evals/s", "instances_per_gpu": B,
             "ms_per_step": el / steps * 1e3, "n_v": lay.n_v, "n_g": lay.n_g, "nnz_jac": ev.nnz,
             "colours_shooting_radau": [ncol[0], ncol[1]],
-            "finite": bool(torch.isfinite(jac).all().item() and torch.isfinite(g).all().item()),
+            "finite": finite,
+            "eval_path": "generated instance-minor (adl_eval_nlp_im)" if gen else "colour kernel",
+            "colour_kernel_ms": colour_ms,
             "roofline": dict({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": achieved / HBM_PEAK_GBS, "kernel": "dual_interval_kernel<4>",
+                              "frac": achieved / HBM_PEAK_GBS,
+                              "kernel": ("dual_gen_in + dual_gen_node + dual_gen_interval + dual_gen_finalize "
+                                         "(one evaluation)" if gen else "dual_interval_kernel<4> + dual_finalize_kernel"),
                               "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)),
                               "bytes_per_eval": bytes_per_eval, "traffic": None},
-                             **(config_traffic("dual", B, kernel_ms) or {})),
+                             **({"kernel_ms_parts": dict(zip(("transpose_in", "node", "interval", "finalize"),
+                                                             np.mean(parts, axis=0).tolist()))} if gen else
+                                (config_traffic("dual", B, kernel_ms) or {}))),
             "cpu_baseline": cpu}
 
 

@@ -80,3 +80,19 @@ def test_instance_minor_path_is_default_and_matches_the_other_paths(B):
     for a, b in zip(out["generated"], out["colour"]):
         for i in range(B):
             _close(a[i], b[i])
+
+
+@pytest.mark.parametrize("B", [70, 1])
+def test_colour_and_generated_paths_in_the_solvers_layout(B):
+    """awe_eval_nlp_im on the colour and the node + gather paths (per-instance evaluation into the
+    handle's scratch, then transposed into the instance-minor J_g and grad f the solver allocates)
+    equal the same path's per-instance layout bitwise, at a ragged batch and at B = 1."""
+    from awebox_amd import evaluator as E
+    consts, V, P = _inputs(B)
+    ev = E.Ap2Evaluator(consts, batch=B)
+    for path in ("colour", "generated"):
+        im = _eval(ev, V, P, path, True)
+        aos = _eval(ev, V, P, path, False)
+        for lab, a, b in zip(("f", "g", "grad_f", "jac"), im, aos):
+            assert np.isfinite(a).all(), (path, lab)
+            assert np.array_equal(a, b), (path, lab, float(np.max(np.abs(a - b))))
