@@ -25,11 +25,7 @@ namespace {
 using namespace dlt;
 thread_local std::string g_err;
 
-constexpr int kNPart = 8;
-constexpr int kCostTracking = 0, kCostURegularisation = 1, kCostXdotRegularisation = 2, kCostFictitious = 10,
-              kCostPower = 11, kCostTf = 13, kCostThetaRegularisation = 14, kCostBeta = 18;
-constexpr int kPhiCost[7] = {3, 6, 4, 5, 7, 8, 9};
-constexpr int kPhiPsi = 3;
+// objective constants (kNPart, kCost*, kPhiCost, kPhiPsi): dual_tables.hpp
 
 struct Handle {
     Tables t;

@@ -12,7 +12,7 @@ step() {  # step <limit> <log> <cmd...>
     echo "=== $log rc=$rc"; tail -2 "gpurun_out/$log"
     if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step 900 pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+step 1200 pytest_gpu.log python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread --durations=15
 step 300 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
 step 600 bench.log python bench.py
 step 300 rocprof_ap2.log rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ap2 -o run --output-format csv -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --sweep-points 0 --dual-sweep-points 0 --no-hessian --no-latency
