@@ -74,9 +74,11 @@ SOURCES = {   # the files each evaluator kernel is built from (a PMC record is t
     "ap2": ["awebox_amd/csrc/ap2_model.hpp", "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/awegpu.hip",
             "awebox_amd/csrc/scalar.hpp", "awebox_amd/csrc/ap2_nodejac.gen.hpp", "include/awegpu.h"],
     "dual": ["awebox_amd/csrc/dual_model.hpp", "awebox_amd/csrc/dual_tables.hpp", "awebox_amd/csrc/awedual.hip",
+             "awebox_amd/csrc/awedual_gen.hip", "awebox_amd/csrc/dual_nodejac.gen.hpp", "awebox_amd/csrc/im_layout.hpp",
              "awebox_amd/csrc/ap2_model.hpp", "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/scalar.hpp",
              "include/awedual.h", "include/awegpu.h"],
     "mpc": ["awebox_amd/csrc/kite3_model.hpp", "awebox_amd/csrc/kite3_tables.hpp", "awebox_amd/csrc/awempc.hip",
+            "awebox_amd/csrc/kite3_nodejac.gen.hpp", "awebox_amd/csrc/im_layout.hpp",
             "awebox_amd/csrc/ap2_tables.hpp", "awebox_amd/csrc/scalar.hpp", "include/awempc.h", "include/awegpu.h"],
 }
 PMC_RECORD_CONFIGS = os.path.join(ROOT, "profiles", "pmc_traffic_configs.json")
@@ -584,8 +586,8 @@ def dual_block(B, rank, dev, dist, world, steps=20, warmup=3, cpu_seconds=0.0):
                               "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)),
                               "bytes_per_eval": bytes_per_eval, "traffic": None},
                              **({"kernel_ms_parts": dict(zip(("transpose_in", "node", "interval", "finalize"),
-                                                             np.mean(parts, axis=0).tolist()))} if gen else
-                                (config_traffic("dual", B, kernel_ms) or {}))),
+                                                             np.mean(parts, axis=0).tolist()))} if gen else {}),
+                             **((config_traffic("dual", B, kernel_ms) or {}) if gen else {})),
             "cpu_baseline": cpu}
 
 
@@ -667,7 +669,8 @@ def mpc_block(B, rank, dev, dist, world, steps=50, warmup=5):
                                          if gen else "mpc_interval_kernel<4> + mpc_finalize_kernel"),
                               "kernel_ms": kernel_ms, "bytes_per_eval": bytes_per_eval, "traffic": None},
                              **({"kernel_ms_parts": dict(zip(("transpose_in", "node", "finalize"),
-                                                             np.mean(parts, axis=0).tolist()))} if gen else {})),
+                                                             np.mean(parts, axis=0).tolist()))} if gen else {}),
+                             **((config_traffic("mpc", B, kernel_ms) or {}) if gen else {})),
             "eval_path": "generated instance-minor (awempc_eval_nlp_im)" if gen else "dual-number kernel",
             "dual_kernel_ms": float(np.mean(dms)),
             "rti": rti}

@@ -1,5 +1,6 @@
 """Short driver for PMC passes over the config-3 and config-5 evaluators (no solver, no sweep):
-5 batched evaluations of the dual-kite NLP (B=128) and of the tracking-MPC NLP (B=256).
+5 batched evaluations of the dual-kite NLP (B=128) and of the tracking-MPC NLP (B=256), on the
+paths and layouts the bench measures (the generated instance-minor paths).
 
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_cfg_fetch -o run --output-format csv -- python tools/pmc_kernels.py
 """
@@ -65,6 +66,9 @@ def main():
         return ap2()
     if "--hess" in sys.argv:
         return hess()
+    # --dual / --mpc: one configuration per process (both generated paths start with the same
+    # im::transpose_in_kernel, which the per-kernel summary must not mix)
+    want = [w for w in ("dual", "mpc") if "--" + w in sys.argv] or ["dual", "mpc"]
 
     from awebox_amd import dual as du
     from awebox_amd import kite3 as k3
@@ -79,11 +83,16 @@ def main():
     V = torch.tensor(np.stack([du.batch_member(v0, lay, b) for b in range(B)]), device=dev)
     P = torch.tensor(np.stack([du.pack_p(lay, c, v0)] * B), device=dev)
     ev = DualEvaluator(c, batch=B)
+    # the bench's layout: instance-minor J_g / grad f on the generated path when it serves the handle
+    gen = ev.generated_available
     out = [torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, ev.n_g, dtype=torch.float64, device=dev),
-           torch.empty(B, ev.n_v, dtype=torch.float64, device=dev), torch.empty(B, ev.nnz, dtype=torch.float64, device=dev)]
-    for _ in range(5):
+           ev.alloc_grad(dev, instance_minor=gen), ev.alloc_jac(dev, instance_minor=gen)]
+    for _ in range(5 if "dual" in want else 0):
         ev.eval_nlp_device(V, P, *out)
     torch.cuda.synchronize()
+    if "mpc" not in want:
+        print("pmc_kernels done", flush=True)
+        return
     c3 = k3.build_constants()
     lay3 = k3.MpcLayout(c3.cfg.n_k, c3.cfg.d)
     B = 256
@@ -92,7 +101,7 @@ def main():
     P = torch.tensor(np.stack([p for _, p in inst]), device=dev)
     ev3 = MpcEvaluator(c3, batch=B)
     out = [torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, ev3.n_g, dtype=torch.float64, device=dev),
-           torch.empty(B, ev3.n_v, dtype=torch.float64, device=dev), torch.empty(B, ev3.nnz, dtype=torch.float64, device=dev)]
+           ev3.alloc_grad(dev), ev3.alloc_jac(dev)]
     for _ in range(5):
         ev3.eval_nlp_device(V, P, *out)
     torch.cuda.synchronize()

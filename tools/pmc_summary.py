@@ -36,22 +36,32 @@ def record_configs(fetch_dir, write_dir, *sq_dirs, only=None, hashes=None):
         out = json.load(open(path))
     except (OSError, ValueError):
         out = {}
-    for which, kern, batch in (("dual", "dual_interval_kernel", 128), ("mpc", "mpc_interval_kernel", 256)):
+    # the kernels of one evaluation on the generated instance-minor paths the bench measures
+    configs = (("dual", ("transpose_in_kernel", "dual_gen_node_kernel", "dual_gen_interval_kernel",
+                         "dual_gen_finalize_kernel"), 128),
+               ("mpc", ("transpose_in_kernel", "mpc_gen_node_kernel", "mpc_gen_finalize_kernel"), 256))
+    for which, kerns, batch in configs:
         if only is not None and which not in only:
             continue
-        f = summarise(glob.glob(os.path.join(fetch_dir, "**", "*counter_collection.csv"), recursive=True), kern)
-        w = summarise(glob.glob(os.path.join(write_dir, "**", "*counter_collection.csv"), recursive=True), kern)
-        if "FETCH_SIZE" not in f or "WRITE_SIZE" not in w:
-            continue
-        rec = {"batch": batch, "kernel": kern + "<4>",
+        rec = {"batch": batch, "kernel": " + ".join(kerns),
                "source_hash": (hashes or {}).get(which) or sources_hash(which),
-               "FETCH_SIZE_kB": f["FETCH_SIZE"], "WRITE_SIZE_kB": w["WRITE_SIZE"],
-               "units": "FETCH/WRITE_SIZE in kB per dispatch, SQ_* per dispatch; mean over 5 dispatches "
-                        "(tools/pmc_kernels.py, tools/gpu_records.sh)"}
-        for d in sq_dirs:
-            for k, v in summarise(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True), kern).items():
-                rec[k] = v
-        out[which] = rec
+               "units": "FETCH/WRITE_SIZE in kB, SQ_* counts: per evaluation (the kernels' means per dispatch, "
+                        "summed); 5 evaluations (tools/pmc_kernels.py, tools/gpu_pmc_configs.sh)",
+               "per_kernel": {}}
+        ok = True
+        for kern in kerns:
+            pk = {}
+            for d in (fetch_dir.format(which=which), write_dir.format(which=which)) + tuple(x.format(which=which) for x in sq_dirs):
+                pk.update(summarise(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True), kern))
+            if "FETCH_SIZE" not in pk or "WRITE_SIZE" not in pk:
+                ok = False
+                break
+            rec["per_kernel"][kern] = pk
+            for k, v in pk.items():
+                key = k + "_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else k
+                rec[key] = rec.get(key, 0.0) + v
+        if ok:
+            out[which] = rec
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     print("wrote profiles/pmc_traffic_configs.json", sorted(out))
