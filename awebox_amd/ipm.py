@@ -422,6 +422,13 @@ class StructuredKKT:
     block-tridiagonal chains (awebox_amd/btd.py) or B dense Schur complements.  Every assembly is
     a fixed-order gather-sum (_ScatterSum): the results do not depend on the run."""
 
+    # refinement steps before an instance falls back to a dense LU of its K: IPOPT's
+    # max_refinement_steps.  An instance whose backward error passes within 3 steps (the fused
+    # sweep's earlier budget) is unaffected; on the AP2 sweep the one instance that used to fall back
+    # after 3 converges within 10, with identical iterations and powers and 0.25-0.45 s less wall
+    # time (profiles/r05/solver/sweep_refine)
+    REFINE_STEPS = 10
+
     def __init__(self, nlp, lay, dev, lu_backend="awelu", separators="btd", deterministic=True):
         n, ny, m = nlp.n, nlp.ny, nlp.m
         self.lu_backend = lu_backend
@@ -663,11 +670,8 @@ class StructuredKKT:
         one = rhs.dim() == 1
         rhs = rhs.unsqueeze(0) if one else rhs
         if refine is None:
-            # separators through the block recursion (blocks beyond the fused sweep kernels: the
-            # dual kites) leave larger backward errors than the fused sweep's refined block solves;
-            # they get up to IPOPT's max_refinement_steps (10) before an instance falls back to a
-            # dense LU of the whole K (~0.3 s each at N = 13,848), the fused path keeps 3
-            refine = 10 if (self.use_btd and not self.btd.fused) else 3
+            # the dense fallback is a library LU of the whole K (~0.3 s at N = 12,257 or 13,848)
+            refine = self.REFINE_STEPS
         self.n_solve += 1
         x = self._solve(rhs)
         b_norm = rhs.abs().amax(dim=1)
@@ -753,6 +757,12 @@ def solve(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, opts: Ip
 
 
 _STRUCT_CACHE: dict = {}
+
+
+def cached_kkt_structures():
+    """The StructuredKKT objects of the recent solves' structure cache (read-only use: bench.py
+    times the solver kernels at their block shapes)."""
+    return [e[1] for e in _STRUCT_CACHE.values()]
 
 
 def _structure(ev, nlp, dev, opts):

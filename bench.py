@@ -797,6 +797,86 @@ def sweep_profile(arch: str):
                             for t in rec["top_kernels"][:4]]}
 
 
+def solver_kernels(n_k, batches, reps=5):
+    """Rooflines of the sweep's KKT kernels at the block shapes of its last solves (the structure
+    cache of ipm.solve_batch, interval count n_k), for each batch size in `batches` (the shard's
+    homotopy at B = 1, the fan's batched warm start): the separator sweep (awelu_btd_factor_batched,
+    nb stages of m x m blocks; the dual kites' m > 48 run the block recursion, whose pivot-block LUs
+    are awelu_factor_batched) and the interval blocks' inertia (awelu_sym_inertia_batched, n_k blocks
+    of nI rows per instance).  HIP events on the launch stream around `reps` launches on fresh copies
+    of random blocks (diagonally weighted, symmetric for the inertia).  Algorithmic work per system:
+    Gauss-Jordan sweep (nb - 1) 2 m^3 + nb 6 m^3 flops and 6 m^2 doubles per stage (read L, D, U;
+    write D', W, D'^-1); Bunch-Kaufman n^3 / 3 flops and n^2 doubles read; LU 2 n^3 / 3 flops and
+    2 n^2 doubles.  These chains are latency-bound (a barrier-separated pivot step per column), so
+    both fractions are small; they say how far from either roof the kernels sit."""
+    import ctypes
+
+    import torch
+
+    from awebox_amd import batched_lu as bl
+    from awebox_amd.ipm import ZERO_PIVOT, cached_kkt_structures
+    sks = [s for s in cached_kkt_structures() if s.n_k == n_k and s.btd is not None]
+    if not sks or not torch.cuda.is_available():
+        return None
+    sk = sks[-1]
+    nb, m, nI = sk.btd.nb, sk.btd.m, sk.nI
+    lib = bl.load_library()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream(dev)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def timed(launch, inputs):
+        launch(inputs[0])                                   # warm-up (code object load)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for x in inputs[1:]:
+            launch(x)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / (len(inputs) - 1)
+
+    def line(kernel, shape, systems, ms, flops, doubles):
+        tf = flops * systems / (ms * 1e-3) / 1e12
+        gbs = doubles * 8 * systems / (ms * 1e-3) / 1e9
+        return {"kernel": kernel, "shape": shape, "systems": systems, "ms": ms,
+                "fp64": {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS},
+                "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS},
+                "bound": "latency (dependent pivot columns, one workgroup per system)"}
+
+    out = []
+    f64 = dict(dtype=torch.float64, device=dev)
+    for B in batches:
+        eye = torch.eye(m, **f64)
+        if m <= bl.BTD_MAX_M:
+            T = torch.randn(B, nb, 3, m, m, generator=gen, **f64)
+            T[:, :, 1] += 4.0 * m ** 0.5 * eye
+            Ts = [T.clone() for _ in range(reps + 1)]
+            Dinv = torch.empty(B, nb, m, m, **f64)
+            ms = timed(lambda x: lib.awelu_btd_factor_batched(nb, m, B, ptr(x), ptr(Dinv), ctypes.c_void_p(stream.cuda_stream)), Ts)
+            out.append(line("btd_factor_kernel", f"nb={nb} m={m}", B, ms, (nb - 1) * 2 * m ** 3 + nb * 6 * m ** 3,
+                            nb * 6 * m * m))
+            del Ts
+        else:
+            A = torch.randn(B * nb, m, m, generator=gen, **f64) + 4.0 * m ** 0.5 * eye
+            As = [A.clone() for _ in range(reps + 1)]
+            piv = torch.empty(B * nb, m, dtype=torch.int32, device=dev)
+            ms = timed(lambda x: lib.awelu_factor_batched(m, B * nb, ptr(x), ptr(piv), ctypes.c_void_p(stream.cuda_stream)), As)
+            out.append(line("lu_batched_kernel (separator pivot blocks)", f"n={m}", B * nb, ms, 2 * m ** 3 / 3,
+                            2 * m * m))
+            del As
+        S = torch.randn(B * n_k, nI, nI, generator=gen, **f64)
+        S = S + S.transpose(1, 2)
+        Ss = [S.clone() for _ in range(reps + 1)]
+        counts = torch.empty(B * n_k, 3, dtype=torch.int32, device=dev)
+        ms = timed(lambda x: lib.awelu_sym_inertia_batched(nI, B * n_k, ptr(x), ctypes.c_double(ZERO_PIVOT), ptr(counts),
+                                                           ctypes.c_void_p(stream.cuda_stream)), Ss)
+        out.append(line("sym_inertia_kernel (interval blocks)", f"n={nI}", B * n_k, ms, nI ** 3 / 3, nI * nI))
+        del Ss
+    return out
+
+
 def _grid_points(per_gpu, world):
     """The points of the sweep: the first per_gpu x world of linspace(5, 8, 64) (config 4's grid;
     rank r gets the contiguous block [r per_gpu, (r + 1) per_gpu)), or an even spread over 5..8 m/s
@@ -839,7 +919,8 @@ def sweep_block(per_gpu, world, dist, dev, consts, mode="fan"):
                       "warm start (solve_batch) for the rest; structured KKT (batched interval LU + "
                       "block-tridiagonal separators), exact Hessian, IPOPT inertia correction from exact KKT "
                       "inertia, second-order corrections",
-            "utilisation": sweep_profile("ap2")}
+            "utilisation": sweep_profile("ap2"),
+            "solver_kernels": solver_kernels(consts.cfg.n_k, sorted({1, max(1, per_gpu - 1)}))}
 
 
 def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4, with_chain=True):
@@ -888,7 +969,8 @@ def dual_sweep_block(per_gpu, world, dist, dev, n_k=20, d=4, with_chain=True):
                       "start for the rest; structured KKT with the block-recursion separator sweep, exact KKT "
                       "inertia; exact Hessian of the Lagrangian (dual_hess_kernel: colour-pair hyper-dual forward mode)",
             "mode": "fan: homotopy for the shard's first point, one batched warm start for the rest",
-            "chain": chain, "utilisation": sweep_profile("dual")}
+            "chain": chain, "utilisation": sweep_profile("dual"),
+            "solver_kernels": solver_kernels(n_k, sorted({1, max(1, per_gpu - 1)}))}
 
 
 def hess_gen_counts():

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--arch", choices=["ap2", "dual"], default="ap2")
     ap.add_argument("--points", type=int, default=8)
     ap.add_argument("--profile", action="store_true", help="synchronised phase timings (slower)")
+    ap.add_argument("--refine", type=int, default=None, help="StructuredKKT.REFINE_STEPS override")
     ap.add_argument("--out", default="gpurun_out/sweep_phases.json")
     args = ap.parse_args()
     import torch
@@ -28,6 +29,8 @@ def main():
     import awebox_amd.sweep as sw
     import awebox_amd.trajectory as tr
 
+    if args.refine is not None:
+        ipm.StructuredKKT.REFINE_STEPS = args.refine
     calls = []
     dense = {"n": 0, "s": 0.0}
     orig_sb = ipm.solve_batch
@@ -77,6 +80,7 @@ def main():
         for q, v in c["timing"].items():
             phases[q] = phases.get(q, 0.0) + v
     rec = {"arch": args.arch, "points": args.points, "profile": args.profile, "wall_s": wall,
+           "refine_steps": ipm.StructuredKKT.REFINE_STEPS,
            "trials_per_s": res["trials_per_s"], "iterations": res["iterations"],
            "avg_power_W": [round(p, 3) for p in res["avg_power_W"]], "dense_fallbacks": dense["n"],
            "dense_fallback_s": dense["s"], "phase_s": {q: round(v, 3) for q, v in phases.items()}, "calls": calls}
