@@ -50,6 +50,41 @@ __device__ __forceinline__ void copy_batched(int total, int tid, int nthreads, L
     }
 }
 
+// Max over the 64 lanes of a wave by DPP moves (quad permutes, row rotations, row broadcasts: VALU
+// latency) instead of a __shfl_xor butterfly (six dependent LDS-permute round trips); the result
+// is read from lane 63 and is uniform.  fmax is order-independent, so the value is the butterfly's.
+template <int Ctrl>
+__device__ __forceinline__ double mov_dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, Ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), Ctrl, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+    v = fmax(v, mov_dpp_f64<0xb1>(v));                        // quad_perm [1,0,3,2]
+    v = fmax(v, mov_dpp_f64<0x4e>(v));                        // quad_perm [2,3,0,1]
+    v = fmax(v, mov_dpp_f64<0x124>(v));                       // row_ror 4
+    v = fmax(v, mov_dpp_f64<0x128>(v));                       // row_ror 8
+    v = fmax(v, mov_dpp_f64<0x142>(v));                       // row_bcast 15
+    v = fmax(v, mov_dpp_f64<0x143>(v));                       // row_bcast 31
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Min over the 64 lanes of a wave (the same DPP steps on 32-bit integers); uniform result.
+__device__ __forceinline__ int wave_min_i32(int v) {
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xb1, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4e, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x142, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x143, 0xf, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __restrict__ As, int* __restrict__ pivs) {
     extern __shared__ double panel[];                   // [n][kNB], row-major
     __shared__ double red_v[kThreads / 64];
@@ -78,10 +113,13 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
                 const double v = fabs(panel[r * kNB + c]);
                 if (v > best) { best = v; bi = r; }
             }
-            for (int off = 32; off > 0; off >>= 1) {         // wave reduction by shuffles
-                const double ob = __shfl_xor(best, off);
-                const int oi = __shfl_xor(bi, off);
-                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+            {   // the wave's (largest value, lowest row holding it): a DPP max of the values, then a
+                // DPP min of the rows of the lanes holding it -- the pair the (value, index)
+                // butterfly found, without its twelve dependent LDS permutes (best is never NaN:
+                // NaN does not pass v > best, a lane without rows keeps -1)
+                const double mx = wave_max(best);
+                bi = wave_min_i32(best == mx ? bi : 0x7fffffff);
+                best = mx;
             }
             if ((tid & 63) == 0) {
                 red_v[tid >> 6] = best;
@@ -141,10 +179,14 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
         __syncthreads();
         // ---- U12 (forward substitution with L11) and the trailing update, one column per thread:
         //      the column's kb U12 rows loaded together, then the trailing rows in groups of kRowU
-        //      whose loads are issued one group ahead (a memory latency per group, not per row) --
+        //      whose loads are issued one group ahead (a memory latency per group, not per row).
+        //      Fewer trailing columns than threads / 2 (the last panels; every panel of the MPC's
+        //      126-row blocks): H = threads / columns row chunks per column, one (column, chunk) per
+        //      thread, each chunk's thread repeating the column's substitution (the same operations per
+        //      entry, so the factors are bitwise those of one thread per column); chunk 0 repeats it
+        //      once more after the panel's last barrier, when every chunk has read U12, and stores it --
         constexpr int kRowU = 8;
-        for (int j = k0 + kb + tid; j < n; j += kThreads) {
-            double u[kNB];
+        auto subst = [&](int j, double (&u)[kNB]) {
 #pragma unroll
             for (int r = 0; r < kNB; ++r) u[r] = r < kb ? A[(size_t)(k0 + r) * n + j] : 0.0;
 #pragma unroll
@@ -155,33 +197,62 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
                     u[r] = v;
                 }
             }
+        };
+        auto put_u = [&](int j, const double (&u)[kNB]) {
 #pragma unroll
             for (int r = 0; r < kNB; ++r)
                 if (r < kb) A[(size_t)(k0 + r) * n + j] = u[r];
+        };
+        auto trail = [&](int j, int r0, int r1, const double (&u)[kNB]) {
             double nxt[kRowU];
 #pragma unroll
-            for (int q = 0; q < kRowU; ++q) nxt[q] = kb + q < rows ? A[(size_t)(k0 + kb + q) * n + j] : 0.0;
-            for (int i0 = kb; i0 < rows; i0 += kRowU) {
+            for (int q = 0; q < kRowU; ++q) nxt[q] = r0 + q < r1 ? A[(size_t)(k0 + r0 + q) * n + j] : 0.0;
+            for (int i0 = r0; i0 < r1; i0 += kRowU) {
                 double acc[kRowU];
 #pragma unroll
                 for (int q = 0; q < kRowU; ++q) acc[q] = nxt[q];
 #pragma unroll
                 for (int q = 0; q < kRowU; ++q) {
                     const int i = i0 + kRowU + q;
-                    nxt[q] = i < rows ? A[(size_t)(k0 + i) * n + j] : 0.0;
+                    nxt[q] = i < r1 ? A[(size_t)(k0 + i) * n + j] : 0.0;
                 }
 #pragma unroll
                 for (int q = 0; q < kRowU; ++q) {
                     const int i = i0 + q;
-                    if (i < rows) {
+                    if (i < r1) {
 #pragma unroll
                         for (int c = 0; c < kNB; ++c) acc[q] -= panel[i * kNB + c] * u[c];
                         A[(size_t)(k0 + i) * n + j] = acc[q];
                     }
                 }
             }
+        };
+        const int ncols = n - k0 - kb;
+        const int H = ncols > 0 ? max(1, min(4, kThreads / ncols)) : 1;
+        int jd = -1;
+        if (H == 1) {
+            for (int j = k0 + kb + tid; j < n; j += kThreads) {
+                double u[kNB];
+                subst(j, u);
+                put_u(j, u);
+                trail(j, kb, rows, u);
+            }
+        } else if (tid < ncols * H) {                         // one (column, row chunk) per thread
+            const int h = tid / ncols, j = k0 + kb + (tid - h * ncols);
+            double u[kNB];
+            subst(j, u);
+            if (h == 0) jd = j;
+            const int len = (rows - kb + H - 1) / H;
+            const int r0 = kb + h * len;
+            trail(j, r0, min(rows, r0 + len), u);
         }
         __syncthreads();
+        if (jd >= 0) {                                       // every chunk has read U12 by now: the
+            double u[kNB];                                   // substitution again (same values), stored
+            subst(jd, u);
+            put_u(jd, u);
+        }
+        if (H > 1) __syncthreads();                          // L11 (panel) read before the next staging
     }
 }
 
@@ -279,10 +350,10 @@ constexpr long kSolveMinChunk = 16;
 // there are no interchanges between block rows, partial pivoting inside each diagonal block.
 //
 // btd_factor_kernel:  D'_k = D_k - L_k W_{k-1},  [W_k | D'_k^-1] = D'_k^-1 [U_k | I]
-//   by Gauss-Jordan on the augmented block [D'_k | U_k | I] in LDS (per column: a pivot search by
-//   wave shuffles in every wave, the row interchange folded into the elimination of every other row,
-//   read from one LDS buffer and written to the other: one barrier per column; the 256 threads are a
-//   4 x 64 grid of (row group, column), so no integer division in the inner loops).  W_k
+//   by Gauss-Jordan on the augmented block [D'_k | U_k | I] held in registers (a wave per 12 rows;
+//   per column each wave publishes its own pivot candidate row and one barrier later every thread
+//   picks the same pivot: one barrier per column; the row interchange is folded into the
+//   elimination of every other row).  W_k
 //   overwrites U_k; D'_k^-1 goes to Dinv[b][k][m][m]; W_{k-1} stays in LDS for the next stage
 //   (two augmented blocks and W_{k-1} take 130 KB at m = 48).
 //   D'_k itself replaces D_k in T.
@@ -298,50 +369,6 @@ constexpr long kSolveMinChunk = 16;
 // <256, 48> is instantiated.
 constexpr int kBtdMaxM = 48;
 constexpr int kBtdMaxRhs = 64;
-
-// Max over the 64 lanes of a wave by DPP moves (quad permutes, row rotations, row broadcasts: VALU
-// latency) instead of a __shfl_xor butterfly (six dependent LDS-permute round trips); the result
-// is read from lane 63 and is uniform.  fmax is order-independent, so the value is the butterfly's.
-template <int Ctrl>
-__device__ __forceinline__ double mov_dpp_f64(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)b, Ctrl, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), Ctrl, 0xf, 0xf, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ double wave_max(double v) {
-    v = fmax(v, mov_dpp_f64<0xb1>(v));                        // quad_perm [1,0,3,2]
-    v = fmax(v, mov_dpp_f64<0x4e>(v));                        // quad_perm [2,3,0,1]
-    v = fmax(v, mov_dpp_f64<0x124>(v));                       // row_ror 4
-    v = fmax(v, mov_dpp_f64<0x128>(v));                       // row_ror 8
-    v = fmax(v, mov_dpp_f64<0x142>(v));                       // row_bcast 15
-    v = fmax(v, mov_dpp_f64<0x143>(v));                       // row_bcast 31
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, 63);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// Gauss-Jordan tile helpers of btd_factor_kernel (compile-time register indices)
-template <int Q, int TR, int TC>
-__device__ __forceinline__ void gj_publish_col(const double (&a)[TR][TC], double* colbuf, int rg, int m) {
-#pragma unroll
-    for (int r = 0; r < TR; ++r)
-        if (rg * TR + r < m) colbuf[rg * TR + r] = a[r][Q];
-}
-
-template <int R, int TR, int TC>
-__device__ __forceinline__ void gj_publish_row(const double (&a)[TR][TC], double* rowbuf, int cg) {
-#pragma unroll
-    for (int q = 0; q < TC; ++q) rowbuf[cg * TC + q] = a[R][q];
-}
-
-template <int R, int TR, int TC>
-__device__ __forceinline__ void gj_set_row(double (&a)[TR][TC], const double (&pr)[TC]) {
-#pragma unroll
-    for (int q = 0; q < TC; ++q) a[R][q] = pr[q];
-}
 
 template <int NT, int MAXM>
 __global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* __restrict__ Ts,
@@ -415,115 +442,125 @@ __global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* _
         }
         for (int i = ti; i < m; i += kRG)                     // keep D'_k for the solves' refinement
             for (int j = tj; j < m; j += 64) Dg[i * m + j] = R0[i][j];
-        // Gauss-Jordan with partial pivoting, the augmented block held in registers: thread t owns
-        // the 8 x 4 tile (rows 8 (t / 36) .., columns 4 (t % 36) ..) of [D' | U | I]; per column the
-        // owners publish column c and then the pivot row through LDS (two barriers), every thread
-        // updates its 32 entries.  Rows are not interchanged: row piv[c] ends as row c of
-        // [I | W | D'^-1] and is written there.
-        constexpr int kTR = 8, kTC = 4, kNCG = (3 * MAXM) / kTC;   // 36 column groups
-        const int rg = tid / kNCG, cg = tid - rg * kNCG;
-        const bool owner = rg < MAXM / kTR;
-        double a[kTR][kTC];
-        if (owner) {
+        // Gauss-Jordan with partial pivoting, the augmented block held in registers: wave w owns
+        // rows kWR w .. kWR w + kWR - 1, lane (rq, cq) = (lane / 16, lane % 16) the kLR x kLC tile
+        // (rows kWR w + kLR rq .., columns kLC cq ..) of [D' | U | I].  Per column c every wave
+        // finds its own pivot candidate -- the largest |entry| among its unused rows, its lowest
+        // such row on ties -- and publishes key (that magnitude; -1: no finite candidate, its
+        // lowest unused row instead; -2: no unused row), row and the whole candidate row; after ONE
+        // barrier every thread takes the same pivot from the four candidates (largest key, lowest
+        // wave on ties: the lowest row holding the column maximum, as the block-wide search of the
+        // previous two-barrier form) and reads its kLC pivot-row entries, and its rows' multipliers
+        // come from the lane of its row group holding column c (a shuffle before the barrier).
+        // The arithmetic per entry is the previous form's: pr = a[p][.] (1 / a[p][c]),
+        // a[r][.] -= a[r][c] pr, row p := pr -- factors bitwise equal.  Candidate buffers alternate
+        // between columns (c & 1): a wave writes column c + 2's only after every wave has passed
+        // column c + 1's barrier, i.e. finished reading column c's.  Rows are not interchanged:
+        // row piv[c] ends as row c of [I | W | D'^-1] and is written there.
+        static_assert(NT == 256 && MAXM == 48, "tile layout of the Gauss-Jordan loop");
+        constexpr int kWR = MAXM / kRG, kLR = kWR / 4, kLC = 3 * MAXM / 16;     // 12 rows, 3 x 9 tiles
+        const int rq = tj >> 4, cq = tj & 15;
+        const int row0 = ti * kWR + rq * kLR;
+        double a[kLR][kLC];
 #pragma unroll
-            for (int r = 0; r < kTR; ++r)
+        for (int i = 0; i < kLR; ++i)
 #pragma unroll
-                for (int q = 0; q < kTC; ++q) {
-                    const int i = rg * kTR + r, j = cg * kTC + q;
-                    a[r][q] = (i < m && j < na) ? R0[i][j] : 0.0;
-                }
-        }
-        // column and pivot-row buffers alternate between columns (c & 1), so a column needs two
-        // barriers, not three: a wave can only write column c + 2's buffers after every wave has
-        // passed column c + 1's barriers, i.e. finished reading column c's.  Every wave finds the
-        // same pivot, so the set of used pivot rows is a per-wave register mask.
-        int* pivrow = reinterpret_cast<int*>(&R1[4][0]);      // pivot row of column c
-        unsigned long long usedmask = 0ull;                   // rows already pivots (m <= 48)
+            for (int q = 0; q < kLC; ++q) {
+                const int r = row0 + i, j = cq * kLC + q;
+                a[i][q] = (r < m && j < na) ? R0[r][j] : 0.0;
+            }
+        double* cbuf = &R1[0][0];                             // [2][kRG][3 MAXM] candidate rows
+        double* ckey = cbuf + 2 * kRG * 3 * MAXM;             // [2][kRG]
+        int* crow = reinterpret_cast<int*>(ckey + 2 * kRG);   // [2][kRG]
+        int* pivrow = crow + 2 * kRG;                         // pivot row of column c
+        const int wr0 = ti * kWR, wr1 = min(m, wr0 + kWR);
+        const unsigned long long wmask = wr1 > wr0 ? (((1ull << (wr1 - wr0)) - 1ull) << wr0) : 0ull;
+        unsigned long long usedmask = 0ull;                   // rows already pivots (m <= 48, uniform)
         __syncthreads();
-        for (int c = 0; c < m; ++c) {
-            double* colbuf = &R1[(c & 1) ? 2 : 0][0];         // column c of the current matrix
-            double* rowbuf = &R1[(c & 1) ? 3 : 1][0];         // the pivot row (3 m entries)
-            if (owner && cg == c / kTC) {                     // c % kTC is uniform: a branch, not
-                switch (c % kTC) {                            // a select per register
-                    case 0: gj_publish_col<0>(a, colbuf, rg, m); break;
-                    case 1: gj_publish_col<1>(a, colbuf, rg, m); break;
-                    case 2: gj_publish_col<2>(a, colbuf, rg, m); break;
-                    default: gj_publish_col<3>(a, colbuf, rg, m); break;
-                }
-            }
-            __syncthreads();
-            // every wave finds the same pivot: the largest |entry| among unused rows by a DPP max
-            // reduction, then the smallest such row by one ballot (ties as before: lowest row)
-            const bool cand = tj < m && !((usedmask >> tj) & 1ull);
-            const double best = cand ? fabs(colbuf[tj]) : -1.0;
-            const double mx = wave_max(best);
-            unsigned long long hit = __ballot(cand && best == mx);
-            if (hit == 0ull) hit = ~usedmask & ((1ull << m) - 1ull);    // all-NaN column: any unused row
-            const int p = __ffsll((long long)hit) - 1;
-            usedmask |= 1ull << p;
-            if (owner && rg == p / kTR) {
-                switch (p % kTR) {
-                    case 0: gj_publish_row<0>(a, rowbuf, cg); break;
-                    case 1: gj_publish_row<1>(a, rowbuf, cg); break;
-                    case 2: gj_publish_row<2>(a, rowbuf, cg); break;
-                    case 3: gj_publish_row<3>(a, rowbuf, cg); break;
-                    case 4: gj_publish_row<4>(a, rowbuf, cg); break;
-                    case 5: gj_publish_row<5>(a, rowbuf, cg); break;
-                    case 6: gj_publish_row<6>(a, rowbuf, cg); break;
-                    default: gj_publish_row<7>(a, rowbuf, cg); break;
-                }
-            }
-            // off the critical path (before the barrier): the reciprocal pivot and this thread's
-            // column entries -- colbuf stays valid until column c + 2
-            const double rp = 1.0 / colbuf[p];
-            double f[kTR];
-            if (owner) {
+        for (int cg = 0; cg * kLC < m; ++cg) {
 #pragma unroll
-                for (int r = 0; r < kTR; ++r) f[r] = colbuf[rg * kTR + r];
-            }
-            __syncthreads();
-            if (owner) {
-                double pr[kTC];
+            for (int qc = 0; qc < kLC; ++qc) {
+                const int c = cg * kLC + qc;
+                if (c < m) {
+                    const int bsel = (c & 1) * kRG;
+                    // this lane's candidate: its rows' column-c entries (lanes of column group cg)
+                    double best = -1.0;
+                    int bi = -1;
+                    if (cq == cg) {
 #pragma unroll
-                for (int q = 0; q < kTC; ++q) pr[q] = rowbuf[cg * kTC + q] * rp;
-                // every row eliminated (padding rows i >= m, < MAXM, with stale column entries: never
-                // published or written back), then the pivot row set to the scaled pivot row: no
-                // divergent select per entry
-#pragma unroll
-                for (int r = 0; r < kTR; ++r)
-#pragma unroll
-                    for (int q = 0; q < kTC; ++q) a[r][q] = a[r][q] - f[r] * pr[q];
-                if (rg == p / kTR) {
-                    switch (p % kTR) {
-                        case 0: gj_set_row<0>(a, pr); break;
-                        case 1: gj_set_row<1>(a, pr); break;
-                        case 2: gj_set_row<2>(a, pr); break;
-                        case 3: gj_set_row<3>(a, pr); break;
-                        case 4: gj_set_row<4>(a, pr); break;
-                        case 5: gj_set_row<5>(a, pr); break;
-                        case 6: gj_set_row<6>(a, pr); break;
-                        default: gj_set_row<7>(a, pr); break;
+                        for (int i = 0; i < kLR; ++i) {
+                            const int r = row0 + i;
+                            const double v = fabs(a[i][qc]);
+                            if (r < m && !((usedmask >> r) & 1ull) && v > best) { best = v; bi = r; }
+                        }
                     }
+                    const double mx = wave_max(best);
+                    const unsigned long long hit = __ballot(bi >= 0 && best == mx);
+                    int kr;
+                    double key;
+                    if (hit) {
+                        kr = __builtin_amdgcn_readlane(bi, __ffsll((long long)hit) - 1);
+                        key = mx;
+                    } else {
+                        const unsigned long long fr = wmask & ~usedmask;
+                        kr = fr ? __ffsll((long long)fr) - 1 : -1;
+                        key = fr ? -1.0 : -2.0;
+                    }
+                    // multipliers of this lane's rows: column c from lane (rq, cg)
+                    double f[kLR];
+#pragma unroll
+                    for (int i = 0; i < kLR; ++i) f[i] = __shfl(a[i][qc], (tj & ~15) | cg);
+#pragma unroll
+                    for (int i = 0; i < kLR; ++i)
+                        if (row0 + i == kr) {
+#pragma unroll
+                            for (int q = 0; q < kLC; ++q) cbuf[(bsel + ti) * 3 * MAXM + cq * kLC + q] = a[i][q];
+                        }
+                    if (tj == 0) {
+                        ckey[bsel + ti] = key;
+                        crow[bsel + ti] = kr;
+                    }
+                    __syncthreads();
+                    double kb = ckey[bsel];
+                    int wb = 0;
+#pragma unroll
+                    for (int w = 1; w < kRG; ++w) {
+                        const double kw = ckey[bsel + w];
+                        if (kw > kb) { kb = kw; wb = w; }
+                    }
+                    const int p = crow[bsel + wb];
+                    usedmask |= 1ull << p;
+                    const double* prow = cbuf + (bsel + wb) * 3 * MAXM;
+                    const double rp = 1.0 / prow[c];
+                    double pr[kLC];
+#pragma unroll
+                    for (int q = 0; q < kLC; ++q) pr[q] = prow[cq * kLC + q] * rp;
+#pragma unroll
+                    for (int i = 0; i < kLR; ++i)
+#pragma unroll
+                        for (int q = 0; q < kLC; ++q) a[i][q] = a[i][q] - f[i] * pr[q];
+#pragma unroll
+                    for (int i = 0; i < kLR; ++i)
+                        if (row0 + i == p) {
+#pragma unroll
+                            for (int q = 0; q < kLC; ++q) a[i][q] = pr[q];
+                        }
+                    if (tid == 0) pivrow[c] = p;
                 }
             }
-            if (tid == 0) pivrow[c] = p;
         }
         __syncthreads();
         // row pivrow[c] holds row c of the result: scatter back to R0 in order
-        if (owner) {
 #pragma unroll
-            for (int r = 0; r < kTR; ++r)
+        for (int i = 0; i < kLR; ++i)
 #pragma unroll
-                for (int q = 0; q < kTC; ++q) {
-                    const int i = rg * kTR + r, j = cg * kTC + q;
-                    if (i < m && j < na) R0[i][j] = a[r][q];
-                }
-        }
+            for (int q = 0; q < kLC; ++q) {
+                const int r = row0 + i, j = cq * kLC + q;
+                if (r < m && j < na) R0[r][j] = a[i][q];
+            }
         __syncthreads();
         double (*src)[3 * MAXM + 1] = R0;
-        int* rowof = reinterpret_cast<int*>(&R1[5][0]);
-        for (int c = tid; c < m; c += NT) rowof[c] = pivrow[c];
-        __syncthreads();
+        const int* rowof = pivrow;
         for (int i = ti; i < m; i += kRG) {
             const int ri = rowof[i];
             for (int j = tj; j < m; j += 64) {
@@ -578,29 +615,34 @@ __global__ __launch_bounds__(NT) void btd_apply_kernel(int nb, int m, int ldx, i
     // one memory latency per stage instead of one per row and block (the chain is latency-bound)
     constexpr int R = MAXM / kRG;
 
+    // stage k + 1's loads are issued right after stage k's LDS stores and its barrier, so they are
+    // in flight during stage k's four dependent products instead of starting the next stage
+    double vz[R], vl[R], vi[R], vp[R];
+    auto load_fwd = [&](int k) {
+        const double* Xk = X + (size_t)k * m * ldx;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = ti + r * kRG;
+            const bool in = i < m && tj < m;
+            vz[r] = (i < m && tj < w) ? Xk[(size_t)i * ldx + tj] : 0.0;
+            vl[r] = (in && k > 0) ? T[((size_t)k * 3 + 0) * mm + i * m + tj] : 0.0;
+            vi[r] = in ? Dinv[(size_t)k * mm + i * m + tj] : 0.0;
+            vp[r] = in ? T[((size_t)k * 3 + 1) * mm + i * m + tj] : 0.0;
+        }
+    };
+    load_fwd(0);
     for (int k = 0; k < nb; ++k) {                            // forward: Y_k
         double* Xk = X + (size_t)k * m * ldx;
-        {
-            double vz[R], vl[R], vi[R], vp[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int i = ti + r * kRG;
-                const bool in = i < m && tj < m;
-                vz[r] = (i < m && tj < w) ? Xk[(size_t)i * ldx + tj] : 0.0;
-                vl[r] = (in && k > 0) ? T[((size_t)k * 3 + 0) * mm + i * m + tj] : 0.0;
-                vi[r] = in ? Dinv[(size_t)k * mm + i * m + tj] : 0.0;
-                vp[r] = in ? T[((size_t)k * 3 + 1) * mm + i * m + tj] : 0.0;
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int i = ti + r * kRG;
-                if (i < m) {
-                    if (tj < w) Z[i][tj] = vz[r];
-                    if (tj < m) { A[i][tj] = vl[r]; Ai[i][tj] = vi[r]; Dp[i][tj] = vp[r]; }
-                }
+        for (int r = 0; r < R; ++r) {
+            const int i = ti + r * kRG;
+            if (i < m) {
+                if (tj < w) Z[i][tj] = vz[r];
+                if (tj < m) { A[i][tj] = vl[r]; Ai[i][tj] = vi[r]; Dp[i][tj] = vp[r]; }
             }
         }
         __syncthreads();
+        if (k + 1 < nb) load_fwd(k + 1);
         if (k > 0) {                                          // Z -= L_k Y_{k-1}
             btd_matmul<-1, NT, MAXM>(A, Y, Z, Z, m, w, ti, tj, false);
             __syncthreads();
@@ -614,26 +656,29 @@ __global__ __launch_bounds__(NT) void btd_apply_kernel(int nb, int m, int ldx, i
         for (int i = ti; i < m; i += kRG)
             for (int j = tj; j < w; j += 64) Xk[(size_t)i * ldx + j] = Y[i][j];
     }
+    double vu[R];
+    auto load_bwd = [&](int k) {
+        const double* Xk = X + (size_t)k * m * ldx;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = ti + r * kRG;
+            vu[r] = (i < m && tj < m) ? T[((size_t)k * 3 + 2) * mm + i * m + tj] : 0.0;
+            vz[r] = (i < m && tj < w) ? Xk[(size_t)i * ldx + tj] : 0.0;
+        }
+    };
+    if (nb >= 2) load_bwd(nb - 2);
     for (int k = nb - 2; k >= 0; --k) {                       // backward: x_k = Y_k - W_k x_{k+1}
         double* Xk = X + (size_t)k * m * ldx;
-        {
-            double vu[R], vz[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int i = ti + r * kRG;
-                vu[r] = (i < m && tj < m) ? T[((size_t)k * 3 + 2) * mm + i * m + tj] : 0.0;
-                vz[r] = (i < m && tj < w) ? Xk[(size_t)i * ldx + tj] : 0.0;
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int i = ti + r * kRG;
-                if (i < m) {
-                    if (tj < m) A[i][tj] = vu[r];
-                    if (tj < w) Z[i][tj] = vz[r];
-                }
+        for (int r = 0; r < R; ++r) {
+            const int i = ti + r * kRG;
+            if (i < m) {
+                if (tj < m) A[i][tj] = vu[r];
+                if (tj < w) Z[i][tj] = vz[r];
             }
         }
         __syncthreads();
+        if (k > 0) load_bwd(k - 1);
         btd_matmul<-1, NT, MAXM>(A, Y, Z, Z, m, w, ti, tj, false);
         __syncthreads();
         for (int i = ti; i < m; i += kRG) {

@@ -95,11 +95,12 @@ def lu_ab(libs, b, n, nrhs, dev, gen, reps):
     return rec
 
 
-def btd_ab(libs, b, nb, m, nrhs, dev, gen, reps):
+def btd_ab(libs, b, nb, m, nrhs, dev, gen, reps, boost=4.0):
+    """boost: multiple of m added to the diagonal blocks' diagonal (0: random pivot rows)."""
     T = torch.randn(b, nb, 3, m, m, dtype=torch.float64, device=dev, generator=gen)
-    T[:, :, 1] += 4 * m * torch.eye(m, dtype=torch.float64, device=dev)
+    T[:, :, 1] += boost * m * torch.eye(m, dtype=torch.float64, device=dev)
     X0 = torch.randn(b, nb, m, nrhs, dtype=torch.float64, device=dev, generator=gen)
-    rec = {"op": "btd", "batch": b, "nb": nb, "m": m, "nrhs": nrhs}
+    rec = {"op": "btd", "batch": b, "nb": nb, "m": m, "nrhs": nrhs, "boost": boost}
     res = {}
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for name, lib in libs.items():
@@ -136,9 +137,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--base", default=os.path.join(ROOT, "tools", "ab", "libawelu_r03base.so"))
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--btd-only", action="store_true")
+    ap.add_argument("--lu-only", action="store_true")
+    ap.add_argument("--new", default=None, help="library under test (default: the product libawelu.so)")
     args = ap.parse_args()
     from awebox_amd.batched_lu import load_library
-    libs = {"new": load_library()}
+    libs = {"new": load_library(args.new) if args.new else load_library()}
     if os.path.exists(args.base):
         b = ctypes.CDLL(args.base)
         b.awelu_factor_batched.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -152,10 +156,18 @@ def main():
     dev = "cuda"
     gen = torch.Generator(device=dev)
     gen.manual_seed(0)
-    for b, nb, m, nrhs in [(8, 41, 46, 1), (1, 41, 46, 1), (8, 41, 46, 7), (64, 21, 22, 1)]:
+    for b, nb, m, nrhs in ([] if args.lu_only else [(8, 41, 46, 1), (1, 41, 46, 1), (8, 41, 46, 7), (64, 21, 22, 1)]):
         print(json.dumps(btd_ab(libs, b, nb, m, nrhs, dev, gen, args.reps)), flush=True)
-    for b, n, nrhs in [(40, 268, 120), (20, 640, 160), (140, 640, 160), (160, 100, 100), (1280, 126, 44)]:
+    for b, nb, m, nrhs, boost in [(8, 41, 46, 1, 0.0), (64, 21, 22, 1, 0.0), (4, 9, 48, 3, 0.0), (4, 9, 17, 3, 0.0),
+                                  (7, 41, 46, 1, 0.05)] if not args.lu_only else []:
+        print(json.dumps(btd_ab(libs, b, nb, m, nrhs, dev, gen, args.reps, boost)), flush=True)
+    if args.btd_only:
+        return
+    for b, n, nrhs in [(40, 268, 120), (280, 268, 70), (20, 640, 160), (140, 640, 160), (160, 100, 100), (1, 100, 100),
+                       (7, 100, 100), (1280, 126, 44), (1, 46, 46)]:
         print(json.dumps(lu_ab(libs, b, n, nrhs, dev, gen, args.reps)), flush=True)
+    if args.lu_only:
+        return
     for b, n in [(20, 640), (140, 640), (40, 268), (320, 268), (40, 160), (40, 200), (1280, 126), (41, 46), (328, 46), (1344, 22), (1, 1887)]:
         A = kkt_batch(b, n, dev, gen)
         rec = {"op": "inertia", "batch": b, "n": n}

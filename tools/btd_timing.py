@@ -18,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "awebox_amd", "csrc", "batched_lu.hip")
 OUT_SRC = os.path.join(ROOT, "tools", "exp_src", "btd_timing.hip")
-OUT_LIB = os.path.join(ROOT, "tools", "ab", "libawelu_btdtiming.so")
+OUT_LIB = os.path.join(ROOT, "abv", "libawelu_btdtiming.so")
 
 
 def _after(s, anchor, text, start=0):
@@ -44,12 +44,14 @@ def instrument(s):
                    "        " + T.format(clk="wall_clock64", acc="t_load", prev="t_prev"), i)
     s, i = _before(s, "        // Gauss-Jordan with partial pivoting",
                    "        " + T.format(clk="wall_clock64", acc="t_prod", prev="t_prev"), i)
-    s, i = _after(s, "        for (int c = 0; c < m; ++c) {\n", "            if (c == 0) c_prev = clock64();\n", i)
-    s, i = _after(s, "            __syncthreads();\n", "            " + T.format(clk="clock64", acc="c_col", prev="c_prev"), i)
-    s, i = _after(s, "            usedmask |= 1ull << p;\n", "            " + T.format(clk="clock64", acc="c_piv", prev="c_prev"), i)
-    s, i = _after(s, "            __syncthreads();\n", "            " + T.format(clk="clock64", acc="c_row", prev="c_prev"), i)
-    s, i = _before(s, "            if (tid == 0) pivrow[c] = p;",
-                   T.format(clk="clock64", acc="c_upd", prev="c_prev") + "            ", i)
+    s, i = _after(s, "                if (c < m) {\n", "                    if (c == 0) c_prev = clock64();\n", i)
+    s, i = _before(s, "                    __syncthreads();\n                    double kb",
+                   "                    " + T.format(clk="clock64", acc="c_col", prev="c_prev"), i)
+    s, i = _after(s, "                    __syncthreads();\n", "                    " + T.format(clk="clock64", acc="c_piv", prev="c_prev"), i)
+    s, i = _after(s, "                    const int p = crow[bsel + wb];\n",
+                  "                    " + T.format(clk="clock64", acc="c_row", prev="c_prev"), i)
+    s, i = _before(s, "                    if (tid == 0) pivrow[c] = p;",
+                   T.format(clk="clock64", acc="c_upd", prev="c_prev") + "                    ", i)
     s, i = _before(s, "        // row pivrow[c] holds row c of the result",
                    "        " + T.format(clk="wall_clock64", acc="t_gj", prev="t_prev"), i)
     end = "        __syncthreads();\n    }\n}\n"
@@ -98,7 +100,7 @@ def run():
         us = [v / 100.0 / nb for v in out[:4]]
         mhz = out[8] / out[9] * 100.0 if out[9] else 0.0
         cyc = {k: round(v / (nb * m), 1) for k, v in
-               zip(["publish_col+barrier", "pivot_search", "publish_row+barrier", "update"], out[4:8])}
+               zip(["candidate+publish", "barrier", "pivot_choice", "update"], out[4:8])}
         print(json.dumps({"batch": b, "nb": nb, "m": m,
                           "us_per_stage": dict(zip(["load", "product", "gauss_jordan", "write"], [round(u, 2) for u in us])),
                           "us_per_gj_column": round(us[2] / m, 3), "shader_clock_mhz": round(mhz, 1),

@@ -46,7 +46,7 @@ for s in $STAGES; do
       trace pmc_hess_trace 150 python -u tools/pmc_kernels.py --hess ;;
     sweep)
       trace sweep_ap2_prof 300 python -u bench.py --steps 1 --warmup 1 --batch 8 --no-cpu-baseline --no-hessian --no-latency --mpc-batch 0 --dual-batch 0 --dual-sweep-points 0 --sweep-points 8
-      trace sweep_dual_prof 400 python -u bench.py --steps 1 --warmup 1 --batch 8 --no-cpu-baseline --no-hessian --no-latency --mpc-batch 0 --dual-batch 0 --sweep-points 0 --dual-sweep-points 8 ;;
+      trace sweep_dual_prof 400 python -u bench.py --steps 1 --warmup 1 --batch 8 --no-cpu-baseline --no-hessian --no-latency --mpc-batch 0 --dual-batch 0 --sweep-points 0 --dual-sweep-points 8 --no-dual-chain ;;
   esac
 done
 echo RECORDS_DONE

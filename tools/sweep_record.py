@@ -4,7 +4,7 @@ kernels with their share} for bench.py to attach to BENCH.sweep / BENCH.dual_swe
 solver and evaluator sources are unchanged (hash).
 
     python tools/sweep_record.py --stats gpurun_out/sprof/.../kernel_stats.csv \
-        --bench gpurun_out/sweep_bench.log --arch ap2 --out profiles/r03/sweep_profile_ap2.json
+        --bench gpurun_out/sweep_ap2_prof.log --arch ap2 --out profiles/r05/sweep/sweep_profile_ap2.json
 """
 import argparse
 import csv
