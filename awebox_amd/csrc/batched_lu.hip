@@ -237,14 +237,23 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
                 put_u(j, u);
                 trail(j, kb, rows, u);
             }
-        } else if (tid < ncols * H) {                         // one (column, row chunk) per thread
-            const int h = tid / ncols, j = k0 + kb + (tid - h * ncols);
-            double u[kNB];
-            subst(j, u);
-            if (h == 0) jd = j;
-            const int len = (rows - kb + H - 1) / H;
-            const int r0 = kb + h * len;
-            trail(j, r0, min(rows, r0 + len), u);
+        } else {
+            // H > 1: ncols H <= kThreads, one (column, row chunk) item per thread.  (This loop form
+            // measured 7.8 ms for 20 x 640 against 10.3 ms for the same work as an if on tid;
+            // profiles/r05/solver/lu_variants.)
+            for (int it = tid; it < ncols * H; it += kThreads) {
+                const int h = it / ncols, j = k0 + kb + (it - h * ncols);
+                double u[kNB];
+                subst(j, u);
+                if (H == 1) {
+                    put_u(j, u);
+                } else if (h == 0) {
+                    jd = j;
+                }
+                const int len = (rows - kb + H - 1) / H;
+                const int r0 = kb + h * len;
+                trail(j, r0, min(rows, r0 + len), u);
+            }
         }
         __syncthreads();
         if (jd >= 0) {                                       // every chunk has read U12 by now: the
@@ -259,8 +268,9 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
 // Solve A X = B with the factors of lu_batched_kernel, for the columns [j0, j0 + w) of the
 // row-major right-hand sides X[b][n][ldx] (in place).  One workgroup per matrix; the w columns of
 // X live in LDS for the whole solve, and the factors stream through LDS in 16-column panels:
-//   forward (unit L):  panel L[k0:n, k0:k0+16]; the 16 x 16 diagonal block by substitution, then
-//                      every later row updated by a 16-term dot product (threads over rows x cols);
+//   forward (unit L):  panel L[k0:n, k0:k0+16]; the 16 x 16 diagonal block by substitution (one
+//                      thread per right-hand side, in registers), then every later row updated by a
+//                      16-term dot product (threads over rows x cols);
 //   backward (U):      panel U[0:k1+16, k1:k1+16], bottom block first, same two phases.
 // The library path (rocBLAS trsv for one right-hand side) re-reads the factors per column step
 // from HBM: 20 ms for 256 systems of n = 463 against ~0.1 ms here.
@@ -298,13 +308,27 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
         copy_batched<8>(rows * kb, tid, kThreads, [&](int t) { return A[(size_t)(k0 + t / kb) * n + k0 + t % kb]; },
                         [&](int t, double v) { panel[(t / kb) * kNB + t % kb] = v; });
         __syncthreads();
-        for (int c = 0; c + 1 < kb; ++c) {
-            for (int t = tid; t < (kb - 1 - c) * w; t += kThreads) {
-                const int r = c + 1 + t / w, j = t % w;
-                X[(k0 + r) * w + j] -= panel[r * kNB + c] * X[(k0 + c) * w + j];
+        // the kb x kb unit-lower diagonal block: one thread per right-hand side, the substitution
+        // in registers (per entry the subtractions of the column-by-column form in the same order:
+        // bitwise the same, without its kb - 1 barriers)
+        for (int j = tid; j < w; j += kThreads) {
+            double x[kNB];
+#pragma unroll
+            for (int r = 0; r < kNB; ++r) x[r] = r < kb ? X[(k0 + r) * w + j] : 0.0;
+#pragma unroll
+            for (int r = 1; r < kNB; ++r) {
+                if (r < kb) {
+                    double v = x[r];
+#pragma unroll
+                    for (int c = 0; c < r; ++c) v -= panel[r * kNB + c] * x[c];
+                    x[r] = v;
+                }
             }
-            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kNB; ++r)
+                if (r < kb) X[(k0 + r) * w + j] = x[r];
         }
+        __syncthreads();
         for (int t = tid; t < (rows - kb) * w; t += kThreads) {
             const int r = kb + t / w, j = t % w;
             double acc = X[(k0 + r) * w + j];
@@ -319,15 +343,24 @@ __global__ __launch_bounds__(kThreads) void lu_solve_kernel(int n, int ldx, int 
         copy_batched<8>(rows * kb, tid, kThreads, [&](int t) { return A[(size_t)(t / kb) * n + k1 + t % kb]; },
                         [&](int t, double v) { panel[(t / kb) * kNB + t % kb] = v; });
         __syncthreads();
-        for (int c = kb - 1; c >= 0; --c) {
-            for (int j = tid; j < w; j += kThreads) X[(k1 + c) * w + j] /= panel[(k1 + c) * kNB + c];
-            __syncthreads();
-            for (int t = tid; t < c * w; t += kThreads) {
-                const int r = t / w, j = t % w;
-                X[(k1 + r) * w + j] -= panel[(k1 + r) * kNB + c] * X[(k1 + c) * w + j];
+        // the upper diagonal block, one thread per right-hand side (same order per entry)
+        for (int j = tid; j < w; j += kThreads) {
+            double x[kNB];
+#pragma unroll
+            for (int r = 0; r < kNB; ++r) x[r] = r < kb ? X[(k1 + r) * w + j] : 0.0;
+#pragma unroll
+            for (int c = kNB - 1; c >= 0; --c) {
+                if (c < kb) {
+                    x[c] /= panel[(k1 + c) * kNB + c];
+#pragma unroll
+                    for (int r = 0; r < c; ++r) x[r] -= panel[(k1 + r) * kNB + c] * x[c];
+                }
             }
-            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kNB; ++r)
+                if (r < kb) X[(k1 + r) * w + j] = x[r];
         }
+        __syncthreads();
         for (int t = tid; t < k1 * w; t += kThreads) {
             const int r = t / w, j = t % w;
             double acc = X[r * w + j];
