@@ -613,16 +613,48 @@ __global__ __launch_bounds__(NT) void btd_factor_kernel(int nb, int m, double* _
 // sides (six dependent cross-lane steps per row), one thread per (row group, column) otherwise (12
 // rows serially per thread; 4 of 256 threads busy for one column) -- were latency-bound: the
 // 41-stage solve took 3.1 ms, 2.2 ms with this mapping for one column.
+template <int K, int SIGN, int NT, int MAXM>
+__device__ __forceinline__ void btd_chains(double (*M)[MAXM + 1], double (*Yv)[kBtdMaxRhs + 1],
+                                           double (*Zv)[kBtdMaxRhs + 1], double (*Out)[kBtdMaxRhs + 1],
+                                           int m, int w, int total, int p0, bool init_zero) {
+    int ii[K], jj[K];
+    double acc[K];
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        const int p = p0 + u * NT;
+        ii[u] = p / w;
+        jj[u] = p - ii[u] * w;
+        acc[u] = 0.0;
+    }
+#pragma unroll 8
+    for (int c = 0; c < m; ++c) {
+#pragma unroll
+        for (int u = 0; u < K; ++u) acc[u] += M[ii[u]][c] * Yv[c][jj[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < K; ++u) Out[ii[u]][jj[u]] = (init_zero ? 0.0 : Zv[ii[u]][jj[u]]) + SIGN * acc[u];
+}
+
 template <int SIGN, int NT, int MAXM>
 __device__ __forceinline__ void btd_matmul(double (*M)[MAXM + 1], double (*Yv)[kBtdMaxRhs + 1],
                                            double (*Zv)[kBtdMaxRhs + 1], double (*Out)[kBtdMaxRhs + 1],
                                            int m, int w, int ti, int tj, bool init_zero) {
-    for (int p = ti * 64 + tj; p < m * w; p += NT) {
-        const int i = p / w, j = p - i * w;
-        double acc = 0.0;
-#pragma unroll 8
-        for (int c = 0; c < m; ++c) acc += M[i][c] * Yv[c][j];
-        Out[i][j] = (init_zero ? 0.0 : Zv[i][j]) + SIGN * acc;
+    // a thread's outputs p, p + NT, .. (several when w > 1: the factorisation's T^-1 E with the
+    // border columns) four or two at a time, so their in-order sums run as independent chains
+    const int total = m * w;
+    int p0 = ti * 64 + tj;
+    while (p0 < total) {
+        const int left = (total - p0 + NT - 1) / NT;
+        if (left >= 4) {
+            btd_chains<4, SIGN, NT, MAXM>(M, Yv, Zv, Out, m, w, total, p0, init_zero);
+            p0 += 4 * NT;
+        } else if (left >= 2) {
+            btd_chains<2, SIGN, NT, MAXM>(M, Yv, Zv, Out, m, w, total, p0, init_zero);
+            p0 += 2 * NT;
+        } else {
+            btd_chains<1, SIGN, NT, MAXM>(M, Yv, Zv, Out, m, w, total, p0, init_zero);
+            p0 += NT;
+        }
     }
 }
 

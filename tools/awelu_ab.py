@@ -156,7 +156,7 @@ def main():
     dev = "cuda"
     gen = torch.Generator(device=dev)
     gen.manual_seed(0)
-    for b, nb, m, nrhs in ([] if args.lu_only else [(8, 41, 46, 1), (1, 41, 46, 1), (8, 41, 46, 7), (64, 21, 22, 1)]):
+    for b, nb, m, nrhs in ([] if args.lu_only else [(8, 41, 46, 1), (1, 41, 46, 1), (8, 41, 46, 7), (1, 41, 46, 24), (7, 41, 46, 24), (64, 21, 22, 1)]):
         print(json.dumps(btd_ab(libs, b, nb, m, nrhs, dev, gen, args.reps)), flush=True)
     for b, nb, m, nrhs, boost in [(8, 41, 46, 1, 0.0), (64, 21, 22, 1, 0.0), (4, 9, 48, 3, 0.0), (4, 9, 17, 3, 0.0),
                                   (7, 41, 46, 1, 0.05)] if not args.lu_only else []:
