@@ -154,11 +154,18 @@ class BorderedBtd:
         self.Dp = torch.stack(Dp, 1)
         self.LUs, self.Ws = LUs, Ws
 
-    @staticmethod
-    def _lu_solve(LU, X):
+    AWELU_SOLVE = False         # device: the awelu solve kernel instead of rocSOLVER getrs (A/B)
+
+    def _lu_solve(self, LU, X):
         """D'^-1 X from an LU of the pivot block (LAPACK convention: the awelu factors on the
-        device): rocBLAS/LAPACK triangular solves -- for the block recursion's few large blocks
-        the library's batched trsm beats the one-workgroup-per-matrix awelu solve."""
+        device): rocBLAS/LAPACK triangular solves.  For the block recursion's 100 x 100 blocks the
+        library's getrs (a row swap and two trsm launches) stays ahead of the one-launch awelu
+        solve: with AWELU_SOLVE the dual homotopy's first 62 iterations took 4.3 s against 3.8 s,
+        and the changed rounding moved later iterations and brought back dense fallbacks
+        (profiles/r05/solver/dual_solve_ab)."""
+        if X.is_cuda and self.AWELU_SOLVE:
+            from .batched_lu import lu_solve
+            return lu_solve(LU[0], LU[1], X)
         return torch.linalg.lu_solve(LU[0], LU[1], X)
 
     def _t_solve(self, X):

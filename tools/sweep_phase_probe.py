@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--points", type=int, default=8)
     ap.add_argument("--profile", action="store_true", help="synchronised phase timings (slower)")
     ap.add_argument("--refine", type=int, default=None, help="StructuredKKT.REFINE_STEPS override")
+    ap.add_argument("--awelu-solve", action="store_true", help="btd.BorderedBtd.AWELU_SOLVE (block recursion)")
     ap.add_argument("--out", default="gpurun_out/sweep_phases.json")
     args = ap.parse_args()
     import torch
@@ -31,6 +32,9 @@ def main():
 
     if args.refine is not None:
         ipm.StructuredKKT.REFINE_STEPS = args.refine
+    if args.awelu_solve:
+        import awebox_amd.btd as btd
+        btd.BorderedBtd.AWELU_SOLVE = True
     calls = []
     dense = {"n": 0, "s": 0.0}
     orig_sb = ipm.solve_batch
