@@ -25,6 +25,8 @@ namespace {
 
 constexpr int kNB = 16;
 constexpr int kThreads = 256;
+constexpr int kLuSmallN = 128;           // lu_batched_kernel<128> for blocks up to this size ...
+constexpr int kLuSmallMinBatch = 1100;   // ... in batches beyond what 4 workgroups per CU hold
 constexpr int kMaxN = 1024;
 
 thread_local std::string g_err;
@@ -85,23 +87,24 @@ __device__ __forceinline__ int wave_min_i32(int v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-__global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __restrict__ As, int* __restrict__ pivs) {
+template <int NT>
+__global__ __launch_bounds__(NT) void lu_batched_kernel(int n, double* __restrict__ As, int* __restrict__ pivs) {
     extern __shared__ double panel[];                   // [n][kNB], row-major
-    __shared__ double red_v[kThreads / 64];
-    __shared__ int red_i[kThreads / 64];
+    __shared__ double red_v[NT / 64];
+    __shared__ int red_i[NT / 64];
     __shared__ int piv_loc[kNB];
     __shared__ int orgmap[kMaxN];                       // row -> original row under the panel's swaps
     __shared__ int perm_pos[2 * kNB], perm_org[2 * kNB]; // the panel's interchanges as one permutation
     double* A = As + (size_t)blockIdx.x * n * n;
     int* piv = pivs + (size_t)blockIdx.x * n;
     const int tid = threadIdx.x;
-    for (int i = tid; i < n; i += kThreads) orgmap[i] = i;
+    for (int i = tid; i < n; i += NT) orgmap[i] = i;
 
     for (int k0 = 0; k0 < n; k0 += kNB) {
         const int kb = min(kNB, n - k0);
         const int rows = n - k0;
         // ---- stage the panel A[k0:n, k0:k0+kb] ----------------------------------------------
-        copy_batched<8>(rows * kb, tid, kThreads,
+        copy_batched<8>(rows * kb, tid, NT,
                         [&](int t) { return A[(size_t)(k0 + t / kb) * n + k0 + t % kb]; },
                         [&](int t, double v) { panel[(t / kb) * kNB + t % kb] = v; });
         __syncthreads();
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
         for (int c = 0; c < kb; ++c) {
             double best = -1.0;
             int bi = c;
-            for (int r = c + tid; r < rows; r += kThreads) {
+            for (int r = c + tid; r < rows; r += NT) {
                 const double v = fabs(panel[r * kNB + c]);
                 if (v > best) { best = v; bi = r; }
             }
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
             __syncthreads();
             best = red_v[0];
             bi = red_i[0];
-            for (int w = 1; w < kThreads / 64; ++w) {         // the 4 wave results, same order everywhere
+            for (int w = 1; w < NT / 64; ++w) {         // the 4 wave results, same order everywhere
                 if (red_v[w] > best || (red_v[w] == best && red_i[w] < bi)) { best = red_v[w]; bi = red_i[w]; }
             }
             const int p = bi;
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
             __syncthreads();
             const double d = panel[c * kNB + c];
             const double rd = 1.0 / d;
-            for (int r = c + 1 + tid; r < rows; r += kThreads) {
+            for (int r = c + 1 + tid; r < rows; r += NT) {
                 const double l = panel[r * kNB + c] * rd;
                 panel[r * kNB + c] = l;
                 for (int j = c + 1; j < kb; ++j) panel[r * kNB + j] -= l * panel[c * kNB + j];
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
         // ---- write the panel back, record pivots; the kb sequential interchanges as one permutation
         //      of the rows they touch (positions k0 + c and k0 + piv_loc[c]; a position listed twice
         //      moves the same value twice), applied with all loads of a column before its stores --
-        for (int t = tid; t < rows * kb; t += kThreads) {
+        for (int t = tid; t < rows * kb; t += NT) {
             const int r = t / kb, c = t % kb;
             A[(size_t)(k0 + r) * n + k0 + c] = panel[r * kNB + c];
         }
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
         }
         __syncthreads();
         if (tid < 2 * kNB) orgmap[perm_pos[tid]] = perm_pos[tid];   // back to the identity
-        for (int j = tid; j < n; j += kThreads) {            // interchanges outside the panel: each
+        for (int j = tid; j < n; j += NT) {            // interchanges outside the panel: each
             if (j >= k0 && j < k0 + kb) continue;            // thread owns its columns
             double v[2 * kNB];
 #pragma unroll
@@ -228,20 +231,20 @@ __global__ __launch_bounds__(kThreads) void lu_batched_kernel(int n, double* __r
             }
         };
         const int ncols = n - k0 - kb;
-        const int H = ncols > 0 ? max(1, min(4, kThreads / ncols)) : 1;
+        const int H = ncols > 0 ? max(1, min(4, NT / ncols)) : 1;
         int jd = -1;
         if (H == 1) {
-            for (int j = k0 + kb + tid; j < n; j += kThreads) {
+            for (int j = k0 + kb + tid; j < n; j += NT) {
                 double u[kNB];
                 subst(j, u);
                 put_u(j, u);
                 trail(j, kb, rows, u);
             }
         } else {
-            // H > 1: ncols H <= kThreads, one (column, row chunk) item per thread.  (This loop form
+            // H > 1: ncols H <= NT, one (column, row chunk) item per thread.  (This loop form
             // measured 7.8 ms for 20 x 640 against 10.3 ms for the same work as an if on tid;
             // profiles/r05/solver/lu_variants.)
-            for (int it = tid; it < ncols * H; it += kThreads) {
+            for (int it = tid; it < ncols * H; it += NT) {
                 const int h = it / ncols, j = k0 + kb + (it - h * ncols);
                 double u[kNB];
                 subst(j, u);
@@ -778,17 +781,18 @@ __global__ __launch_bounds__(NT) void btd_apply_kernel(int nb, int m, int ldx, i
 // lower triangle is row c of the array: the column gathers, the interchanges of rows below the
 // pivot and the trailing update (a wave per 4 columns, lanes over rows, W from LDS column-major)
 // all touch contiguous memory.  tools/bk_blocked_model.py is a host model of exactly this scheme.
+template <int NT = kThreads>
 __device__ __forceinline__ void block_argmax(double& v, int& i, double* rv, int* ri, int tid) {
-    for (int off = 32; off > 0; off >>= 1) {
-        const double ov = __shfl_xor(v, off);
-        const int oi = __shfl_xor(i, off);
-        if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
-    }
+    // per wave: a DPP max of the values, then a DPP min of the indices of the lanes holding it
+    // (the (value, lowest index) pair of a shuffle butterfly; v is never NaN here)
+    const double mx = wave_max(v);
+    i = wave_min_i32(v == mx ? i : 0x7fffffff);
+    v = mx;
     if ((tid & 63) == 0) { rv[tid >> 6] = v; ri[tid >> 6] = i; }
     __syncthreads();
     v = rv[0];
     i = ri[0];
-    for (int w = 1; w < kThreads / 64; ++w)
+    for (int w = 1; w < NT / 64; ++w)
         if (rv[w] > v || (rv[w] == v && ri[w] < i)) { v = rv[w]; i = ri[w]; }
     __syncthreads();
 }
@@ -798,11 +802,12 @@ __device__ __forceinline__ void block_argmax(double& v, int& i, double* rv, int*
 // updated one row per wave with lanes over the row's columns (row-major, coalesced).  Below ~200
 // rows its per-pivot work is cheaper than the panel bookkeeping of the blocked kernel, and the
 // trailing triangle is L2-resident.
-__global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, double* __restrict__ As, double ztol,
-                                                                         int* __restrict__ counts) {
+template <int NT>
+__global__ __launch_bounds__(NT) void sym_inertia_unblocked_kernel(int n, double* __restrict__ As, double ztol,
+                                                                   int* __restrict__ counts) {
     extern __shared__ double pc[];                      // pivot columns: [2][n]
-    __shared__ double rv[kThreads / 64];
-    __shared__ int ri[kThreads / 64];
+    __shared__ double rv[NT / 64];
+    __shared__ int ri[NT / 64];
     double* A = As + (size_t)blockIdx.x * n * n;
     const int tid = threadIdx.x;
     const int wv = tid >> 6, ln = tid & 63;
@@ -811,11 +816,11 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, 
     // scale for the zero-pivot test
     double amax = 0.0;
     int dummy = 0;
-    for (int t = tid; t < n * n; t += kThreads) {
+    for (int t = tid; t < n * n; t += NT) {
         const int i = t / n, j = t - i * n;
         if (j <= i) amax = fmax(amax, fabs(A[t]));
     }
-    block_argmax(amax, dummy, rv, ri, tid);
+    block_argmax<NT>(amax, dummy, rv, ri, tid);
     const double zlim = ztol * amax;
     int pos = 0, neg = 0, zero = 0;                     // uniform across the workgroup
     int k = 0;
@@ -823,11 +828,11 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, 
         const double absakk = fabs(L(k, k));
         double colmax = 0.0;
         int imax = k;
-        for (int i = k + 1 + tid; i < n; i += kThreads) {
+        for (int i = k + 1 + tid; i < n; i += NT) {
             const double v = fabs(L(i, k));
             if (v > colmax) { colmax = v; imax = i; }
         }
-        block_argmax(colmax, imax, rv, ri, tid);
+        block_argmax<NT>(colmax, imax, rv, ri, tid);
         if (fmax(absakk, colmax) <= zlim) {             // zero column: a zero eigenvalue
             ++zero;
             ++k;
@@ -837,12 +842,12 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, 
         if (absakk < alpha * colmax) {
             double rowmax = 0.0;
             int jm = 0;
-            for (int j = k + tid; j < n; j += kThreads)
+            for (int j = k + tid; j < n; j += NT)
                 if (j != imax) {
                     const double v = fabs(L(imax, j));
                     if (v > rowmax) { rowmax = v; jm = j; }
                 }
-            block_argmax(rowmax, jm, rv, ri, tid);
+            block_argmax<NT>(rowmax, jm, rv, ri, tid);
             if (absakk >= alpha * colmax * (colmax / rowmax)) {
                 kp = k;
             } else if (fabs(L(imax, imax)) >= alpha * rowmax) {
@@ -854,12 +859,12 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, 
         }
         const int kk = k + kstep - 1;
         if (kp != kk) {                                  // symmetric interchange of kk and kp
-            for (int i = kp + 1 + tid; i < n; i += kThreads) {
+            for (int i = kp + 1 + tid; i < n; i += NT) {
                 const double a = A[(size_t)i * n + kk];
                 A[(size_t)i * n + kk] = A[(size_t)i * n + kp];
                 A[(size_t)i * n + kp] = a;
             }
-            for (int j = kk + 1 + tid; j < kp; j += kThreads) {
+            for (int j = kk + 1 + tid; j < kp; j += NT) {
                 const double a = A[(size_t)j * n + kk];
                 A[(size_t)j * n + kk] = A[(size_t)kp * n + j];
                 A[(size_t)kp * n + j] = a;
@@ -878,7 +883,7 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, 
         }
         // stage the pivot column(s) below the pivot block
         const int r0 = k + kstep;
-        for (int i = r0 + tid; i < n; i += kThreads) {
+        for (int i = r0 + tid; i < n; i += NT) {
             pc[i] = A[(size_t)i * n + k];
             if (kstep == 2) pc[n + i] = A[(size_t)i * n + k + 1];
         }
@@ -892,7 +897,7 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, 
         if (kstep == 1) {
             if (d11 > 0.0) ++pos; else if (d11 < 0.0) ++neg; else ++zero;
             const double rd = 1.0 / d11;
-            for (int i = r0 + wv; i < n; i += kThreads / 64) {     // one row per wave, lanes over j <= i
+            for (int i = r0 + wv; i < n; i += NT / 64) {     // one row per wave, lanes over j <= i
                 const double ci = pc[i] * rd;
                 double* row = A + (size_t)i * n;
                 for (int j = r0 + ln; j <= i; j += 64) row[j] -= ci * pc[j];
@@ -903,7 +908,7 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_unblocked_kernel(int n, 
             else if (det > 0.0) { if (d11 + d22 > 0.0) pos += 2; else neg += 2; }
             else { ++zero; if (d11 + d22 > 0.0) ++pos; else if (d11 + d22 < 0.0) ++neg; else ++zero; }
             const double i11 = d22 / det, i22 = d11 / det, i21 = -d21 / det;   // D^-1
-            for (int i = r0 + wv; i < n; i += kThreads / 64) {
+            for (int i = r0 + wv; i < n; i += NT / 64) {
                 const double ai = pc[i], bi = pc[n + i];
                 const double wi1 = i11 * ai + i21 * bi, wi2 = i21 * ai + i22 * bi;
                 double* row = A + (size_t)i * n;
@@ -1168,7 +1173,13 @@ int awelu_factor_batched(int n, int batch, double* A, int* piv, void* stream) {
         return 1;
     }
     const size_t lds = sizeof(double) * (size_t)n * kNB;
-    lu_batched_kernel<<<dim3((unsigned)batch), kThreads, lds, (hipStream_t)stream>>>(n, A, piv);
+    // small blocks in large batches (the MPC's 1,280 interval blocks of 126 rows): two waves per
+    // matrix keep every block resident at once (8 workgroups per CU instead of 4: one round of the
+    // grid instead of two); the factors are the same bits (per entry the same operations)
+    if (n <= kLuSmallN && batch >= kLuSmallMinBatch)
+        lu_batched_kernel<128><<<dim3((unsigned)batch), 128, lds, (hipStream_t)stream>>>(n, A, piv);
+    else
+        lu_batched_kernel<kThreads><<<dim3((unsigned)batch), kThreads, lds, (hipStream_t)stream>>>(n, A, piv);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);
@@ -1265,9 +1276,11 @@ int awelu_sym_inertia_batched(int n, int batch, double* A, double ztol, int* cou
         hipFuncSetAttribute((const void*)sym_inertia_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSyLds);
         attr = true;
     }
+    // (a <128> instantiation, two waves per matrix as in lu_batched_kernel, measured slower on the
+    // MPC's 1,280 x 126: 1.66 vs 1.27 ms; profiles/r05/solver/mpc_check/ab.log)
     if (n < kSyBlockedMinN)
-        sym_inertia_unblocked_kernel<<<dim3((unsigned)batch), kThreads, sizeof(double) * 2 * (size_t)n,
-                                       (hipStream_t)stream>>>(n, A, ztol, counts);
+        sym_inertia_unblocked_kernel<kThreads><<<dim3((unsigned)batch), kThreads, sizeof(double) * 2 * (size_t)n,
+                                                 (hipStream_t)stream>>>(n, A, ztol, counts);
     else
         sym_inertia_kernel<<<dim3((unsigned)batch), kThreads, sizeof(double) * (size_t)nb * n, (hipStream_t)stream>>>(
             n, nb, A, ztol, counts);

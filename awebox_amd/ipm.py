@@ -677,8 +677,12 @@ class StructuredKKT:
         b_norm = rhs.abs().amax(dim=1)
         done = torch.zeros(rhs.shape[0], dtype=torch.bool, device=self.dev)
         if active is not None:
-            done = ~torch.as_tensor(np.asarray(active) if not torch.is_tensor(active) else active,
-                                    dtype=torch.bool, device=self.dev).reshape(-1)
+            # a host mask goes through pinned memory asynchronously: a pageable copy would wait
+            # for the solve just launched before the refinement's first launches are queued
+            a = active if torch.is_tensor(active) else torch.from_numpy(np.ascontiguousarray(active, dtype=bool))
+            if not a.is_cuda and torch.device(self.dev).type == "cuda":
+                a = a.pin_memory().to(self.dev, non_blocking=True)
+            done = ~a.to(device=self.dev, dtype=torch.bool).reshape(-1)
         for it in range(refine + 1):
             r = rhs - self.matvec(x)
             err = r.abs().amax(dim=1)

@@ -164,11 +164,11 @@ def main():
     if args.btd_only:
         return
     for b, n, nrhs in [(40, 268, 120), (280, 268, 70), (20, 640, 160), (140, 640, 160), (160, 100, 100), (1, 100, 100),
-                       (7, 100, 100), (1280, 126, 44), (1, 46, 46)]:
+                       (7, 100, 100), (1280, 126, 44), (5120, 126, 44), (1, 46, 46)]:
         print(json.dumps(lu_ab(libs, b, n, nrhs, dev, gen, args.reps)), flush=True)
     if args.lu_only:
         return
-    for b, n in [(20, 640), (140, 640), (40, 268), (320, 268), (40, 160), (40, 200), (1280, 126), (41, 46), (328, 46), (1344, 22), (1, 1887)]:
+    for b, n in [(20, 640), (140, 640), (40, 268), (320, 268), (40, 160), (40, 200), (1280, 126), (5120, 126), (41, 46), (328, 46), (1344, 22), (1, 1887)]:
         A = kkt_batch(b, n, dev, gen)
         rec = {"op": "inertia", "batch": b, "n": n}
         counts = {}
