@@ -28,6 +28,9 @@ def load_library(path: str = _PATH):
                                                   ctypes.c_void_p, ctypes.c_void_p]
         lib.awelu_gather_sum.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_longlong] + \
             [ctypes.c_void_p] * 2 + [ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p]
+        ll, vp = ctypes.c_longlong, ctypes.c_void_p
+        lib.awelu_row_sum.argtypes = [ll, ll, vp, ll, vp, vp]
+        lib.awelu_bmm.argtypes = [ctypes.c_int] * 4 + [vp, ll, ll, ll] * 3 + [vp]
         lib.awelu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB

@@ -25,6 +25,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import det
+
 
 class BorderedBtd:
     """Separator system with ``stage_of[q]`` (block index, -1 = border) and ``pos_of[q]`` (row
@@ -105,7 +107,7 @@ class BorderedBtd:
         self.Fm = Fm.view(B, nG, n_t)
         if nG:
             self.Z = self._t_solve(E.view(B, n_t, nG))                     # T^-1 E
-            Cp = C.view(B, nG, nG) - self.Fm @ self.Z
+            Cp = C.view(B, nG, nG) - det.bmm(self.Fm, self.Z)
             self.Cp = Cp
             self.Cf = self._lu(Cp)
 
@@ -145,7 +147,7 @@ class BorderedBtd:
         D = T[:, 0, 1]
         for k in range(nb):
             if k > 0:
-                D = T[:, k, 1] - T[:, k, 0] @ Ws[k - 1]
+                D = T[:, k, 1] - det.bmm(T[:, k, 0], Ws[k - 1])
             LU = self._lu(D.contiguous())
             Dp.append(D)
             LUs.append(LU)
@@ -154,15 +156,16 @@ class BorderedBtd:
         self.Dp = torch.stack(Dp, 1)
         self.LUs, self.Ws = LUs, Ws
 
-    AWELU_SOLVE = False         # device: the awelu solve kernel instead of rocSOLVER getrs (A/B)
+    AWELU_SOLVE = True          # device: the awelu solve kernel (False: rocSOLVER getrs, A/B only)
 
     def _lu_solve(self, LU, X):
         """D'^-1 X from an LU of the pivot block (LAPACK convention: the awelu factors on the
-        device): rocBLAS/LAPACK triangular solves.  For the block recursion's 100 x 100 blocks the
-        library's getrs (a row swap and two trsm launches) stays ahead of the one-launch awelu
-        solve: with AWELU_SOLVE the dual homotopy's first 62 iterations took 4.3 s against 3.8 s,
-        and the changed rounding moved later iterations and brought back dense fallbacks
-        (profiles/r05/solver/dual_solve_ab)."""
+        device).  On the device the awelu solve kernel: one workgroup per (block, right-hand-side
+        chunk), the same operations per entry whatever the batch, so the block recursion rounds the
+        same for one instance as inside a batch (rocSOLVER's getrs calls rocBLAS trsm, whose kernel
+        choice follows the batch count).  Round 5 measured the library getrs ahead for the dual
+        kites' 100 x 100 blocks (the dual homotopy's first 62 iterations 3.8 s against 4.3 s,
+        profiles/r05/solver/dual_solve_ab); batch invariance decides.  Host tensors: LAPACK."""
         if X.is_cuda and self.AWELU_SOLVE:
             from .batched_lu import lu_solve
             return lu_solve(LU[0], LU[1], X)
@@ -178,10 +181,10 @@ class BorderedBtd:
         T = self.T_blocks
         Y = []
         for k in range(nb):                                # forward: Y_k = D'_k^-1 (X_k - L_k Y_{k-1})
-            rk = Xb[:, k] if k == 0 else Xb[:, k] - T[:, k, 0] @ Y[k - 1]
+            rk = Xb[:, k] if k == 0 else Xb[:, k] - det.bmm(T[:, k, 0], Y[k - 1])
             Y.append(self._lu_solve(self.LUs[k], rk.contiguous()))
         for k in range(nb - 2, -1, -1):                    # backward: x_k = Y_k - W_k x_{k+1}
-            Y[k] = Y[k] - self.Ws[k] @ Y[k + 1]
+            Y[k] = Y[k] - det.bmm(self.Ws[k], Y[k + 1])
         return torch.stack(Y, 1).reshape(B, nb * m, -1)
 
     @staticmethod
@@ -206,9 +209,9 @@ class BorderedBtd:
         z = self._t_solve(rT.unsqueeze(-1)).squeeze(-1)
         x = torch.empty_like(r2)
         if self.nG:
-            rG = r2[:, self.sep_g] - (self.Fm @ z.unsqueeze(-1)).squeeze(-1)
+            rG = r2[:, self.sep_g] - det.bmv(self.Fm, z)
             xG = self._c_solve(rG.unsqueeze(-1)).squeeze(-1)
-            z = z - (self.Z @ xG.unsqueeze(-1)).squeeze(-1)
+            z = z - det.bmv(self.Z, xG)
             x[:, self.sep_g] = xG
         x[:, self.sep_t] = z[:, self.slot_t]
         return x[0] if r.dim() == 1 else x

@@ -69,17 +69,38 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wn
          "-Wno-unused-result"]
 
 
-def _stale(lib, deps) -> bool:
-    if not os.path.exists(lib):
+def _lib_hash(lib) -> str:
+    """Content hash of everything a library is built from: its sources and headers (names and
+    bytes), the compiler flags and the offload architecture."""
+    import hashlib
+    sources, headers = TARGETS[lib]
+    h = hashlib.sha1(" ".join(FLAGS).encode() + b"\0")
+    for p in sources + headers:
+        with open(p, "rb") as fh:
+            h.update(os.path.basename(p).encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
+def _stamp(lib) -> str:
+    return lib + ".sha1"
+
+
+def _stale(lib) -> bool:
+    """A library is stale unless the content hash recorded beside it at its build (``<lib>.sha1``)
+    matches its inputs now.  File times are not used: they do not survive a checkout or the copy of
+    the tree to the GPU box, and a library copied there with newer times than edited sources would
+    pass a time check while being built from other code."""
+    if not os.path.exists(lib) or not os.path.exists(_stamp(lib)):
         return True
-    t = os.path.getmtime(lib)
-    return any(os.path.getmtime(p) > t for p in deps)
+    with open(_stamp(lib)) as fh:
+        return fh.read().strip() != _lib_hash(lib)
 
 
 def build_one(lib: str, force: bool = False, verbose: bool = False) -> str:
     sources, headers = TARGETS[lib]
-    if not force and not _stale(lib, sources + headers):
+    if not force and not _stale(lib):
         return lib
+    want = _lib_hash(lib)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     if len(sources) == 1:
         cmd = [hipcc, *FLAGS, *sources, "-o", lib + ".tmp"]
@@ -106,6 +127,9 @@ def build_one(lib: str, force: bool = False, verbose: bool = False) -> str:
                 print(" ".join(cmd), file=sys.stderr)
             subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(lib + ".tmp", lib)
+    with open(_stamp(lib) + ".tmp", "w") as fh:
+        fh.write(want + "\n")
+    os.replace(_stamp(lib) + ".tmp", _stamp(lib))
     return lib
 
 

@@ -1161,6 +1161,110 @@ __global__ __launch_bounds__(256) void gather_sum_kernel(int L, const int* __res
     if (l < L && d >= 0) out[r * ldo + d] = out[r * ldo + d] + v;
 }
 
+// ---- Batch-invariant reductions and products (awebox_amd/det.py) --------------------------------
+// The interior-point solver's per-instance algebra on [B, n] tensors must round the same way
+// whatever B is: a problem solved alone and the same problem inside a batch of 128 (or inside a
+// sweep shard of 8, 4, 2 or 1 points) must follow the same iterates.  torch's
+// row reductions pick a strategy by the tensor's shape, and rocBLAS picks a GEMM kernel by the batch
+// count, so their last bits change with B.  These kernels fix one order per output that depends only
+// on the row length (row_sum) or the inner dimension (bmm), never on the number of rows or matrices,
+// and that det.py restates with elementwise torch operations on any device (the CPU harness and the
+// bitwise tests).
+
+// out[r] = sum_j x[r * ldx + j], j < n: thread t (of 256) adds x[t], x[t + 256], ... in sequence from
+// 0.0; the 256 partial sums are then added as the adjacent-pair tree ((p0 + p1) + (p2 + p3)) + ..
+// (xor butterfly inside each wave, the four wave sums through LDS).
+constexpr int kRowSumThreads = 256;
+
+__global__ __launch_bounds__(kRowSumThreads) void row_sum_kernel(long long n, const double* __restrict__ x,
+                                                                 long long ldx, double* __restrict__ out) {
+    __shared__ double part[kRowSumThreads / 64];
+    const long long r = blockIdx.x;
+    const int t = threadIdx.x;
+    const double* xr = x + r * ldx;
+    double acc = 0.0;
+    long long j = t;
+    // four independent loads in flight per step; the additions stay in sequence
+    for (; j + 3 * kRowSumThreads < n; j += 4 * kRowSumThreads) {
+        const double a = xr[j], b = xr[j + kRowSumThreads], c = xr[j + 2 * kRowSumThreads],
+                     d = xr[j + 3 * kRowSumThreads];
+        acc = acc + a;
+        acc = acc + b;
+        acc = acc + c;
+        acc = acc + d;
+    }
+    for (; j < n; j += kRowSumThreads) acc = acc + xr[j];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) acc = acc + __shfl_xor(acc, o);
+    if ((t & 63) == 0) part[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) out[r] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+// C[b] = A[b] B[b] (M x K times K x N), strided operands (a transposed view is a pair of strides):
+// every output entry is acc = 0; acc = acc + a_ik b_kj for k = 0, 1, .., K - 1, product and sum
+// rounded separately (no contraction), so the bits do not depend on the tile shape chosen below or
+// on the batch.  Workgroup: a TM x TN output tile (TY x TX threads, RM x RN entries each) of one
+// matrix; the K dimension streams through LDS in chunks of KC.
+template <int TX, int TY, int RM, int RN, int KC>
+__global__ __launch_bounds__(TX * TY) void bmm_kernel(int M, int N, int K, const double* __restrict__ A, long long sAb,
+                                                      long long sAm, long long sAk, const double* __restrict__ Bm,
+                                                      long long sBb, long long sBk, long long sBn,
+                                                      double* __restrict__ C, long long sCb, long long sCm,
+                                                      long long sCn, int tiles_n) {
+#pragma clang fp contract(off)
+    constexpr int NT = TX * TY, TM = TY * RM, TN = TX * RN;
+    __shared__ double As[KC][TM + 1];
+    __shared__ double Bs[KC][TN + 1];
+    const long long b = blockIdx.x;
+    const int tm = blockIdx.y / tiles_n, tn = blockIdx.y % tiles_n;
+    const int m0 = tm * TM, n0 = tn * TN;
+    const double* Ab = A + b * sAb;
+    const double* Bb = Bm + b * sBb;
+    const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
+    double acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = 0.0;
+    const bool a_mfast = sAm == 1;                       // load A along its contiguous dimension
+    const bool b_nfast = sBn == 1;
+    for (int k0 = 0; k0 < K; k0 += KC) {
+        for (int e = tid; e < TM * KC; e += NT) {
+            const int mm = a_mfast ? e % TM : e / KC, kk = a_mfast ? e / TM : e % KC;
+            const int gm = m0 + mm, gk = k0 + kk;
+            As[kk][mm] = (gm < M && gk < K) ? Ab[gm * sAm + gk * sAk] : 0.0;
+        }
+        for (int e = tid; e < TN * KC; e += NT) {
+            const int nn = b_nfast ? e % TN : e / KC, kk = b_nfast ? e / TN : e % KC;
+            const int gn = n0 + nn, gk = k0 + kk;
+            Bs[kk][nn] = (gn < N && gk < K) ? Bb[gk * sBk + gn * sBn] : 0.0;
+        }
+        __syncthreads();
+        const int kc = min(KC, K - k0);                  // padded k would add 0 * 0 = +0: skipped
+        for (int kk = 0; kk < kc; ++kk) {
+            double a[RM], bv[RN];
+#pragma unroll
+            for (int i = 0; i < RM; ++i) a[i] = As[kk][ty + i * TY];
+#pragma unroll
+            for (int j = 0; j < RN; ++j) bv[j] = Bs[kk][tx + j * TX];
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int j = 0; j < RN; ++j) acc[i][j] = acc[i][j] + a[i] * bv[j];
+        }
+        __syncthreads();
+    }
+    double* Cb = C + b * sCb;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+            const int gm = m0 + ty + i * TY, gn = n0 + tx + j * TX;
+            if (gm < M && gn < N) Cb[gm * sCm + gn * sCn] = acc[i][j];
+        }
+}
+
 extern "C" {
 
 const char* awelu_last_error(void) { return g_err.c_str(); }
@@ -1304,6 +1408,69 @@ int awelu_gather_sum(int L, int rows, const int* lsrc, const unsigned char* lw, 
     if (L == 0 || rows == 0) return 0;
     gather_sum_kernel<<<dim3((unsigned)((L + 255) / 256), (unsigned)rows), 256, 0, (hipStream_t)stream>>>(
         L, lsrc, lw, ldst, vals, ldv, x, cols, ldx, out, ldo);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// out[r] = sum of x[r][0 .. n) in row_sum_kernel's fixed order, r < rows (x row stride ldx >= n).
+int awelu_row_sum(long long rows, long long n, const double* x, long long ldx, double* out, void* stream) {
+    if (rows < 0 || rows > 0x7fffffffLL || n < 0 || ldx < n || (rows > 0 && (!x || !out))) {
+        g_err = "need 0 <= rows < 2^31, n >= 0, ldx >= n and device pointers";
+        return 1;
+    }
+    if (rows == 0) return 0;
+    row_sum_kernel<<<dim3((unsigned)rows), kRowSumThreads, 0, (hipStream_t)stream>>>(n, x, ldx, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// C[b] = A[b] B[b] for b < batch: M x K times K x N with element strides (sAm, sAk), (sBk, sBn),
+// (sCm, sCn) and batch strides sAb, sBb, sCb (a transposed operand is a swapped stride pair).  C must
+// not overlap A or B.  Every entry is summed over k in sequence (bmm_kernel): the result is the same
+// for every batch and every tile shape.
+int awelu_bmm(int batch, int M, int N, int K, const double* A, long long sAb, long long sAm, long long sAk,
+              const double* B, long long sBb, long long sBk, long long sBn, double* C, long long sCb, long long sCm,
+              long long sCn, void* stream) {
+    if (batch < 0 || M < 0 || N < 0 || K < 0 || (batch > 0 && M > 0 && N > 0 && (!A || !B || !C))) {
+        g_err = "need non-negative sizes and device pointers";
+        return 1;
+    }
+    if (batch == 0 || M == 0 || N == 0) return 0;
+    const hipStream_t s = (hipStream_t)stream;
+    // the tile shape follows the output's shape only (never the batch): wide outputs 64 x 64
+    // (4 x 4 per thread), narrow ones 128 x 8 (2 x 2), single columns 256 x 1
+    auto tiles = [](int total, int t) { return (total + t - 1) / t; };
+    long long grid_y;
+    if (N >= 24) {
+        const int tn = tiles(N, 64);
+        grid_y = (long long)tiles(M, 64) * tn;
+        if (grid_y <= 65535)
+            bmm_kernel<16, 16, 4, 4, 16><<<dim3((unsigned)batch, (unsigned)grid_y), 256, 0, s>>>(
+                M, N, K, A, sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, tn);
+    } else if (N > 1) {
+        const int tn = tiles(N, 8);
+        grid_y = (long long)tiles(M, 128) * tn;
+        if (grid_y <= 65535)
+            bmm_kernel<4, 64, 2, 2, 16><<<dim3((unsigned)batch, (unsigned)grid_y), 256, 0, s>>>(
+                M, N, K, A, sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, tn);
+    } else {
+        grid_y = tiles(M, 256);
+        if (grid_y <= 65535)
+            bmm_kernel<1, 256, 1, 1, 32><<<dim3((unsigned)batch, (unsigned)grid_y), 256, 0, s>>>(
+                M, N, K, A, sAb, sAm, sAk, B, sBb, sBk, sBn, C, sCb, sCm, sCn, 1);
+    }
+    if (grid_y > 65535) {
+        g_err = "output too large for one launch";
+        return 1;
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

@@ -292,6 +292,16 @@ class Ap2Evaluator:
     @hess_path.setter
     def hess_path(self, name):
         self._check(self._lib.awe_set_hess_path(self._h, self.HESS_PATHS[name]))
+        self._hess_mode = name
+
+    @property
+    def hess_mode(self):
+        """The Hessian selection as set: 'follow' (the default: the kernel follows the evaluation
+        path, resolved on every call), 'generated' or 'hyperdual'.  ``hess_path`` returns what the
+        next call resolves to.  A solver that reads ``hess_path`` once to pick the H layout
+        (ipm.DeviceNlp.h_im) only picks a layout: the C side dispatches the kernel on every call and
+        both entry points (awe_eval_hess / awe_eval_hess_im) handle either kernel."""
+        return getattr(self, "_hess_mode", "follow")
 
     def eval_hess(self, V, P, sigma, lam_g):
         """Host arrays in, host array out: H [B, nnz_h] (upper triangle, CCS)."""

@@ -38,6 +38,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
+from . import det
 from . import problem as pb
 
 
@@ -285,9 +286,13 @@ class _ScatterSum:
 
     # --- the torch reduction (host tensors, and the buckets wider than 64) ------------------------
     def _torch_buckets(self, out, vals, buckets):
+        """The gather-sums by torch indexing, in the kernels' orders: a list of width <= 64 as the
+        adjacent-pair tree of awelu_gather_sum, a wider one in det.row_sum's order (awelu_row_sum on
+        the device).  Neither depends on the leading (batch) shape."""
         ext = torch.cat([vals, vals.new_zeros(vals.shape[:-1] + (1,))], dim=-1)
         for d, table in buckets:
-            out[..., d] += ext[..., table].sum(dim=-1)
+            g = ext[..., table]
+            out[..., d] += det.tree_sum(g) if table.shape[1] <= self.NATIVE_MAX_W else det.row_sum(g)
         return out
 
     def _native_ok(self, out, vals, x=None):
@@ -585,7 +590,7 @@ class StructuredKKT:
         else:
             self.LU_I, self.piv_I = torch.linalg.lu_factor(KII)
         self.X = self._block_solve(KIS)                                        # K_II^-1 K_IS
-        T = (KIS.transpose(1, 2) @ self.X).reshape(B, n_k * L * L)             # [B, n_k L L]
+        T = det.bmm(KIS.transpose(1, 2), self.X).reshape(B, n_k * L * L)       # [B, n_k L L]
         self.KIS = KIS
         if self.btd is not None and not self.btd_off and (KII.is_cuda or self.force_btd):
             self.btd.factor(torch.cat([vals[:, self.sel_ss], -T], dim=1))
@@ -727,7 +732,7 @@ class StructuredKKT:
         rS = torch.zeros(B, nS + 1, **f64)
         rS[:, :nS] = rhs[:, self.sep_p]
         z = self._block_solve(rI.view(B * n_k, nI, 1))                         # [B n_k, nI, 1]
-        upd = (self.KIS.transpose(1, 2) @ z).reshape(B, n_k * L)
+        upd = det.bmm(self.KIS.transpose(1, 2), z).reshape(B, n_k * L)
         self.sc_rs.add_into(rS, -upd)
         rS[:, nS] = 0.0
         xS = torch.zeros(B, nS + 1, **f64)
@@ -735,7 +740,7 @@ class StructuredKKT:
             xS[:, :nS] = self.btd.solve(rS[:, :nS])
         else:
             xS = torch.linalg.lu_solve(self.LU_S, self.piv_S, rS.unsqueeze(-1)).squeeze(-1)
-        xI = z.view(B * n_k, nI) - (self.X @ xS[:, self.lsep].reshape(B * n_k, L, 1)).view(B * n_k, nI)
+        xI = z.view(B * n_k, nI) - det.bmm(self.X, xS[:, self.lsep].reshape(B * n_k, L, 1)).view(B * n_k, nI)
         sol = torch.empty(B, self.N, **f64)
         sol[:, self.int_p] = xI.view(B, n_k * nI)[:, self.int_flat]
         sol[:, self.sep_p] = xS[:, :nS]
@@ -883,7 +888,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     tau = np.maximum(opts.tau_min, 1.0 - mu)
     filt = [[] for _ in range(B)]
     c = nlp.constraints(g, y[:, n:])
-    theta0 = c.abs().sum(1).cpu().numpy()
+    theta0 = det.row_sum(c.abs()).cpu().numpy()
     theta_max = 1e4 * np.maximum(1.0, theta0)
     theta_min = 1e-4 * np.maximum(1.0, theta0)
     delta_w_last = np.zeros(B)
@@ -940,9 +945,9 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
 
     def barrier_phi(fv, yv, mu_t):
         dl, du = gaps(yv)
-        lg = torch.where(hl, torch.log(dl), torch.zeros_like(dl)).sum(1) + \
-            torch.where(hu, torch.log(du), torch.zeros_like(du)).sum(1)
-        dmp = (lo_only * dl).sum(1) + (hi_only * du).sum(1)
+        lg = det.row_sum(torch.where(hl, torch.log(dl), torch.zeros_like(dl))) + \
+            det.row_sum(torch.where(hu, torch.log(du), torch.zeros_like(du)))
+        dmp = det.row_sum(lo_only * dl) + det.row_sum(hi_only * du)
         return fv - mu_t * lg + opts.kappa_d * mu_t * dmp
 
     def grad_y(gradv):
@@ -971,8 +976,8 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             dual = dual + opts.kappa_d * mu_t[:, None] * damp_dir
         compl_l = torch.where(hl, dl * zlv - mu_t[:, None], torch.zeros_like(yv))
         compl_u = torch.where(hu, du * zuv - mu_t[:, None], torch.zeros_like(yv))
-        zsum = zlv.abs().sum(1) + zuv.abs().sum(1)
-        s_d = torch.clamp((lamv.abs().sum(1) + zsum) / max(1, m + nb), min=opts.s_max) / opts.s_max
+        zsum = det.row_sum(zlv.abs()) + det.row_sum(zuv.abs())
+        s_d = torch.clamp((det.row_sum(lamv.abs()) + zsum) / max(1, m + nb), min=opts.s_max) / opts.s_max
         s_c = torch.clamp(zsum / max(1, nb), min=opts.s_max) / opts.s_max
         e_dual = dual.abs().amax(1) / s_d
         e_pr = cv.abs().amax(1) if m else torch.zeros(B, **f64)
@@ -1057,8 +1062,8 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 if not exact_inertia:
                     dy = sol[:, :ny]
                     Wd = h_op.mv(torch.cat([hv, hv[:, nlp.h_offdiag]], 1), dy)
-                    curv = (dy * (Wd + (sigma + dev_b(delta_w)[:, None]) * dy)).sum(1)
-                    cpass = (curv >= opts.curvature_kappa * (dy * dy).sum(1)).cpu().numpy()
+                    curv = det.row_sum(dy * (Wd + (sigma + dev_b(delta_w)[:, None]) * dy))
+                    cpass = (curv >= opts.curvature_kappa * det.row_sum(dy * dy)).cpu().numpy()
                     bad_fin = good & ~fin
                     delta_c = np.where(bad_fin & (delta_c == 0.0), opts.delta_c * mu_t ** 0.25, delta_c)
                     newly = good & fin & cpass
@@ -1097,7 +1102,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         # are the same exact operation)
         alpha_dev = torch.minimum(torch.minimum(ftb_dev(dl, dy, hl, tau_t), ftb_dev(du, -dy, hu, tau_t)),
                                   torch.ones(B, **f64))
-        gphi_dev = (grad_phi * dy).sum(1)
+        gphi_dev = det.row_sum(grad_phi * dy)
         alpha = gphi_d = alpha_min = None
         live = want.copy()
         acc = np.zeros(B, dtype=bool)
@@ -1139,7 +1144,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             with _Phase("eval_fg"):
                 ft, gt = nlp.eval_fg(yt[:, :n])
             ct = nlp.constraints(gt, yt[:, n:])
-            theta_t = ct.abs().sum(1)
+            theta_t = det.row_sum(ct.abs())
             phi_t = barrier_phi(ft, yt, dev_b(mu_t))
             if alpha is None:
                 tp4 = torch.stack([theta_t, phi_t, alpha_dev, gphi_dev]).cpu().numpy()
@@ -1226,7 +1231,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 break
             _, _, g_c, jv_c = nlp.eval_all(yv[:, :n])
             cv = nlp.constraints(g_c, yv[:, n:])
-            th = cv.abs().sum(1).cpu().numpy()
+            th = det.row_sum(cv.abs()).cpu().numpy()
             dlv, duv = gaps(yv)
             sig = torch.where(hl, 1.0 / dlv ** 2, torch.zeros_like(yv)) + torch.where(hu, 1.0 / duv ** 2, torch.zeros_like(yv))
             skkt.factor(hv_zero, sig + 1e-8, jv_c, 0.0, mI)
@@ -1243,7 +1248,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 yt = yv + dev_b(a)[:, None] * dyv
                 ft, gt = nlp.eval_fg(yt[:, :n])
                 ct = nlp.constraints(gt, yt[:, n:])
-                tht = ct.abs().sum(1).cpu().numpy()
+                tht = det.row_sum(ct.abs()).cpu().numpy()
                 okb = searching & np.isfinite(tht) & (tht < (1 - 1e-4 * a) * th)
                 a_acc = np.where(okb, a, a_acc)
                 searching &= ~okb
@@ -1256,7 +1261,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             lam_r = torch.where(sel, lam_r + dev_b(a_acc)[:, None] * sol[:, ny:], lam_r)
             ft, gt = nlp.eval_fg(yv[:, :n])
             ct = nlp.constraints(gt, yv[:, n:])
-            tp = torch.stack([ct.abs().sum(1), barrier_phi(ft, yv, dev_b(mu_t))]).cpu().numpy()
+            tp = torch.stack([det.row_sum(ct.abs()), barrier_phi(ft, yv, dev_b(mu_t))]).cpu().numpy()
             for b in np.where(live)[0]:
                 if tp[0, b] <= 0.9 * theta0_[b] and filter_ok(b, tp[0, b], tp[1, b]):
                     succ[b], live[b] = True, False
@@ -1276,7 +1281,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         head = torch.stack(errors(grad, jv, c, y, lam, zl, zu, torch.full((B,), opts.mu_target, **f64),
                                   unscaled=True, dev_only=True) +
                            [errors(grad, jv, c, y, lam, zl, zu, mu_head, damped=True, dev_only=True)[0],
-                            c.abs().sum(1), barrier_phi(f, y, mu_head)]).cpu().numpy()
+                            det.row_sum(c.abs()), barrier_phi(f, y, mu_head)]).cpu().numpy()
         kkt_err, e_d, e_p, e_c, u_d, u_p, u_c = head[:7]
         e_mu_head, theta_head, phi_head = head[7], head[8], head[9]
         # IPOPT's OptimalityErrorConvergenceCheck: the scaled error and the unscaled tests
@@ -1314,7 +1319,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         grad_phi = grad_y(grad) - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
             torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y)) + opts.kappa_d * mu_d[:, None] * damp_dir
         if mu_changed:
-            theta, phi = torch.stack([c.abs().sum(1), barrier_phi(f, y, mu_d)]).cpu().numpy()
+            theta, phi = torch.stack([det.row_sum(c.abs()), barrier_phi(f, y, mu_d)]).cpu().numpy()
         else:
             theta, phi = theta_head, phi_head
         rhs_top = -(grad_phi + A_T_lam(jv, lam))

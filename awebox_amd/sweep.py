@@ -101,12 +101,18 @@ class _Dual:
 
 
 def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda", opts: IpmOptions | None = None,
-              verbose=False, point_solver=None, arch="single", mode="chain"):
+              verbose=False, point_solver=None, arch="single", mode="chain", reconcile=True, coll_device=None):
     """Returns (on rank 0) dict with per-point outputs, V_opt [P, n_v] and timing; None elsewhere.
 
     mode "chain": the reference's sweeping warm start within a shard -- the homotopy for the
     shard's first point, then the warm-started final step for each next point;
     ``point_solver(u, prev) -> (V, outputs, iterations, ok, prev)`` replaces the per-point solve.
+    With ``reconcile`` (chain mode, more than one rank) the shards are then joined into the
+    reference's single chain (awebox/sweep.py:148-172: every point warm-started from the previous
+    point's solution): rank r re-solves its first point warm-started from rank r-1's last solution
+    (one point-to-point message of that solution), keeps its shard if the re-solved point is the same
+    optimum as its own homotopy's (``same_optimum``) and re-chains its shard from the re-solved point
+    otherwise (see reconcile_shard).
     mode "batch": the shard's points are independent trials solved side by side, the full homotopy
     from the standard initial guess for every point as one batched interior-point solve per step
     (``make_evaluator(consts, batch)``).
@@ -114,7 +120,7 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     its solution in one batched final-step solve."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
-    coll_dev = torch.device(device)
+    coll_dev = torch.device(coll_device or device)
     prob = _Dual(n_k, d) if arch == "dual" else _Ap2(n_k, d)
     consts, lay, nconst = prob.consts, prob.lay, prob.nconst
     n_pts = len(u_refs)
@@ -159,6 +165,7 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
                         opts=hippo_options("final", opts), device=device)
             return res.x, prob.outputs(res.x), res.iterations, res.status in done, res
 
+    states = [None] * per          # (x, lam_g, zl, zu) of every local point: the reconciliation's warm starts
     res_v = torch.zeros(per, lay.n_v, dtype=torch.float64, device=coll_dev)
     res_o = torch.full((per, N_OUT), float("nan"), dtype=torch.float64, device=coll_dev)
     prev = None
@@ -263,9 +270,14 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
         res_v[i] = torch.tensor(V, device=coll_dev)
         res_o[i] = torch.tensor([u, out["avg_power_W"], out["period_s"], iters, float(ok),
                                  time.perf_counter() - t0], device=coll_dev)
+        if prev is not None and hasattr(prev, "lam_g"):
+            states[i] = (prev.x, prev.lam_g, prev.zl, prev.zu)
         if verbose:
             print(f"[rank {rank}] u_ref={u:.3f} P={out['avg_power_W']:.1f} W T={out['period_s']:.2f} s "
                   f"iters={iters} ok={ok} {time.perf_counter() - t0:.1f} s", flush=True)
+    if reconcile and mode == "chain" and dist is not None and world > 1 and make_evaluator is not None:
+        _reconcile_ranks(dist, rank, world, prob, ev, opts, device, v0, seeds.cpu().numpy(), states, res_v, res_o,
+                         coll_dev, verbose)
     t_rank = time.perf_counter() - t_rank
 
     # ---- gather to rank 0 -----------------------------------------------------------------------
@@ -289,6 +301,121 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
             "iterations": O_all[:, 3].astype(int).tolist(), "ok": O_all[:, 4].astype(bool).tolist(),
             "seconds": O_all[:, 5].tolist(), "V_opt": V_all, "wall_s": t_rank, "world": world,
             "trials_per_s": len(O_all) / t_rank}
+
+
+SAME_OPTIMUM_RTOL = 1e-4      # relative power and period difference of two solutions of one optimum
+
+
+def same_optimum(out_a, out_b, rtol=SAME_OPTIMUM_RTOL) -> bool:
+    """Whether two converged solutions of one sweep point are the same local optimum: average power
+    and period agree to ``rtol`` (a different orbit family differs by percents; a different KKT point
+    of a flat optimum reached from another warm start by 1e-3 -- profiles/r05/config4/compare.json)."""
+    pa, pb = out_a["avg_power_W"], out_b["avg_power_W"]
+    ta, tb = out_a["period_s"], out_b["period_s"]
+    if not all(np.isfinite(v) for v in (pa, pb, ta, tb)):
+        return False
+    return abs(pa - pb) <= rtol * abs(pb) and abs(ta - tb) <= rtol * abs(tb)
+
+
+def warm_point_solver(prob, ev, opts, device, v0):
+    """solve(u, state) -> (state, outputs, iterations, ok): the reference's sweeping warm start of one
+    point (the final homotopy step's costs and bounds, multipliers kept)."""
+    final = prob.final_step(v0)
+    lbg, ubg = prob.lay.g_bounds()
+    done = ("solve_succeeded", "solved_to_acceptable_level")
+
+    def solve_warm(u, state):
+        x, lam, zl, zu = state
+        P = prob.pack_p(v0, final.cost_step, u)
+        r = solve(ev, P, x, final.lbx, final.ubx, lbg, ubg, lam0=lam, zl0=zl, zu0=zu,
+                  opts=hippo_options("final", opts), device=device)
+        return (r.x, r.lam_g, r.zl, r.zu), prob.outputs(r.x), r.iterations, r.status in done
+    return solve_warm
+
+
+def reconcile_shard(solve_warm, us, states, outs, iters, oks, pred_state, pred_changed, spec_first=None):
+    """Join one shard to the chain of the shards before it (the reference solves the sweep as one
+    chain, awebox/sweep.py:148-172).  ``pred_state``: the final solution of the previous shard's last
+    point.  The shard's first point is re-solved warm-started from it (``spec_first``: that re-solve,
+    done beforehand from the previous shard's own last point, valid when ``pred_changed`` is False);
+    if the result is the same optimum as the shard's own homotopy solution (same_optimum), the shard's
+    chain stands with the re-solved first point; otherwise the shard is re-chained from the re-solved
+    point.  Lists are updated in place; returns whether the shard's last solution changed."""
+    first = spec_first if (spec_first is not None and not pred_changed) else solve_warm(us[0], pred_state)
+    st0, out0, it0, ok0 = first
+    keep = bool(ok0 and oks[0] and same_optimum(out0, outs[0]))
+    states[0], outs[0], iters[0], oks[0] = st0, out0, it0, ok0
+    if keep:
+        return len(us) == 1
+    for i in range(1, len(us)):
+        states[i], outs[i], iters[i], oks[i] = solve_warm(us[i], states[i - 1])
+    return True
+
+
+def _pack_state(state, n_v, n_g, dev, flag=0.0):
+    t = torch.zeros(1 + 3 * n_v + n_g, dtype=torch.float64, device=dev)
+    t[0] = flag
+    if state is not None:
+        x, lam, zl, zu = state
+        t[1:1 + n_v] = torch.as_tensor(x)
+        t[1 + n_v:1 + n_v + n_g] = torch.as_tensor(lam)
+        t[1 + n_v + n_g:1 + 2 * n_v + n_g] = torch.as_tensor(zl)
+        t[1 + 2 * n_v + n_g:] = torch.as_tensor(zu)
+    return t
+
+
+def _unpack_state(t, n_v, n_g):
+    a = t.cpu().numpy()
+    return float(a[0]), (a[1:1 + n_v].copy(), a[1 + n_v:1 + n_v + n_g].copy(),
+                         a[1 + n_v + n_g:1 + 2 * n_v + n_g].copy(), a[1 + 2 * n_v + n_g:].copy())
+
+
+def _reconcile_ranks(dist, rank, world, prob, ev, opts, device, v0, seeds, states, res_v, res_o, coll_dev, verbose):
+    """reconcile_shard across the ranks, with the first re-solves speculative and parallel: every rank
+    sends its last solution to the next rank and re-solves its first point from the one it receives
+    (all ranks at once); then, in rank order, each rank learns whether the previous shard's last
+    solution changed (re-solving again only then), keeps or re-chains its shard, and passes the flag and
+    its final last solution on.  Only point-to-point messages of one solution between neighbours."""
+    n_v, n_g = prob.lay.n_v, int(len(prob.lay.g_bounds()[0]))
+    us = [float(u) for u in seeds if np.isfinite(u)]
+    n = len(us)
+    if n == 0 or any(s is None for s in states[:n]):
+        raise RuntimeError("reconciliation needs every local point's solution")
+    t0 = time.perf_counter()
+    solve_warm = warm_point_solver(prob, ev, opts, device, v0)
+    outs = [{"avg_power_W": float(res_o[i, 1]), "period_s": float(res_o[i, 2])} for i in range(n)]
+    iters = [int(res_o[i, 3]) for i in range(n)]
+    oks = [bool(res_o[i, 4] > 0) for i in range(n)]
+    sts = list(states[:n])
+    # speculative phase: last solution -> next rank, first point re-solved from the previous rank's
+    reqs = []
+    if rank + 1 < world:
+        reqs.append(dist.isend(_pack_state(sts[-1], n_v, n_g, coll_dev), dst=rank + 1))
+    spec = None
+    if rank > 0:
+        buf = _pack_state(None, n_v, n_g, coll_dev)
+        dist.recv(buf, src=rank - 1)
+        _, pred_spec = _unpack_state(buf, n_v, n_g)
+        spec = solve_warm(us[0], pred_spec)
+    for rq in reqs:
+        rq.wait()
+    # sequential phase, in rank order
+    changed = False
+    if rank > 0:
+        buf = _pack_state(None, n_v, n_g, coll_dev)
+        dist.recv(buf, src=rank - 1)
+        flag, pred_final = _unpack_state(buf, n_v, n_g)
+        changed = reconcile_shard(solve_warm, us, sts, outs, iters, oks, pred_final, flag > 0, spec_first=spec)
+    if rank + 1 < world:
+        dist.send(_pack_state(sts[-1], n_v, n_g, coll_dev, flag=1.0 if changed else 0.0), dst=rank + 1)
+    el = time.perf_counter() - t0
+    for i in range(n):
+        res_v[i] = torch.as_tensor(sts[i][0], device=coll_dev)
+        res_o[i, 1], res_o[i, 2] = outs[i]["avg_power_W"], outs[i]["period_s"]
+        res_o[i, 3], res_o[i, 4] = iters[i], float(oks[i])
+    if verbose:
+        print(f"[rank {rank}] reconciled with the previous shard: {'re-chained' if changed else 'kept'} "
+              f"({el:.1f} s)", flush=True)
 
 
 def main():

@@ -34,18 +34,38 @@ def hippo_options(label: str, base: IpmOptions | None = None) -> IpmOptions:
 # Evaluation path of the homotopy drivers.  The final homotopy step crosses a
 # non-convex region in which the regularised Newton map expands roundoff ~1.2x per iteration, so the
 # local optimum it ends on depends on the last bits of the evaluation (35.9 / 51.7 / 70 s branches
-# under 1e-13 perturbations, profiles/r05/ensemble/).  The drivers therefore pin one path for every
-# batch size -- the colour kernel with the hyper-dual Hessian, whose unperturbed run reaches the
-# reference's 35 s anchor -- so that a problem solved alone or inside a batch of any size follows the
-# same iterates (tests/test_regression.py).  eval_path=None keeps the evaluator's own path.
+# under 1e-13 perturbations, profiles/r05/ensemble/).  The drivers run one path for every batch size
+# -- the colour kernel with the hyper-dual Hessian -- because each evaluation path rounds differently.
+# The pin alone does not make a batched solve reproduce a single one: that also needs every reduction
+# and product of the solver in an order that does not depend on the batch (ipm.py, det.py; DESIGN.md
+# section 9, "Batch invariance").  eval_path=None keeps the evaluator's own path.
 HOMOTOPY_EVAL_PATH = "colour"
 
 
-def _pin_path(ev, eval_path):
-    if eval_path is not None and hasattr(ev, "path"):
-        ev.path = eval_path
-        if hasattr(ev, "hess_path"):
-            ev.hess_path = "follow"
+class _pinned_path:
+    """Run the evaluator on ``eval_path`` (with the Hessian following it) inside the block and
+    restore the caller's path and Hessian mode afterwards (None: leave the evaluator alone)."""
+
+    def __init__(self, ev, eval_path):
+        self.ev, self.eval_path = ev, eval_path
+
+    def __enter__(self):
+        ev = self.ev
+        self.saved = None
+        if self.eval_path is not None and hasattr(ev, "path"):
+            self.saved = (ev.path, getattr(ev, "hess_mode", None))
+            ev.path = self.eval_path
+            if hasattr(ev, "hess_path"):
+                ev.hess_path = "follow"
+        return ev
+
+    def __exit__(self, *exc):
+        if self.saved is not None:
+            path, hmode = self.saved
+            self.ev.path = path
+            if hmode is not None:
+                self.ev.hess_path = hmode
+        return False
 
 
 def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device="cuda",
@@ -54,7 +74,11 @@ def optimize(consts: pb.Ap2Constants, ev, opts: IpmOptions | None = None, device
     """Run the homotopy; returns (V_opt, per-step summaries, outputs, last IpmResult).
     ``u_ref`` overrides the wind reference speed in P (the sweep parameter); ``eval_path`` is the
     evaluation path the homotopy runs on (HOMOTOPY_EVAL_PATH; None: the evaluator's own)."""
-    _pin_path(ev, eval_path)
+    with _pinned_path(ev, eval_path):
+        return _optimize(consts, ev, opts, device, v_init, final_step, verbose, u_ref, keep_logs)
+
+
+def _optimize(consts, ev, opts, device, v_init, final_step, verbose, u_ref, keep_logs):
     lay = pb.NlpLayout(consts.cfg.n_k, consts.cfg.d)
     v0 = initial_guess(consts, lay) if v_init is None else v_init
     steps = hm.schedule(consts, lay, v0)
@@ -89,7 +113,11 @@ def optimize_batch(consts: pb.Ap2Constants, ev, u_refs, opts: IpmOptions | None 
     batched interior-point solve (ipm.solve_batch) in which each instance keeps its own IPOPT
     iteration; all instances share the layout, bounds and schedule, and differ in P's u_ref.
     Returns (V [B, n_v], per-step summaries (lists over instances), outputs per instance, results)."""
-    _pin_path(ev, eval_path)
+    with _pinned_path(ev, eval_path):
+        return _optimize_batch(consts, ev, u_refs, opts, device, v_init, verbose)
+
+
+def _optimize_batch(consts, ev, u_refs, opts, device, v_init, verbose):
     lay = pb.NlpLayout(consts.cfg.n_k, consts.cfg.d)
     v0 = initial_guess(consts, lay) if v_init is None else v_init
     B = len(u_refs)

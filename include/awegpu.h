@@ -127,7 +127,12 @@ int awe_sparsity_jac(awe_handle h, int* colind, int* row);
 int awe_sparsity_jac_static(int n_k, int d, const double* consts, int n_consts, int* nnz, int* colind,
                             int* row);
 
-/* Device-pointer evaluation on HIP stream `stream` (NULL = default stream); asynchronous. */
+/* Device-pointer evaluation on HIP stream `stream` (NULL = default stream); asynchronous.
+ * Concurrency: a handle owns scratch buffers (the instance-minor transposes, the generated
+ * Hessian's HD / partial / H buffers, the hyper-dual scratch) and timing events that every call
+ * reuses without ordering them across streams.  Use each handle from one stream at a time: calls on
+ * one handle must be serialised (one stream, or the caller orders the streams with events).  Two
+ * handles are independent and may run on different streams concurrently. */
 int awe_eval_nlp(awe_handle h, const double* V, const double* P, double* f, double* g,
                  double* grad_f, double* jac, void* stream);
 int awe_eval_g(awe_handle h, const double* V, const double* P, double* g, void* stream);

@@ -51,6 +51,23 @@ int awelu_gather_sum(int L, int rows, const int* lsrc, const unsigned char* lw, 
                      long long ldv, const double* x, const int* cols, long long ldx, double* out, long long ldo,
                      void* stream);
 
+/* Batch-invariant row sums (awebox_amd/det.py): out[r] = sum of x[r * ldx + j] over j < n, for
+ * r < rows.  Thread t of 256 adds x[t], x[t + 256], ... in sequence; the 256 partial sums are added
+ * as an adjacent-pair tree.  The order depends on n only, never on rows, so a solver's norms, dot
+ * products and merit terms round the same for one instance as inside any batch (the reference
+ * solves every sweep point as its own IPOPT problem: awebox/sweep.py:148-172,
+ * opti/optimization.py:363). */
+int awelu_row_sum(long long rows, long long n, const double* x, long long ldx, double* out, void* stream);
+
+/* Batch-invariant batched matrix products (awebox_amd/det.py): C[b] = A[b] B[b], M x K times K x N,
+ * element strides (sAm, sAk), (sBk, sBn), (sCm, sCn) and batch strides sAb, sBb, sCb (a transposed
+ * operand is a swapped stride pair); C must not overlap A or B.  Every entry is summed over k in
+ * sequence from 0, product and sum rounded separately: the bits depend on K only, not on the batch
+ * or on the tile shape the launch picks (rocBLAS picks its kernel by the batch count). */
+int awelu_bmm(int batch, int M, int N, int K, const double* A, long long sAb, long long sAm, long long sAk,
+              const double* B, long long sBb, long long sBk, long long sBn, double* C, long long sCb, long long sCm,
+              long long sCn, void* stream);
+
 /* Message of the last failed call on this thread. */
 const char* awelu_last_error(void);
 

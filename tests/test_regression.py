@@ -191,27 +191,30 @@ def test_ap2_n40_final_step_branch_ensemble(path):
 
 @pytest.mark.gpu
 def test_ap2_n40_batched_homotopy_b128():
-    """The outcome of a batched homotopy: the default N=40 homotopy for 128 identical
-    instances in one batch (trajectory.optimize_batch, the drivers' colour path, every IPM step batched
-    over the 128).  Every member converges in every step, all 128 return bitwise the same V, and the
-    power anchor holds.  The batch does not reproduce the single-instance run bitwise: the solver's
-    reductions and batched GEMMs round with the batch's shape, and the final step amplifies that
-    (profiles/r05/ensemble/batch_homotopy.log: the 51.7 s branch at B = 128 against
-    35.9 s alone), so the period is one of the ensemble's branches."""
+    """A batched homotopy reproduces the single one bitwise (batch invariance):
+    the default N=40 homotopy for 128 identical instances in one batch (trajectory.optimize_batch, the
+    drivers' colour path, every interior-point step batched over the 128) returns for every member the
+    V and the per-step iteration counts of the B = 1 run, and so meets the reference's anchors exactly
+    when the single run does (test_examples.py:29-58: 4.7 kW and 35 s, each within 20 %).  Every
+    reduction and product of the solver has an order that does not depend on the batch (det.py;
+    round 5 measured 51.7 s at B = 128 against 35.9 s alone, profiles/r05/ensemble/batch_homotopy.log)."""
     import torch
     if not torch.cuda.is_available():
         pytest.fail("GPU test on a machine without a visible GPU")
     from awebox_amd.evaluator import Ap2Evaluator
-    from awebox_amd.trajectory import optimize_batch, period_branch
-    consts = pb.build_constants()
+    from awebox_amd.trajectory import optimize_batch
+    consts, lay, ev1, V1, summary1, out1 = _default_homotopy_cached(None)
     B = 128
     ev = Ap2Evaluator(consts, batch=B)
     V, summary, outs, _ = optimize_batch(consts, ev, [10.0] * B, IpmOptions(max_iter=2000))
-    for r in summary:
+    for r, r1 in zip(summary, summary1):
         assert all(s == "solve_succeeded" for s in r["status"]), r["step"]
-    assert all(np.array_equal(V[b], V[0]) for b in range(B))
-    assert abs(4.7 - outs[0]["avg_power_W"] / 1e3) / 4.7 <= ANCHOR_THRESHOLD, outs[0]
-    assert not period_branch(outs[0]["period_s"]).startswith("other"), outs[0]
+        assert r["iterations"] == [r1["iterations"]] * B, (r["step"], r1["iterations"], r["iterations"][:4])
+    for b in range(B):
+        assert np.array_equal(V[b], V1), b
+    err_p = (4.7 - outs[0]["avg_power_W"] / 1e3) / 4.7
+    err_t = (35.0 - outs[0]["period_s"]) / 35.0
+    assert abs(err_p) <= ANCHOR_THRESHOLD and abs(err_t) <= ANCHOR_THRESHOLD, outs[0]
 
 
 @pytest.mark.gpu

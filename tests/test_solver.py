@@ -241,20 +241,6 @@ def test_sweep_single_process_warm_start_chain():
     assert res["avg_power_W"][1] > 0
 
 
-def test_batched_homotopy_matches_single_solves_on_cpu_port():
-    """ipm.solve_batch: three wind speeds solved side by side through the whole homotopy reach the
-    solutions of three separate solves (each instance keeps its own IPOPT iteration)."""
-    from oracle.cpu_device import CpuDeviceEvaluator
-    from awebox_amd.trajectory import optimize_batch
-    consts = pb.build_constants(pb.Ap2Config(n_k=6, d=3))
-    lay = pb.NlpLayout(6, 3)
-    ev = CpuDeviceEvaluator(consts)
-    u_refs = [9.0, 10.0, 11.0]
-    Vb, summary, outs, res = optimize_batch(consts, ev, u_refs, IpmOptions(max_iter=400), device="cpu")
-    for r in summary:
-        assert all(s == "solve_succeeded" for s in r["status"]), r
-    for b, u in enumerate(u_refs):
-        V1, s1, o1, _ = optimize(consts, ev, IpmOptions(max_iter=400), device="cpu", u_ref=u)
-        assert all(r["status"] == "solve_succeeded" for r in s1)
-        assert abs(outs[b]["avg_power_W"] - o1["avg_power_W"]) <= 1e-6 * abs(o1["avg_power_W"]), (u, outs[b], o1)
-        assert np.abs(Vb[b] - V1).max() <= 1e-5 * max(1.0, np.abs(V1).max())
+# test_batched_homotopy_matches_single_solves_on_cpu_port (rounds 2-5: a batch of three wind speeds
+# within 1e-5 of three separate solves) is now tests/test_det.py's bitwise statement of the same
+# property: batched and single solves return the same bits (det.py).
