@@ -856,6 +856,10 @@ __global__ __launch_bounds__(NT) void sym_inertia_unblocked_kernel(int n, double
                 kp = imax;
                 kstep = 2;
             }
+            // every thread has read L(imax, imax) for the decision above before any thread's
+            // interchange below writes it (without this barrier a late wave could decide on the
+            // swapped value: the pivot choice, and with it the counts, then depended on timing)
+            __syncthreads();
         }
         const int kk = k + kstep - 1;
         if (kp != kk) {                                  // symmetric interchange of kk and kp
@@ -1025,6 +1029,10 @@ __global__ __launch_bounds__(kThreads) void sym_inertia_kernel(int n, int nb, do
                 }
                 kp = __builtin_amdgcn_readfirstlane(kp);     // uniform by construction; made
                 kstep = __builtin_amdgcn_readfirstlane(kstep);   // scalar for the compiler
+                // every wave has read W(imax, j + 1) for the decision above before the 2 x 2
+                // interchange below rewrites it (a late wave would otherwise decide on the swapped
+                // value, and the waves could disagree on the pivot)
+                __syncthreads();
             }
             const int kk = k + kstep - 1;
             if (kp != kk) {

@@ -29,10 +29,13 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
 ROW_SUM_THREADS = 256
+# AWE_DET_OFF=1: torch's own reductions and matmul instead (A/B measurements only: batch-dependent)
+_OFF = os.environ.get("AWE_DET_OFF", "0") == "1"
 
 
 def _lib():
@@ -50,6 +53,8 @@ def row_sum(x: torch.Tensor, emulate: bool = False) -> torch.Tensor:
     """Sum over the last dimension of float64 ``x`` [..., n] in the fixed order of awelu_row_sum."""
     if x.dtype != torch.float64:
         raise ValueError("row_sum needs float64")
+    if _OFF and not emulate:
+        return x.sum(-1)
     n = x.shape[-1]
     lead = x.shape[:-1]
     R = math.prod(lead)
@@ -106,6 +111,8 @@ def bmm(A: torch.Tensor, B: torch.Tensor, emulate: bool = False) -> torch.Tensor
     contiguous [batch, M, N] (or [M, N]) tensor."""
     if A.dtype != torch.float64 or B.dtype != torch.float64:
         raise ValueError("bmm needs float64")
+    if _OFF and not emulate:
+        return A @ B
     squeeze = A.dim() == 2
     A3 = A.unsqueeze(0) if squeeze else A
     B3 = B.unsqueeze(0) if squeeze else B

@@ -101,7 +101,8 @@ class _Dual:
 
 
 def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda", opts: IpmOptions | None = None,
-              verbose=False, point_solver=None, arch="single", mode="chain", reconcile=True, coll_device=None):
+              verbose=False, point_solver=None, arch="single", mode="chain", reconcile=True, coll_device=None,
+              return_states=False):
     """Returns (on rank 0) dict with per-point outputs, V_opt [P, n_v] and timing; None elsewhere.
 
     mode "chain": the reference's sweeping warm start within a shard -- the homotopy for the
@@ -117,7 +118,9 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     from the standard initial guess for every point as one batched interior-point solve per step
     (``make_evaluator(consts, batch)``).
     mode "fan": the homotopy for the shard's first point, then the other points warm-started from
-    its solution in one batched final-step solve."""
+    its solution in one batched final-step solve.
+    ``return_states`` (one process): the result also holds every point's (x, lam_g, zl, zu) under
+    "states" (chain mode), the problem under "problem" and the template initial guess under "v0"."""
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     coll_dev = torch.device(coll_device or device)
@@ -297,7 +300,10 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
         V_all, O_all = res_v.cpu().numpy(), res_o.cpu().numpy()
     keep = np.isfinite(O_all[:, 0])
     O_all, V_all = O_all[keep], V_all[keep]
-    return {"u_ref": O_all[:, 0].tolist(), "avg_power_W": O_all[:, 1].tolist(), "period_s": O_all[:, 2].tolist(),
+    extra = {}
+    if return_states and dist is None:
+        extra = {"states": states[:len(O_all)], "problem": prob, "v0": v0}
+    return {**extra, "u_ref": O_all[:, 0].tolist(), "avg_power_W": O_all[:, 1].tolist(), "period_s": O_all[:, 2].tolist(),
             "iterations": O_all[:, 3].astype(int).tolist(), "ok": O_all[:, 4].astype(bool).tolist(),
             "seconds": O_all[:, 5].tolist(), "V_opt": V_all, "wall_s": t_rank, "world": world,
             "trials_per_s": len(O_all) / t_rank}

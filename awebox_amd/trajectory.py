@@ -33,12 +33,14 @@ def hippo_options(label: str, base: IpmOptions | None = None) -> IpmOptions:
 
 # Evaluation path of the homotopy drivers.  The final homotopy step crosses a
 # non-convex region in which the regularised Newton map expands roundoff ~1.2x per iteration, so the
-# local optimum it ends on depends on the last bits of the evaluation (35.9 / 51.7 / 70 s branches
-# under 1e-13 perturbations, profiles/r05/ensemble/).  The drivers run one path for every batch size
-# -- the colour kernel with the hyper-dual Hessian -- because each evaluation path rounds differently.
-# The pin alone does not make a batched solve reproduce a single one: that also needs every reduction
-# and product of the solver in an order that does not depend on the batch (ipm.py, det.py; DESIGN.md
-# section 9, "Batch invariance").  eval_path=None keeps the evaluator's own path.
+# local optimum it ends on depends on the last bits of the evaluation (35.9 / 51.7 / 53.6 / 70 s
+# branches under 1e-13 perturbations, profiles/r06/ensemble/).  The drivers run one path for every
+# batch size -- the colour kernel with the hyper-dual Hessian -- because each evaluation path rounds
+# differently; together with the solver's batch-invariant sums and products (det.py) and race-free
+# inertia kernels, a problem solved alone or inside a batch of any size then follows the same iterates
+# bitwise (tests/test_regression.py::test_ap2_n40_batched_homotopy_b128, tests/test_det_gpu.py).
+# Which branch the default run lands on is still a matter of its rounding (round 6: the t_f bound).
+# eval_path=None keeps the evaluator's own path.
 HOMOTOPY_EVAL_PATH = "colour"
 
 

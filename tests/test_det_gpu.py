@@ -145,3 +145,41 @@ def test_fan_shard_warm_start_is_partition_invariant():
             assert a.iterations == b.iterations, (per, i, a.iterations, b.iterations)
             assert np.array_equal(a.x, b.x), (per, i)
             assert np.array_equal(a.lam_g, b.lam_g), (per, i)
+
+
+def test_dual_fan_shard_warm_start_is_partition_invariant():
+    """The same partition invariance for config 4's dual kites (N=20 d=4, the block recursion of
+    100 x 100 separator blocks: det.bmm products and the awelu solve): rank 0's first 4 points of
+    linspace(5, 8, 64) warm-started from the homotopy solution at the first point, solved as one batch
+    of 4 and one by one, return the same V and iteration counts."""
+    _need_gpu()
+    from awebox_amd import dual as du
+    from awebox_amd import dual_homotopy as dh
+    from awebox_amd.ipm import IpmOptions, solve_batch
+    from awebox_amd.trajectory import hippo_options
+    consts = du.build_constants(du.MultiConfig(n_k=20, d=4))
+    lay = du.layout_for(consts)
+    v0 = du.initial_guess(consts, lay)
+    us = np.linspace(5.0, 8.0, 64)[:5]
+    ev1 = dh.make_evaluator(consts, batch=1)
+    _, _, _, res0 = dh.optimize(consts, ev1, IpmOptions(max_iter=3000), v_init=v0, u_ref=float(us[0]))
+    final = dh.schedule(consts, lay, v0)[-1]
+    lbg, ubg = lay.g_bounds()
+    opts = hippo_options("final", IpmOptions(max_iter=3000))
+    evs = {1: ev1}
+
+    def run(chunk):
+        b = len(chunk)
+        if b not in evs:
+            evs[b] = dh.make_evaluator(consts, batch=b)
+        P = np.stack([du.pack_p(lay, consts, v0, step=final.cost_step, u_ref=u) for u in chunk])
+        return solve_batch(evs[b], P, np.tile(res0.x, (b, 1)), final.lbx, final.ubx, lbg, ubg,
+                           lam0=np.tile(res0.lam_g, (b, 1)), zl0=np.tile(res0.zl, (b, 1)),
+                           zu0=np.tile(res0.zu, (b, 1)), opts=opts)
+
+    ref = run(us[1:])
+    assert all(r.status in ("solve_succeeded", "solved_to_acceptable_level") for r in ref), [r.status for r in ref]
+    got = [run(us[i:i + 1])[0] for i in range(1, 5)]
+    for i, (a, b) in enumerate(zip(ref, got)):
+        assert a.iterations == b.iterations, (i, a.iterations, b.iterations)
+        assert np.array_equal(a.x, b.x), i

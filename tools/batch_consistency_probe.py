@@ -63,17 +63,9 @@ def wrap(cls, name, in_fn, out_fn):
     setattr(cls, name, w)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--K", type=int, default=64)
-    ap.add_argument("--path", default="colour")
-    args = ap.parse_args()
-    from awebox_amd import det, ipm
-    from awebox_amd import problem as pb
-    from awebox_amd.evaluator import Ap2Evaluator
-    from awebox_amd.ipm import IpmOptions
-    from awebox_amd.trajectory import final_step_ensemble, optimize
-
+def install():
+    """Wrap the solver's building blocks (see the module docstring)."""
+    from awebox_amd import ipm
     wrap(ipm.DeviceNlp, "eval_all", lambda s, a, k: [a[0]],
          lambda s, r, a, k: [("f", r[0], 0), ("grad", r[1], 0), ("g", r[2], 0), ("jv", r[3], 0)])
     wrap(ipm.DeviceNlp, "eval_fg", lambda s, a, k: [a[0]], lambda s, r, a, k: [("f", r[0], 0), ("g", r[1], 0)])
@@ -88,6 +80,18 @@ def main():
     wrap(ipm.StructuredKKT, "matvec", lambda s, a, k: [a[0]], lambda s, r, a, k: [("Kx", r, 0)])
     wrap(ipm.StructuredKKT, "inertia", lambda s, a, k: [], lambda s, r, a, k: [("inertia", r, 0)])
 
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=64)
+    ap.add_argument("--path", default="colour")
+    args = ap.parse_args()
+    from awebox_amd import problem as pb
+    from awebox_amd.evaluator import Ap2Evaluator
+    from awebox_amd.ipm import IpmOptions
+    from awebox_amd.trajectory import final_step_ensemble, optimize
+    install()
     consts = pb.build_constants()
     ev1 = Ap2Evaluator(consts, batch=1)
     _, summary, _, res = optimize(consts, ev1, IpmOptions(max_iter=2000), final_step="power1", eval_path=args.path)
