@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = ["awe_create", "awe_destroy", "awe_last_error", "awe_sizes", 
                     "awe_last_kernel_ms", "awe_device_count", "awe_hess_nnz", "awe_sparsity_hess",
                     "awe_sparsity_hess_static", "awe_eval_hess", "awe_eval_hess_host", "awe_last_hess_ms",
                     "awe_set_eval_path", "awe_get_eval_path", "awe_last_kernel_ms_gen", "awe_eval_nlp_im",
-                    "awe_last_kernel_ms_soa", "awe_eval_hess_im", "awe_set_hess_path", "awe_get_hess_path"]
+                    "awe_last_kernel_ms_soa", "awe_eval_hess_im", "awe_set_hess_path", "awe_get_hess_path",
+                    "awe_eval_nlp_imv", "awe_instance_ld"]
 
 PATH_COLOUR, PATH_GENERATED, PATH_SOA = 0, 1, 2
 
@@ -63,6 +64,9 @@ def load_library(path: str = _LIB_PATH):
     lib.awe_eval_nlp_im.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     lib.awe_last_kernel_ms_soa.argtypes = [h, ctypes.POINTER(ctypes.c_float)]
+    lib.awe_eval_nlp_imv.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4 + \
+        [ctypes.c_int, ctypes.c_void_p]
+    lib.awe_instance_ld.argtypes = [h, ip]
     lib.awe_eval_g.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.awe_eval_f.argtypes = [h, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.awe_eval_nlp_host.argtypes = [h, dp, dp, dp, dp, dp, dp]
@@ -195,9 +199,14 @@ class Ap2Evaluator:
         one ld >= B (awe_eval_nlp_im, the layout the batched solver reads; ``alloc_grad`` /
         ``alloc_jac``)."""
         import torch
+        ld_in = self.instance_ld
+        vin_im = (self.batch > 1 and tuple(V.shape) == (self.batch, self.n_v) and V.stride() == (1, ld_in)
+                  and tuple(P.shape) == (self.batch, self.n_p) and P.stride() == (1, ld_in))
         for t, n in ((V, self.n_v), (P, self.n_p), (g, self.n_g)):
-            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != self.batch * n:
-                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape")
+            if t.dtype != torch.float64 or not t.is_cuda or t.numel() != self.batch * n or \
+                    not (t.is_contiguous() or (vin_im and t is not g)):
+                raise ValueError("device tensors must be contiguous float64 CUDA tensors of the batch shape "
+                                 "(V and P may be instance-minor views from alloc_inputs)")
         if f.numel() != self.batch:
             raise ValueError("f must hold one value per batch member")
         for t, n, name in ((jac, self.nnz, "jac"), (grad_f, self.n_v, "grad_f")):
@@ -205,7 +214,13 @@ class Ap2Evaluator:
                 raise ValueError(f"{name} must be a float64 CUDA tensor of shape [batch, {n}]")
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         im = lambda t: t.stride(0) == 1 and t.stride(1) >= self.batch   # noqa: E731
-        if self.batch == 1 or (jac.is_contiguous() and grad_f.is_contiguous()):
+        if vin_im:
+            if not (im(jac) and im(grad_f) and jac.stride(1) == grad_f.stride(1)):
+                raise ValueError("instance-minor V and P need instance-minor jac and grad_f")
+            self._check(self._lib.awe_eval_nlp_imv(self._h, V.data_ptr(), P.data_ptr(), ld_in, f.data_ptr(),
+                                                   g.data_ptr(), grad_f.data_ptr(), jac.data_ptr(),
+                                                   int(jac.stride(1)), ctypes.c_void_p(s)))
+        elif self.batch == 1 or (jac.is_contiguous() and grad_f.is_contiguous()):
             self._check(self._lib.awe_eval_nlp(self._h, V.data_ptr(), P.data_ptr(), f.data_ptr(), g.data_ptr(),
                                                grad_f.data_ptr(), jac.data_ptr(), ctypes.c_void_p(s)))
         elif im(jac) and im(grad_f) and jac.stride(1) == grad_f.stride(1):
@@ -215,6 +230,22 @@ class Ap2Evaluator:
         else:
             raise ValueError("jac and grad_f must both be contiguous or both instance-minor views "
                              "(strides (1, ld), one ld)")
+
+    @property
+    def instance_ld(self):
+        """Leading dimension of the handle's instance-minor buffers (awe_instance_ld)."""
+        v = ctypes.c_int()
+        self._check(self._lib.awe_instance_ld(self._h, ctypes.byref(v)))
+        return v.value
+
+    def alloc_inputs(self, device="cuda"):
+        """(V, P) value tensors [B, n_v], [B, n_p] stored instance-minor (the transposed views of
+        contiguous [n, instance_ld] tensors): eval_nlp_device then runs awe_eval_nlp_imv, which reads
+        them in place instead of transposing per-instance inputs (instance-minor path only)."""
+        import torch
+        ld = self.instance_ld
+        return (torch.zeros(self.n_v, ld, dtype=torch.float64, device=device).t()[:self.batch],
+                torch.zeros(self.n_p, ld, dtype=torch.float64, device=device).t()[:self.batch])
 
     def alloc_jac(self, device="cuda", instance_minor=True):
         """A J_g value tensor [B, nnz]; instance-minor (the transposed view of [nnz, B], which the

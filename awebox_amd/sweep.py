@@ -339,23 +339,41 @@ def warm_point_solver(prob, ev, opts, device, v0):
     return solve_warm
 
 
-def reconcile_shard(solve_warm, us, states, outs, iters, oks, pred_state, pred_changed, spec_first=None):
+def reconcile_shard(solve_warm, us, states, outs, iters, oks, pred_state, pred_changed, spec=None, depth=2):
     """Join one shard to the chain of the shards before it (the reference solves the sweep as one
     chain, awebox/sweep.py:148-172).  ``pred_state``: the final solution of the previous shard's last
-    point.  The shard's first point is re-solved warm-started from it (``spec_first``: that re-solve,
-    done beforehand from the previous shard's own last point, valid when ``pred_changed`` is False);
-    if the result is the same optimum as the shard's own homotopy solution (same_optimum), the shard's
-    chain stands with the re-solved first point; otherwise the shard is re-chained from the re-solved
-    point.  Lists are updated in place; returns whether the shard's last solution changed."""
-    first = spec_first if (spec_first is not None and not pred_changed) else solve_warm(us[0], pred_state)
-    st0, out0, it0, ok0 = first
-    keep = bool(ok0 and oks[0] and same_optimum(out0, outs[0]))
-    states[0], outs[0], iters[0], oks[0] = st0, out0, it0, ok0
+    point.  The shard's first ``depth`` points are re-solved as the chain solves them -- the first
+    warm-started from ``pred_state``, each next one from the one before (``spec``: those re-solves,
+    done beforehand from the previous shard's own last point, valid when ``pred_changed`` is False).
+    If the last re-solved point is the same optimum as the shard's own (same_optimum), the chains have
+    merged and the rest of the shard stands; otherwise the rest is re-chained from the re-solved points.
+    (One point is not enough: a shard's first point comes from its own homotopy and can sit 1e-3 off
+    the chain's on a flat optimum even where the next warm start already agrees to 1e-5,
+    profiles/r06/config4/.)  Lists are updated in place; returns whether the shard's last solution
+    changed."""
+    depth = max(1, min(depth, len(us)))
+    if spec is None or pred_changed:
+        spec, st = [], pred_state
+        for i in range(depth):
+            spec.append(solve_warm(us[i], st))
+            st = spec[-1][0]
+    keep = all(r[3] for r in spec) and oks[depth - 1] and same_optimum(spec[-1][1], outs[depth - 1])
+    for i, r in enumerate(spec):
+        states[i], outs[i], iters[i], oks[i] = r
     if keep:
-        return len(us) == 1
-    for i in range(1, len(us)):
+        return depth == len(us)
+    for i in range(depth, len(us)):
         states[i], outs[i], iters[i], oks[i] = solve_warm(us[i], states[i - 1])
     return True
+
+
+def speculate(solve_warm, us, pred_state, depth=2):
+    """reconcile_shard's re-solves from a predecessor's (possibly provisional) last solution."""
+    out, st = [], pred_state
+    for i in range(max(1, min(depth, len(us)))):
+        out.append(solve_warm(us[i], st))
+        st = out[-1][0]
+    return out
 
 
 def _pack_state(state, n_v, n_g, dev, flag=0.0):
@@ -402,7 +420,7 @@ def _reconcile_ranks(dist, rank, world, prob, ev, opts, device, v0, seeds, state
         buf = _pack_state(None, n_v, n_g, coll_dev)
         dist.recv(buf, src=rank - 1)
         _, pred_spec = _unpack_state(buf, n_v, n_g)
-        spec = solve_warm(us[0], pred_spec)
+        spec = speculate(solve_warm, us, pred_spec)
     for rq in reqs:
         rq.wait()
     # sequential phase, in rank order
@@ -411,7 +429,7 @@ def _reconcile_ranks(dist, rank, world, prob, ev, opts, device, v0, seeds, state
         buf = _pack_state(None, n_v, n_g, coll_dev)
         dist.recv(buf, src=rank - 1)
         flag, pred_final = _unpack_state(buf, n_v, n_g)
-        changed = reconcile_shard(solve_warm, us, sts, outs, iters, oks, pred_final, flag > 0, spec_first=spec)
+        changed = reconcile_shard(solve_warm, us, sts, outs, iters, oks, pred_final, flag > 0, spec=spec)
     if rank + 1 < world:
         dist.send(_pack_state(sts[-1], n_v, n_g, coll_dev, flag=1.0 if changed else 0.0), dst=rank + 1)
     el = time.perf_counter() - t0

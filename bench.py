@@ -196,7 +196,7 @@ def soa_kernels(ev, lay, B, ms):
     out = {}
     for i, name in enumerate(names):
         t = float(ms[i])
-        if t <= 0:
+        if t <= 0 or (name == "ap2_soa_in_kernel" and t < 0.01):   # no transpose (instance-minor inputs)
             continue
         o = {"ms": t}
         if name in by:
@@ -320,9 +320,18 @@ def main():
     gr = ev.alloc_grad(dev, instance_minor=True)
     jac = ev.alloc_jac(dev, instance_minor=True)
     stream = torch.cuda.current_stream(dev)
+    # on the instance-minor path the decision vectors and parameters are handed over instance-minor
+    # too (awe_eval_nlp_imv: no input transposition), the layout a batched caller keeps them in; the
+    # per-instance inputs' rate is paths.soa_instance_minor (awe_eval_nlp_im)
+    V_in, P_in, input_layout = V, P, "per-instance"
+    if ev.path == "soa":
+        V_in, P_in = ev.alloc_inputs(dev)
+        V_in.copy_(V)
+        P_in.copy_(P)
+        input_layout = "instance-minor"
 
     def step():
-        ev.eval_nlp_device(V, P, f, g, gr, jac, stream=stream.cuda_stream)
+        ev.eval_nlp_device(V_in, P_in, f, g, gr, jac, stream=stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -407,12 +416,13 @@ def main():
                    "parallelism": f"replicas x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": ("ap2_soa_in + ap2_soa_shoot + ap2_soa_radau + ap2_soa_interval + ap2_finalize "
-                                "(one evaluation)"
+                     "kernel": ("ap2_soa_shoot + ap2_soa_radau + ap2_soa_interval + ap2_finalize "
+                                "(one evaluation, V and P instance-minor)"
                                 if soa else "ap2_node_kernel + ap2_gather_kernel" if gen else "ap2_interval_kernel"),
                      "kernel_ms": kernel_ms, "finalize_ms": float(np.mean(fms)), "bytes_per_eval": bytes_per_eval},
         "outputs_finite": finite,
         "eval_path": ev.path,
+        "input_layout": input_layout,
     }
     if gen:
         line["roofline"]["kernels"] = gen_kernels(ev, lay, B, float(np.mean(nms)), float(np.mean(gms)))

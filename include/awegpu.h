@@ -189,6 +189,18 @@ int awe_get_hess_path(awe_handle h, int* path);
 int awe_eval_nlp_im(awe_handle h, const double* V, const double* P, double* f, double* g,
                     double* grad_f, double* jac, int ldj, void* stream);
 
+/* awe_eval_nlp_im with V and P instance-minor as well: entry i of instance b at VT[i * ldin + b] and
+ * PT[i * ldin + b], ldin = awe_instance_ld(h).  A batched caller that keeps its decision vectors in
+ * the layout the kernels read (as the batched solver keeps J_g) saves the input transposition (the
+ * first kernel of awe_eval_nlp_im, ~12 % of an evaluation at batch 2048).  Instance-minor evaluation
+ * path only (AWE_PATH_SOA); with batch 1 the layouts coincide and awe_eval_nlp is the same call.
+ * Replaces, for a batch, the per-instance calls of the reference's nlp_jac_g / nlp_grad_f
+ * (awebox/opti/preparation.py:366-400). */
+int awe_eval_nlp_imv(awe_handle h, const double* VT, const double* PT, int ldin, double* f, double* g,
+                     double* grad_f, double* jac, int ldj, void* stream);
+/* Leading dimension of the handle's instance-minor buffers (batch rounded up to 16). */
+int awe_instance_ld(awe_handle h, int* ld);
+
 /* Evaluation path of awe_eval_nlp / awe_eval_nlp_im (f, g, grad f, J_g).  Default: AWE_PATH_SOA
  * for batches of 128 or more instances (when the model constants have the structure the code was
  * generated for), AWE_PATH_COLOUR below (a call is then one round of waves on every path, and the

@@ -96,3 +96,25 @@ def test_colour_and_generated_paths_in_the_solvers_layout(B):
         for lab, a, b in zip(("f", "g", "grad_f", "jac"), im, aos):
             assert np.isfinite(a).all(), (path, lab)
             assert np.array_equal(a, b), (path, lab, float(np.max(np.abs(a - b))))
+
+
+@pytest.mark.parametrize("B", [130, 2])
+def test_instance_minor_inputs_give_the_same_bits(B):
+    """awe_eval_nlp_imv (V and P handed over instance-minor, Ap2Evaluator.alloc_inputs) against
+    awe_eval_nlp_im on the same values in the per-instance layout: the same kernels after the input
+    transposition, so f, g, grad f and J_g are bitwise equal (B = 130: two full instance blocks and a
+    partial one)."""
+    import torch
+    from awebox_amd import evaluator as E
+    consts, V, P = _inputs(B)
+    ev = E.Ap2Evaluator(consts, batch=B)
+    ref = _eval(ev, V, P, "soa", True)
+    VT, PT = ev.alloc_inputs("cuda")
+    VT.copy_(V)
+    PT.copy_(P)
+    assert VT.stride() == (1, ev.instance_ld) and torch.equal(VT, V)
+    got = _eval(ev, VT, PT, "soa", True)
+    for a, b in zip(ref, got):
+        assert np.array_equal(a, b, equal_nan=True)
+    with pytest.raises(RuntimeError):
+        _eval(ev, VT, PT, "colour", True)                       # instance-minor inputs: SOA path only

@@ -1,12 +1,12 @@
 """Joining sweep shards into the reference's single chain (sweep.reconcile_shard, run_sweep's
 ``reconcile``; awebox/sweep.py:148-172 solves every point warm-started from the previous one).
 
-* the decision logic with a stand-in solver: a shard whose re-solved first point is the same optimum
-  keeps its own chain; one that is not is re-chained from the re-solved point, and the flag passed on
-  says whether the shard's last solution changed;
-* two gloo ranks on the CPU harness (AP2 N=4 d=2, 2 + 2 points): rank 1's first point equals the
-  single-process chain's bitwise (it IS the chain's warm start from rank 0's last point), and every
-  point matches the chain's power to the same-optimum tolerance."""
+* the decision logic with a stand-in solver: a shard whose re-solved first two points reach the same
+  optimum as its own chain keeps the rest of it; one that does not is re-chained from the re-solved
+  points, and the flag passed on says whether the shard's last solution changed;
+* two gloo ranks on the CPU harness (AP2 N=4 d=2, 2 + 2 points): rank 1's points equal the
+  single-process chain's bitwise (they ARE the chain's warm starts from rank 0's last point), and
+  every point matches the chain's power."""
 import numpy as np
 import pytest
 
@@ -30,28 +30,33 @@ def test_same_optimum():
     assert not same_optimum(a, {"avg_power_W": float("nan"), "period_s": 35.0})
 
 
-def test_reconcile_keeps_a_matching_shard_and_rechains_a_different_one():
-    us = [1.0, 2.0, 3.0]
+def test_reconcile_keeps_a_merged_shard_and_rechains_a_different_one():
+    us = [1.0, 2.0, 3.0, 4.0]
     solve_warm = _fake(0)
-    # the shard's own chain, family 0 (its homotopy found the same family as the chain before it)
-    states = [(np.array([0.0]),) + (None,) * 3 for _ in us]
-    outs = [{"avg_power_W": 1000.0 * u, "period_s": 30.0} for u in us]
-    iters, oks = [50, 9, 9], [True] * 3
-    changed = reconcile_shard(solve_warm, us, states, outs, iters, oks, (np.array([0.0]),) + (None,) * 3, False)
-    assert not changed and iters == [7, 9, 9]                   # first point re-solved, the rest kept
-    # the previous shard ends on family 5: the re-solved first point differs -> whole shard re-chained
-    states = [(np.array([0.0]),) + (None,) * 3 for _ in us]
-    outs = [{"avg_power_W": 1000.0 * u, "period_s": 30.0} for u in us]
-    iters, oks = [50, 9, 9], [True] * 3
+    fam0 = (np.array([0.0]),) + (None,) * 3
+
+    def shard():
+        states = [fam0 for _ in us]
+        outs = [{"avg_power_W": 1000.0 * u, "period_s": 30.0} for u in us]
+        return states, outs, [50, 9, 9, 9], [True] * 4
+    # the previous shard ends on the shard's own family: the first two points re-solved, the rest kept
+    states, outs, iters, oks = shard()
+    changed = reconcile_shard(solve_warm, us, states, outs, iters, oks, fam0, False)
+    assert not changed and iters == [7, 7, 9, 9]
+    # the previous shard ends on family 5: the second re-solved point differs -> the rest re-chained
+    states, outs, iters, oks = shard()
     changed = reconcile_shard(solve_warm, us, states, outs, iters, oks, (np.array([5.0]),) + (None,) * 3, False)
-    assert changed and iters == [7, 7, 7]
-    assert [o["avg_power_W"] for o in outs] == [1005.0, 2005.0, 3005.0]
-    # a speculative re-solve is used only when the predecessor did not change
-    spec = ((np.array([9.0]),) + (None,) * 3, {"avg_power_W": 1.0, "period_s": 1.0}, 3, True)
-    outs = [{"avg_power_W": 1000.0 * u, "period_s": 30.0} for u in us]
-    iters = [50, 9, 9]
-    reconcile_shard(solve_warm, us, states, outs, iters, oks, (np.array([0.0]),) + (None,) * 3, True, spec_first=spec)
-    assert iters[0] == 7                                        # re-solved from pred_state, spec ignored
+    assert changed and iters == [7, 7, 7, 7]
+    assert [o["avg_power_W"] for o in outs] == [1005.0, 2005.0, 3005.0, 4005.0]
+    # speculative re-solves are used only when the predecessor did not change
+    spec = [((np.array([0.0]),) + (None,) * 3, {"avg_power_W": 1000.0, "period_s": 30.0}, 3, True),
+            ((np.array([0.0]),) + (None,) * 3, {"avg_power_W": 2000.0, "period_s": 30.0}, 3, True)]
+    states, outs, iters, oks = shard()
+    reconcile_shard(solve_warm, us, states, outs, iters, oks, fam0, False, spec=spec)
+    assert iters == [3, 3, 9, 9]
+    states, outs, iters, oks = shard()
+    reconcile_shard(solve_warm, us, states, outs, iters, oks, fam0, True, spec=spec)
+    assert iters == [7, 7, 9, 9]                                # re-solved from pred_state, spec ignored
 
 
 def _worker(rank, world, port, q, us):
@@ -107,6 +112,6 @@ def test_reconciled_shards_follow_the_single_chain_on_cpu():
     assert all(res["ok"]), res
     V, Vc = np.asarray(res["V_opt"]), np.asarray(chain["V_opt"])
     assert np.array_equal(V[0], Vc[0]) and np.array_equal(V[1], Vc[1])   # rank 0's shard is the chain's start
-    assert np.array_equal(V[2], Vc[2])                                    # rank 1's first point: the chain's own solve
+    assert np.array_equal(V[2], Vc[2]) and np.array_equal(V[3], Vc[3])   # rank 1: re-solved as the chain solves them
     for i in range(4):
         assert abs(res["avg_power_W"][i] - chain["avg_power_W"][i]) <= SAME_OPTIMUM_RTOL * abs(chain["avg_power_W"][i]) * 3

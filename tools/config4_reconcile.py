@@ -45,7 +45,7 @@ def main():
     args = ap.parse_args()
     from awebox_amd.dual_homotopy import make_evaluator
     from awebox_amd.ipm import IpmOptions
-    from awebox_amd.sweep import reconcile_shard, run_sweep, warm_point_solver
+    from awebox_amd.sweep import reconcile_shard, run_sweep, speculate, warm_point_solver
     grid = np.linspace(5.0, 8.0, 64)[:args.points]
     opts = IpmOptions(max_iter=3000)
     mk = lambda c, b=1: make_evaluator(c, batch=b)  # noqa: E731
@@ -75,14 +75,15 @@ def main():
         us = list(s["u_ref"])
         outs = [{"avg_power_W": p, "period_s": t} for p, t in zip(s["avg_power_W"], s["period_s"])]
         t1 = time.perf_counter()
-        spec = solve_warm(us[0], spec_last[r - 1])                 # the parallel speculative re-solve
+        spec = speculate(solve_warm, us, spec_last[r - 1])          # the parallel speculative re-solves
         spec_s.append(time.perf_counter() - t1)
         t1 = time.perf_counter()
         pred_final = shards[r - 1]["states"][-1]
         changed = reconcile_shard(solve_warm, us, s["states"], outs, s["iterations"], s["ok"], pred_final,
-                                  changed_prev, spec_first=spec)
+                                  changed_prev, spec=spec)
         seq_s += time.perf_counter() - t1
-        decisions.append("re-chained" if changed and len(us) > 1 else "kept")
+        decisions.append(("re-chained" if changed and len(us) > 2 else "kept")
+                         + (" (predecessor changed)" if changed_prev else ""))
         s["avg_power_W"] = [o["avg_power_W"] for o in outs]
         s["period_s"] = [o["period_s"] for o in outs]
         s["V_opt"] = np.stack([st[0] for st in s["states"]])
@@ -116,8 +117,8 @@ def main():
     out = {"summary": summ, "points": rows}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
-        json.dump(out, fh, indent=1)
-    print(json.dumps(summ), flush=True)
+        json.dump(out, fh, indent=1, default=lambda o: o.item() if hasattr(o, "item") else str(o))
+    print(json.dumps(summ, default=lambda o: o.item() if hasattr(o, "item") else str(o)), flush=True)
 
 
 if __name__ == "__main__":

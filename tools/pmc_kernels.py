@@ -25,6 +25,11 @@ def ap2(B=2048):
     V = torch.tensor(np.stack([batch_member(v0, lay, b) for b in range(B)]), device=dev)
     P = torch.tensor(np.stack([pb.pack_p(lay, consts, v0)] * B), device=dev)
     ev = Ap2Evaluator(consts, batch=B)
+    if ev.path == "soa":                                    # the bench's call: V and P instance-minor
+        VT, PT = ev.alloc_inputs(dev)
+        VT.copy_(V)
+        PT.copy_(P)
+        V, P = VT, PT
     # J_g in the layout the bench and the solver use (instance-minor on the default path)
     out = [torch.empty(B, dtype=torch.float64, device=dev), torch.empty(B, ev.n_g, dtype=torch.float64, device=dev),
            ev.alloc_grad(dev), ev.alloc_jac(dev)]

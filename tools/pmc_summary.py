@@ -99,6 +99,7 @@ def record_gen(batch, dirs):
         rec["kernels"][kern] = {k + ("_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else ""): v for k, v in summ.items()}
         for k, v in summ.items():
             tot[k + ("_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else "")] += v
+    rec["kernel"] = " + ".join(rec["kernels"])
     rec.update(tot)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
         json.dump(rec, fh, indent=1, sort_keys=True)
@@ -106,7 +107,7 @@ def record_gen(batch, dirs):
 
 
 SOA_KERNELS = ("ap2_soa_in_kernel", "ap2_soa_shoot_kernel", "ap2_soa_radau_kernel", "ap2_soa_interval_kernel",
-               "ap2_finalize_kernel")
+               "ap2_finalize_kernel")   # ap2_soa_in_kernel only runs with per-instance inputs
 
 
 def record_soa(batch, dirs):
@@ -116,16 +117,19 @@ def record_soa(batch, dirs):
     sys.path.insert(0, ROOT)
     from bench import kernel_source_hash
     paths = [p for d in dirs for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)]
-    rec = {"batch": batch, "source_hash": kernel_source_hash(), "path": "soa",
-           "kernel": " + ".join(SOA_KERNELS), "kernels": {},
+    rec = {"batch": batch, "source_hash": kernel_source_hash(), "path": "soa", "input_layout": "instance-minor",
+           "kernels": {},
            "units": "FETCH/WRITE_SIZE in kB per dispatch; SQ_* per dispatch; mean over 5 dispatches "
                     "(tools/pmc_kernels.py --ap2, tools/gpu_pmc_soa.sh)"}
     tot = defaultdict(float)
     for kern in SOA_KERNELS:
         summ = summarise(paths, kern)
+        if not summ:
+            continue
         rec["kernels"][kern] = {k + ("_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else ""): v for k, v in summ.items()}
         for k, v in summ.items():
             tot[k + ("_kB" if k in ("FETCH_SIZE", "WRITE_SIZE") else "")] += v
+    rec["kernel"] = " + ".join(rec["kernels"])
     rec.update(tot)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
         json.dump(rec, fh, indent=1, sort_keys=True)
