@@ -92,29 +92,33 @@ def test_config4_far_shard_converges_with_rising_power(gpu):
     assert np.allclose(res["u_ref"], u)
 
 
-# the reference-order curve: one chain over all 64 points (awebox/sweep.py:150-172),
-# tools/config4_full.py --global-chain, profiles/r05/config4/config4_global_chain.jsonl
-GLOBAL_CHAIN = {39: (6.857142857142857, 6921.33, 17.79), 40: (6.904761904761905, 6954.31, 17.9)}
-
-
-def test_config4_shard_boundary_matches_the_reference_order_chain(gpu):
-    """The shard 4 / shard 5 boundary of config 4 (points 39 | 40 of linspace(5, 8, 64), N=20 d=4):
-    shard 5's anchor -- the homotopy at point 40 from the standard initial guess, as rank 5 runs it --
-    and the continuation across the boundary to shard 4's last point (39, warm-started from 40) against
-    the reference-order global chain's solutions at those points.  Both land on the chain's interior
-    orbit family (period below the example's t_f bound of 20 s), not the t_f-bound one: measured on
-    MI355X, point 40 at 6955.0 W / 17.84 s (chain 6954.3 W / 17.90 s) and point 39 at 6900.5 W /
-    17.75 s (chain 6921.3 W / 17.79 s) -- the same family, with the flat power curve's optimum
-    reached to 0.3 % from the other side of the boundary (the chain arrives at 39 from 38).  (Shard 4's
-    own anchor at point 32 does not: its homotopy reaches a 17.7 s orbit where the chain has 16.9 s,
-    and its warm starts 33..39 go to the t_f-bound family, 2-8 % above the chain's power --
-    profiles/r05/config4/compare.json.)"""
-    u = np.linspace(5.0, 8.0, 64)
-    res = _sweep([u[40], u[39]], n_k=20, mode="chain")
-    print("boundary", res["avg_power_W"], res["period_s"], res["iterations"], res["wall_s"])
-    assert all(res["ok"]), res
-    for i, (uu, p, t) in zip((40, 39), zip(res["u_ref"], res["avg_power_W"], res["period_s"])):
-        ug, pg, tg = GLOBAL_CHAIN[i]
-        assert abs(uu - ug) < 1e-12
-        assert t < 19.99 and abs(t - tg) < 0.1, (i, t, tg)
-        assert abs(p - pg) / pg < 5e-3, (i, p, pg)
+def test_config4_reconciled_shards_follow_the_reference_order_chain(gpu):
+    """Shards joined into the reference's single chain (sweep.reconcile_shard; awebox/sweep.py:148-172
+    solves every point warm-started from the previous one): the first 8 points of config 4's grid
+    (N=12 to stay within a test's time) as one chain, and as two shards of 4 -- each shard's own
+    homotopy + chain, then shard 1 joined to shard 0 as rank 1 joins rank 0 (its first two points
+    re-solved from shard 0's last solution; kept if the second agrees with its own chain, re-chained
+    otherwise).  Shard 1's re-solved points are bitwise the chain's, and every point is within 0.1 %
+    of the chain's power (the full 64-point config 4 at N=20: 60 of 64 within 0.1 %,
+    profiles/r06/config4/config4_reconcile.json)."""
+    from awebox_amd.dual_homotopy import make_evaluator
+    from awebox_amd.ipm import IpmOptions
+    from awebox_amd.sweep import reconcile_shard, run_sweep, warm_point_solver
+    u = np.linspace(5.0, 8.0, 64)[:8]
+    opts = IpmOptions(max_iter=3000)
+    mk = lambda c, b=1: make_evaluator(c, batch=b)  # noqa: E731
+    chain = run_sweep(u, n_k=N_K, d=4, make_evaluator=mk, device="cuda", opts=opts, arch="dual", mode="chain")
+    s0 = run_sweep(u[:4], n_k=N_K, d=4, make_evaluator=mk, device="cuda", opts=opts, arch="dual", mode="chain",
+                   return_states=True)
+    s1 = run_sweep(u[4:], n_k=N_K, d=4, make_evaluator=mk, device="cuda", opts=opts, arch="dual", mode="chain",
+                   return_states=True)
+    solve_warm = warm_point_solver(s1["problem"], mk(s1["problem"].consts), opts, "cuda", s1["v0"])
+    outs = [{"avg_power_W": p, "period_s": t} for p, t in zip(s1["avg_power_W"], s1["period_s"])]
+    reconcile_shard(solve_warm, list(u[4:]), s1["states"], outs, s1["iterations"], s1["ok"], s0["states"][-1], False)
+    assert all(chain["ok"]) and all(s0["ok"]) and all(s1["ok"])
+    Vc = np.asarray(chain["V_opt"])
+    assert np.array_equal(s1["states"][0][0], Vc[4]) and np.array_equal(s1["states"][1][0], Vc[5])
+    p = np.asarray(s0["avg_power_W"] + [o["avg_power_W"] for o in outs])
+    pc = np.asarray(chain["avg_power_W"])
+    print("chain", pc.round(1).tolist(), "reconciled", p.round(1).tolist())
+    assert np.all(np.abs(p - pc) <= 1e-3 * pc), (p, pc)
