@@ -25,7 +25,10 @@ available here, so this module restates the IPOPT algorithm (Waechter & Biegler,
   restoration (Gauss-Newton steps on ||c|| inside the bounds until the filter accepts) followed
   by least-squares constraint multipliers.
 
-What is left out: IPOPT's full restoration-phase NLP, the watchdog, and quasi-Newton options.
+* IPOPT's watchdog: after 10 consecutive shortened steps, up to 3 full steps judged against the
+  watchdog's starting point, then back to that point with a backtracking line search;
+
+What is left out: IPOPT's full restoration-phase NLP and quasi-Newton options.
 """
 from __future__ import annotations
 
@@ -75,6 +78,13 @@ class IpmOptions:
     max_backtracks: int = 40
     max_soc: int = 4                 # second-order corrections per line search (IPOPT max_soc)
     kappa_soc: float = 0.99
+    # IPOPT's watchdog (Chamberlain et al.'s technique as IPOPT's BacktrackingLineSearch applies it):
+    # after this many consecutive iterations whose accepted step was shortened by the line search, the
+    # next full steps are taken without backtracking, each judged against the point where the
+    # watchdog started; accepted -> the watchdog ends, after watchdog_trial_iter_max failures the
+    # iterate returns to that point and its line search backtracks (0: off)
+    watchdog_shortened_iter_trigger: int = 10
+    watchdog_trial_iter_max: int = 3
     # IPOPT's bound relaxation: every finite bound of a free variable or an inequality row moves
     # outward by min(constr_viol_tol, bound_relax_factor max(1, |b|)) before the solve
     bound_relax_factor: float = 1e-8
@@ -892,6 +902,13 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
     theta_max = 1e4 * np.maximum(1.0, theta0)
     theta_min = 1e-4 * np.maximum(1.0, theta0)
     delta_w_last = np.zeros(B)
+    # watchdog state per instance (IpmOptions.watchdog_*)
+    wd_short = np.zeros(B, dtype=np.int64)                   # consecutive shortened steps
+    in_wd = np.zeros(B, dtype=bool)
+    wd_trial = np.zeros(B, dtype=np.int64)
+    wd_skip = np.zeros(B, dtype=bool)                        # back at the watchdog's start: skip the full step
+    wd_ref = [np.zeros(B), np.zeros(B), np.zeros(B), np.zeros(B)]   # theta, phi, grad phi . d, alpha
+    wd_pt = None                                             # (y, lam, zl, zu) at the watchdog's start
     status = np.array(["max_iter"] * B, dtype=object)
     iters = np.zeros(B, dtype=np.int64)
     kkt_err = np.full(B, math.inf)
@@ -1095,8 +1112,14 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         skkt.factor(hv, sigma + dev_b(delta_w)[:, None], jv, dev_b(delta_c), mI)
 
     # ---- the filter line search with second-order corrections (all instances in `want`) ---------
-    def line_search(want, dy, dlam, rhs_top, c_cur, dl, du, theta, phi, grad_phi, tau_t, mu_t):
-        """Per instance in `want`: (accepted, alpha, y_trial, dy_used, dlam_used, backtracks, socs)."""
+    def line_search(want, dy, dlam, rhs_top, c_cur, dl, du, theta, phi, grad_phi, tau_t, mu_t, wd=None, wd_ref=None,
+                    skip_first=None, wd_new=None):
+        """Per instance in `want`: (accepted, alpha, y_trial, dy_used, dlam_used, backtracks, socs, alpha_max,
+        wd_failed).  ``wd`` [B] bool: instances in the watchdog -- one trial at the full step, judged
+        against ``wd_ref`` = (theta, phi, grad phi . d, alpha) of the watchdog's starting point, no
+        backtracking and no second-order correction (a failure is reported in wd_failed);
+        ``skip_first`` [B] bool: the first trial point is skipped (the line search after a failed
+        watchdog starts at half the step)."""
         # the fraction-to-the-boundary step and grad phi . dy stay on the device for the first trial
         # and come back with its theta / phi in one copy (the host minimum and the device minimum
         # are the same exact operation)
@@ -1119,17 +1142,23 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         dys = torch.zeros(B, ny, **f64)
         dlam_s = torch.zeros(B, m, **f64)
         a_s = np.zeros(B)
+        wd_failed = np.zeros(B, dtype=bool)
+        skipped = np.zeros(B, dtype=bool)
+        alpha_max = None
 
         def accept_test(b, a, theta_t, phi_t):
             if not (math.isfinite(theta_t) and math.isfinite(phi_t)):
                 return False, False
-            switching = gphi_d[b] < 0 and a * (-gphi_d[b]) ** opts.s_phi > opts.delta_switch * theta[b] ** opts.s_theta
-            if theta[b] <= theta_min[b] and switching:
-                ok_ = phi_t <= phi[b] + opts.eta_phi * a * gphi_d[b]
+            th0, ph0, gp0 = theta[b], phi[b], gphi_d[b]
+            if wd is not None and wd[b]:                          # the watchdog's reference point
+                th0, ph0, gp0, a = wd_ref[0][b], wd_ref[1][b], wd_ref[2][b], wd_ref[3][b]
+            switching = gp0 < 0 and a * (-gp0) ** opts.s_phi > opts.delta_switch * th0 ** opts.s_theta
+            if th0 <= theta_min[b] and switching:
+                ok_ = phi_t <= ph0 + opts.eta_phi * a * gp0
                 f_type = True
             else:
-                ok_ = theta_t <= theta_max[b] and (theta_t <= (1 - opts.gamma_theta) * theta[b] or
-                                                   phi_t <= phi[b] - opts.gamma_phi * theta[b])
+                ok_ = theta_t <= theta_max[b] and (theta_t <= (1 - opts.gamma_theta) * th0 or
+                                                   phi_t <= ph0 - opts.gamma_phi * th0)
                 f_type = False
             return ok_ and filter_ok(b, theta_t, phi_t), f_type
 
@@ -1149,16 +1178,37 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             if alpha is None:
                 tp4 = torch.stack([theta_t, phi_t, alpha_dev, gphi_dev]).cpu().numpy()
                 tp, alpha, gphi_d = tp4[:2], tp4[2].copy(), tp4[3].copy()
+                alpha_max = alpha.copy()
                 alpha_min = opts.alpha_min_frac * np.where(
                     gphi_d < 0, np.minimum(opts.gamma_theta, opts.gamma_phi * theta / np.maximum(-gphi_d, 1e-300)),
                     opts.gamma_theta)
+                if wd_new is not None and wd_new.any():       # a watchdog starting here: its reference
+                    wd_ref[2][wd_new] = gphi_d[wd_new]
+                    wd_ref[3][wd_new] = alpha[wd_new]
+                if skip_first is not None and skip_first.any():
+                    # IPOPT's skip_first_trial_point: these instances start at half the step (their first
+                    # trial, evaluated with the others, is discarded)
+                    skipped[:] = skip_first & live
+                    alpha = np.where(skipped, 0.5 * alpha, alpha)
+                    nback[skipped] += 1
+                    first[skipped] = False
             else:
                 tp = torch.stack([theta_t, phi_t]).cpu().numpy()
             start_soc = np.zeros(B, dtype=bool)
             cont_soc = np.zeros(B, dtype=bool)
             for b in np.where(live)[0]:
                 th_b, ph_b = float(tp[0, b]), float(tp[1, b])
+                if skipped[b]:                                # the skipped first trial: half the step next
+                    skipped[b] = False
+                    continue
                 ok_, f_type = accept_test(b, alpha[b], th_b, ph_b)
+                if wd is not None and wd[b]:                  # watchdog: the full step or nothing
+                    if ok_:
+                        acc[b], live[b] = True, False
+                        a_out[b] = alpha[b]
+                    else:
+                        wd_failed[b], live[b] = True, False
+                    continue
                 if ok_:
                     if not f_type:
                         filt[b].append(((1 - opts.gamma_theta) * theta[b], phi[b] - opts.gamma_phi * theta[b]))
@@ -1215,7 +1265,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 dy_out = torch.where(sel & (dev_b(in_soc)[:, None] > 0), dys, dy_out)
                 dlam_out = torch.where(sel & (dev_b(in_soc)[:, None] > 0), dlam_s, dlam_out)
                 want = want & ~acc
-        return acc, a_out, y_out, dy_out, dlam_out, nback, nsoc
+        return acc, a_out, y_out, dy_out, dlam_out, nback, nsoc, alpha_max, wd_failed
 
     # ---- feasibility restoration (all instances in `want`) ---------------------------------------
     def restoration(want, c0, theta0_, mu_t, max_steps=50):
@@ -1310,6 +1360,9 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             tau = np.maximum(opts.tau_min, 1.0 - mu)
             for b in np.where(upd)[0]:
                 filt[b] = []
+            in_wd &= ~upd                                     # a new barrier problem: line search reset
+            wd_short[upd] = 0
+            wd_skip &= ~upd
         # ---- Newton system ----------------------------------------------------------------------
         with _Phase("hessian"):
             hv = nlp.hess(y[:, :n], lam)
@@ -1325,6 +1378,20 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         rhs_top = -(grad_phi + A_T_lam(jv, lam))
         rhs = torch.cat([rhs_top, -c], 1)
         pending = active.copy()
+        wd_new = np.zeros(B, dtype=bool)
+        if opts.watchdog_shortened_iter_trigger > 0:
+            wd_new = active & ~in_wd & ~wd_skip & (wd_short >= opts.watchdog_shortened_iter_trigger)
+            if wd_new.any():
+                in_wd |= wd_new
+                wd_trial[wd_new] = 0
+                wd_short[wd_new] = 0
+                wd_ref[0][wd_new] = theta[wd_new]
+                wd_ref[1][wd_new] = phi[wd_new]
+                seln = dev_b(wd_new)[:, None] > 0
+                if wd_pt is None:
+                    wd_pt = [t.clone() for t in (y, lam, zl, zu)]
+                wd_pt = [torch.where(seln, t, r) for t, r in zip((y, lam, zl, zu), wd_pt)]
+        wd_restore = np.zeros(B, dtype=bool)
         acc_all = np.zeros(B, dtype=bool)
         alpha_acc = np.zeros(B)
         y_new, dy_new, dlam_new = y.clone(), torch.zeros(B, ny, **f64), torch.zeros(B, m, **f64)
@@ -1340,8 +1407,31 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             if want.any():
                 # the factorisation in skkt is the last attempt's: the accepted (delta_w, delta_c)
                 # of every instance that found a direction (others were still growing)
-                acc, a_o, y_o, dy_o, dl_o, nb_, ns_ = line_search(
-                    want, sol[:, :ny], sol[:, ny:], rhs_top, c, dl, du, theta, phi, grad_phi, tau_d, mu)
+                acc, a_o, y_o, dy_o, dl_o, nb_, ns_, a_max, wd_fail = line_search(
+                    want, sol[:, :ny], sol[:, ny:], rhs_top, c, dl, du, theta, phi, grad_phi, tau_d, mu,
+                    wd=in_wd & want, wd_ref=wd_ref, skip_first=wd_skip & want, wd_new=wd_new & want)
+                # steps shortened by the line search count toward the watchdog's trigger
+                norm_acc = acc & ~in_wd
+                short = norm_acc & (a_o < a_max * (1.0 - 1e-14))
+                wd_short = np.where(short, wd_short + 1, np.where(norm_acc, 0, wd_short))
+                in_wd &= ~acc                                     # a watchdog step accepted: the watchdog ends
+                if wd_fail.any():
+                    wd_trial[wd_fail] += 1
+                    back = wd_fail & (wd_trial > opts.watchdog_trial_iter_max)
+                    go_on = wd_fail & ~back
+                    # within the watchdog's trials: the full step is taken anyway
+                    if go_on.any():
+                        sel_g = dev_b(go_on)[:, None] > 0
+                        dyg = sol[:, :ny]
+                        y_o = torch.where(sel_g, y + dev_b(np.where(go_on, a_max, 0.0))[:, None] * dyg, y_o)
+                        dy_o = torch.where(sel_g, dyg, dy_o)
+                        dl_o = torch.where(sel_g, sol[:, ny:], dl_o)
+                        a_o = np.where(go_on, a_max, a_o)
+                        acc = acc | go_on
+                    # too many: back to the watchdog's starting point, whose line search skips the full step
+                    in_wd &= ~back
+                    wd_restore |= back
+                    pending &= ~back
                 sel = dev_b(acc)[:, None] > 0
                 y_new = torch.where(sel, y_o, y_new)
                 dy_new = torch.where(sel, dy_o, dy_new)
@@ -1354,7 +1444,10 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 pending &= ~acc
         # ---- restoration for the instances without an acceptable step ---------------------------
         rest_ok = np.zeros(B, dtype=bool)
+        wd_skip[:] = False
         if pending.any():
+            in_wd &= ~pending                                 # no watchdog across a restoration phase
+            wd_short[pending] = 0
             succ, y_r, lam_r = restoration(pending, c, theta, mu)
             failed = pending & ~succ
             status[failed] = "restoration_failed"
@@ -1382,6 +1475,12 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             zu = zu + az * dzu
         else:
             az_dev = torch.zeros(B, **f64)
+        if wd_restore.any():
+            # the watchdog failed: the iterate returns to its starting point (the next iteration's
+            # direction there is the one the watchdog started with) and skips the full step
+            selr = dev_b(wd_restore)[:, None] > 0
+            y, lam, zl, zu = (torch.where(selr, r, t) for t, r in zip((y, lam, zl, zu), wd_pt))
+            wd_skip |= wd_restore
         # kappa_sigma safeguard
         dl, du = gaps(y)
         zl = torch.where(hl, torch.clamp(zl, min=mu_d[:, None] / (opts.kappa_sigma * dl),

@@ -244,3 +244,20 @@ def test_sweep_single_process_warm_start_chain():
 # test_batched_homotopy_matches_single_solves_on_cpu_port (rounds 2-5: a batch of three wind speeds
 # within 1e-5 of three separate solves) is now tests/test_det.py's bitwise statement of the same
 # property: batched and single solves return the same bits (det.py).
+
+
+def test_watchdog_reaches_the_same_solution_on_cpu_port():
+    """IPOPT's watchdog (IpmOptions.watchdog_*): with the trigger at one shortened step the watchdog
+    runs in nearly every iteration of the homotopy -- full steps judged against its starting point,
+    returns to that point after three failures -- and the homotopy still converges in every step to
+    the solution of the default run."""
+    from oracle.cpu_device import CpuDeviceEvaluator
+    consts = pb.build_constants(pb.Ap2Config(n_k=4, d=2))
+    ev = CpuDeviceEvaluator(consts)
+    ref = optimize(consts, ev, IpmOptions(max_iter=400), device="cpu")
+    got = optimize(consts, ev, IpmOptions(max_iter=400, watchdog_shortened_iter_trigger=1), device="cpu")
+    for _, s, out, _ in (ref, got):
+        assert all(r["status"] == "solve_succeeded" for r in s), s
+    assert [r["iterations"] for r in ref[1]] != [r["iterations"] for r in got[1]]   # the watchdog ran
+    assert abs(got[2]["avg_power_W"] - ref[2]["avg_power_W"]) <= 1e-6 * abs(ref[2]["avg_power_W"])
+    assert abs(got[2]["period_s"] - ref[2]["period_s"]) <= 1e-6 * ref[2]["period_s"]
