@@ -10,7 +10,7 @@ step() {  # step <limit> <log> <cmd...>
     echo "=== $log rc=$rc"; tail -c 1500 "gpurun_out/$log"; echo
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-step 200 chunks_ab.log python -u tools/soa_chunks_ab.py
+
 step 1000 pytest_gpu.log python -u -m pytest -v --durations=30 --timeout 600 --timeout-method thread tests -m gpu
 step 200 smoke.log python -c "import __graft_entry__ as g; g.smoke()"
 echo R06_SUITE_DONE
