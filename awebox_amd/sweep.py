@@ -153,6 +153,7 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
     my_u = [u for u in seeds.cpu().numpy() if np.isfinite(u)]
 
     # ---- local solves ---------------------------------------------------------------------------
+    point_solver_is_default = point_solver is None
     if point_solver is None and mode == "chain":
         ev = make_evaluator(consts)
         final = prob.final_step(v0)
@@ -278,7 +279,8 @@ def run_sweep(u_refs, n_k=40, d=4, make_evaluator=None, dist=None, device="cuda"
         if verbose:
             print(f"[rank {rank}] u_ref={u:.3f} P={out['avg_power_W']:.1f} W T={out['period_s']:.2f} s "
                   f"iters={iters} ok={ok} {time.perf_counter() - t0:.1f} s", flush=True)
-    if reconcile and mode == "chain" and dist is not None and world > 1 and make_evaluator is not None:
+    if reconcile and mode == "chain" and dist is not None and world > 1 and make_evaluator is not None \
+            and point_solver_is_default:
         _reconcile_ranks(dist, rank, world, prob, ev, opts, device, v0, seeds.cpu().numpy(), states, res_v, res_o,
                          coll_dev, verbose)
     t_rank = time.perf_counter() - t_rank
@@ -394,52 +396,80 @@ def _unpack_state(t, n_v, n_g):
                          a[1 + n_v + n_g:1 + 2 * n_v + n_g].copy(), a[1 + 2 * n_v + n_g:].copy())
 
 
+_NO_STATE = 2.0        # message flag: the sender has no usable last solution (0: unchanged, 1: changed)
+
+
 def _reconcile_ranks(dist, rank, world, prob, ev, opts, device, v0, seeds, states, res_v, res_o, coll_dev, verbose):
     """reconcile_shard across the ranks, with the first re-solves speculative and parallel: every rank
-    sends its last solution to the next rank and re-solves its first point from the one it receives
+    sends its last solution to the next rank and re-solves its first points from the one it receives
     (all ranks at once); then, in rank order, each rank learns whether the previous shard's last
     solution changed (re-solving again only then), keeps or re-chains its shard, and passes the flag and
-    its final last solution on.  Only point-to-point messages of one solution between neighbours."""
+    its final last solution on.  Only point-to-point messages of one solution between neighbours.
+    Every rank takes part in both message rounds whatever happens locally -- a rank without points
+    forwards its predecessor's messages, a failed solve passes a flag instead of a solution -- so no
+    rank waits forever on a neighbour."""
     n_v, n_g = prob.lay.n_v, int(len(prob.lay.g_bounds()[0]))
+    failures = (RuntimeError, ValueError, FloatingPointError, ArithmeticError)
     us = [float(u) for u in seeds if np.isfinite(u)]
     n = len(us)
-    if n == 0 or any(s is None for s in states[:n]):
-        raise RuntimeError("reconciliation needs every local point's solution")
     t0 = time.perf_counter()
     solve_warm = warm_point_solver(prob, ev, opts, device, v0)
     outs = [{"avg_power_W": float(res_o[i, 1]), "period_s": float(res_o[i, 2])} for i in range(n)]
     iters = [int(res_o[i, 3]) for i in range(n)]
     oks = [bool(res_o[i, 4] > 0) for i in range(n)]
     sts = list(states[:n])
-    # speculative phase: last solution -> next rank, first point re-solved from the previous rank's
-    reqs = []
-    if rank + 1 < world:
-        reqs.append(dist.isend(_pack_state(sts[-1], n_v, n_g, coll_dev), dst=rank + 1))
+    valid = n > 0 and all(st is not None for st in sts)
+    my_last = sts[-1] if valid else None
+    recv = lambda: _unpack_state(_recv(dist, _pack_state(None, n_v, n_g, coll_dev), rank - 1), n_v, n_g)  # noqa: E731
+    # speculative phase: last solution -> next rank, first points re-solved from the previous rank's
     spec = None
-    if rank > 0:
-        buf = _pack_state(None, n_v, n_g, coll_dev)
-        dist.recv(buf, src=rank - 1)
-        _, pred_spec = _unpack_state(buf, n_v, n_g)
-        spec = speculate(solve_warm, us, pred_spec)
-    for rq in reqs:
-        rq.wait()
+    if n > 0:
+        reqs = []
+        if rank + 1 < world:
+            reqs.append(dist.isend(_pack_state(my_last, n_v, n_g, coll_dev, 0.0 if valid else _NO_STATE), dst=rank + 1))
+        if rank > 0:
+            flag, pred_spec = recv()
+            if valid and flag != _NO_STATE:
+                try:
+                    spec = speculate(solve_warm, us, pred_spec)
+                except failures as exc:
+                    print(f"[rank {rank}] speculative re-solve failed: {exc}", flush=True)
+        for rq in reqs:
+            rq.wait()
+    elif rank > 0:                                          # no points: the predecessor's state passes on
+        flag, pred_spec = recv()
+        if rank + 1 < world:
+            dist.send(_pack_state(pred_spec, n_v, n_g, coll_dev, flag), dst=rank + 1)
     # sequential phase, in rank order
-    changed = False
+    changed, out_flag, out_state = False, (0.0 if valid else _NO_STATE), my_last
     if rank > 0:
-        buf = _pack_state(None, n_v, n_g, coll_dev)
-        dist.recv(buf, src=rank - 1)
-        flag, pred_final = _unpack_state(buf, n_v, n_g)
-        changed = reconcile_shard(solve_warm, us, sts, outs, iters, oks, pred_final, flag > 0, spec=spec)
+        flag, pred_final = recv()
+        if n == 0:
+            out_flag, out_state = flag, pred_final
+        elif valid and flag != _NO_STATE:
+            try:
+                changed = reconcile_shard(solve_warm, us, sts, outs, iters, oks, pred_final, flag == 1.0, spec=spec)
+            except failures as exc:
+                print(f"[rank {rank}] reconciliation failed, shard kept: {exc}", flush=True)
+                changed = True
+            out_flag, out_state = (1.0 if changed else 0.0), sts[-1]
     if rank + 1 < world:
-        dist.send(_pack_state(sts[-1], n_v, n_g, coll_dev, flag=1.0 if changed else 0.0), dst=rank + 1)
+        dist.send(_pack_state(out_state, n_v, n_g, coll_dev, out_flag if out_state is not None else _NO_STATE),
+                  dst=rank + 1)
     el = time.perf_counter() - t0
     for i in range(n):
-        res_v[i] = torch.as_tensor(sts[i][0], device=coll_dev)
+        if sts[i] is not None:
+            res_v[i] = torch.as_tensor(sts[i][0], device=coll_dev)
         res_o[i, 1], res_o[i, 2] = outs[i]["avg_power_W"], outs[i]["period_s"]
         res_o[i, 3], res_o[i, 4] = iters[i], float(oks[i])
     if verbose:
         print(f"[rank {rank}] reconciled with the previous shard: {'re-chained' if changed else 'kept'} "
               f"({el:.1f} s)", flush=True)
+
+
+def _recv(dist, buf, src):
+    dist.recv(buf, src=src)
+    return buf
 
 
 def main():
