@@ -789,7 +789,7 @@ def sweep_profile(arch: str):
     """GPU utilisation of the sweep block from its committed rocprofv3 record (tools/sweep_record.py):
     busy fraction and the dominant solver kernels, or None when the solver / evaluator sources
     changed since the record was taken."""
-    path = os.path.join(ROOT, "profiles", "r05", "sweep", f"sweep_profile_{arch}.json")
+    path = os.path.join(ROOT, "profiles", "r06", "sweep", f"sweep_profile_{arch}.json")
     try:
         with open(path) as fh:
             rec = json.load(fh)

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 6 records on the final sources: the headline PMC passes (tools/gpu_pmc_soa.sh) and the
+# kernel-trace statistics of the bench's dual-kite sweep block alone (tools/sweep_record.py input).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+bash tools/gpu_pmc_soa.sh || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dsweep -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --dual-batch 0 --mpc-batch 0 --pmpc-loops 0 --sweep-points 0 --no-hessian --no-dual-chain > gpurun_out/rocprof_dsweep.log 2>&1 || exit $?
+find gpurun_out/prof_dsweep -name '*_trace.csv' -size +4M -delete
+echo R06_RECORDS_DONE
