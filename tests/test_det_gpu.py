@@ -183,3 +183,28 @@ def test_dual_fan_shard_warm_start_is_partition_invariant():
     for i, (a, b) in enumerate(zip(ref, got)):
         assert a.iterations == b.iterations, (i, a.iterations, b.iterations)
         assert np.array_equal(a.x, b.x), i
+
+
+def test_batch_mode_sweep_is_partition_invariant():
+    """The sweep's "batch" mode (every point its own full homotopy from the standard initial guess,
+    the shard's points side by side: sweep.run_sweep) on 4 AP2 N=40 points of config 4's grid, as one
+    shard of 4 (one GPU), two shards of 2 (two GPUs) and four shards of 1 (four GPUs): every point
+    returns bitwise the same V and iteration count -- a 1/2/4/8-GPU sweep compares the same answers."""
+    _need_gpu()
+    from awebox_amd.evaluator import Ap2Evaluator
+    from awebox_amd.ipm import IpmOptions
+    from awebox_amd.sweep import run_sweep
+    u = np.linspace(5.0, 8.0, 64)[[0, 9, 18, 27]]
+    mk = lambda c, b=1: Ap2Evaluator(c, batch=b)  # noqa: E731
+
+    def sweep(points):
+        return run_sweep(points, n_k=40, d=4, make_evaluator=mk, device="cuda", opts=IpmOptions(max_iter=2000),
+                         mode="batch")
+    ref = sweep(u)
+    assert all(ref["ok"]), ref
+    for per in (2, 1):
+        parts = [sweep(u[i:i + per]) for i in range(0, 4, per)]
+        V = np.concatenate([np.asarray(p["V_opt"]) for p in parts])
+        its = [i for p in parts for i in p["iterations"]]
+        assert its == ref["iterations"], (per, its, ref["iterations"])
+        assert np.array_equal(V, np.asarray(ref["V_opt"])), per
