@@ -62,7 +62,7 @@ TARGETS = {
                _COMMON + [os.path.join(CSRC, f) for f in ("dual_model.hpp", "dual_tables.hpp", "dual_hess_tables.hpp",
                                                           "awedual_gen.hpp", "im_layout.hpp")]
                + [os.path.join(INCLUDE, "awedual.h"), DUAL_HEADER]),
-    LIB_LU: ([os.path.join(CSRC, "batched_lu.hip")], []),
+    LIB_LU: ([os.path.join(CSRC, "batched_lu.hip")], [os.path.join(INCLUDE, "awelu.h")]),
 }
 ARCH = os.environ.get("AWE_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wno-unused-value",

@@ -18,6 +18,8 @@
 // error test sees the resulting non-finite values.
 #include <hip/hip_runtime.h>
 
+#include "../../include/awelu.h"
+
 #include <algorithm>
 #include <string>
 
@@ -1273,6 +1275,126 @@ __global__ __launch_bounds__(TX * TY) void bmm_kernel(int M, int N, int K, const
         }
 }
 
+// ---- Interior-point measures (awebox_amd/ipm.py, solve_batch) -------------------------------------
+// One workgroup per instance computes, in one pass over its vectors, what the solver's loop head and
+// line search otherwise assemble from ~130 torch operations per iteration: IPOPT's scaled optimality
+// error and its parts (dual, primal, complementarity; the unscaled tests; the barrier problem's error
+// at the current mu) and the merit pair theta = ||c||_1, phi = the barrier function.  Every value is
+// the torch composition's (ipm.errors_torch / ipm.barrier_phi_torch): the same operations per entry,
+// rounded separately (no contraction), each sum in row_sum_kernel's order (thread t adds entries t,
+// t + 256, .. from 0.0, then the adjacent-pair tree), maxima with NaN propagation like torch's amax,
+// a division by a host scalar as torch performs it (a product with the host reciprocal).
+constexpr int kIpmThreads = 256;
+
+__device__ __forceinline__ double nan_max(double a, double b) { return (a != a || a > b) ? a : b; }
+__device__ __forceinline__ double clamp_lo(double v, double lo) { return (v != v) ? v : (v < lo ? lo : v); }
+
+__global__ __launch_bounds__(kIpmThreads) void ipm_measures_kernel(AweluIpmMeasures a) {
+#pragma clang fp contract(off)
+    constexpr int NW = kIpmThreads / 64;
+    __shared__ double part[16][NW];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const size_t oy = (size_t)b * a.ny, om = (size_t)b * a.m, oi = (size_t)b * a.mI, on = (size_t)b * a.n;
+    const bool head = a.mode == 0;
+    const double mu_h = a.mu[b];
+    const double kd_mu = mu_h * a.kappa_d;
+    // sums: 0 |zl|, 1 |zu|, 2 log gaps (lower), 3 (upper), 4 lower-only gaps, 5 upper-only gaps, 6 |c|,
+    // 7 |lam|; maxima: 0 |dual|, 1 |damped dual|, 2 |compl| at mu_target, 3 at mu, 4 unscaled |dual|,
+    // 5 |c|, 6 unscaled equality |c|, 7 inequality-row bound violation
+    double s[8], mx[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] = mx[q] = 0.0;
+    for (int i = t; i < a.ny; i += kIpmThreads) {
+        const double yv = a.y[oy + i];
+        const bool hl = a.hl[oy + i] != 0, hu = a.hu[oy + i] != 0;
+        const double dl = hl ? yv - a.yl[oy + i] : 1.0;
+        const double du = hu ? a.yu[oy + i] - yv : 1.0;
+        const double lo = a.lo_only[i], hi = a.hi_only[i];
+        s[2] = s[2] + (hl ? log(dl) : 0.0);
+        s[3] = s[3] + (hu ? log(du) : 0.0);
+        s[4] = s[4] + lo * dl;
+        s[5] = s[5] + hi * du;
+        if (head) {
+            const double zl = a.zl[oy + i], zu = a.zu[oy + i];
+            s[0] = s[0] + fabs(zl);
+            s[1] = s[1] + fabs(zu);
+            const double r = a.jt_lam[oy + i];
+            const double g = i < a.n ? a.grad[on + i] + r : 0.0 + (r - a.lam[om + a.ineq[i - a.n]]);
+            const double d = (g - zl) + zu;
+            const double dd = d + kd_mu * (lo - hi);
+            mx[0] = nan_max(mx[0], fabs(d));
+            mx[1] = nan_max(mx[1], fabs(dd));
+            const double clt = hl ? dl * zl - a.mu_target : 0.0, cut = hu ? du * zu - a.mu_target : 0.0;
+            const double clh = hl ? dl * zl - mu_h : 0.0, cuh = hu ? du * zu - mu_h : 0.0;
+            mx[2] = nan_max(mx[2], nan_max(fabs(clt), fabs(cut)));
+            mx[3] = nan_max(mx[3], nan_max(fabs(clh), fabs(cuh)));
+            mx[4] = nan_max(mx[4], i < a.n ? fabs(d) : fabs(d * a.cs_slack[oi + (i - a.n)]));
+        }
+    }
+    for (int j = t; j < a.m; j += kIpmThreads) {
+        const double cj = a.c[om + j];
+        s[6] = s[6] + fabs(cj);
+        mx[5] = nan_max(mx[5], fabs(cj));
+        if (head) {
+            s[7] = s[7] + fabs(a.lam[om + j]);
+            mx[6] = nan_max(mx[6], a.eq_row[j] ? fabs(cj / a.c_scale[om + j]) : 0.0);
+        }
+    }
+    if (head)
+        for (int k = t; k < a.mI; k += kIpmThreads) {
+            const double gI = (a.c[om + a.ineq[k]] + a.y[oy + a.n + k]) / a.cs_slack[oi + k];
+            const double gu = a.gu0[k], gl = a.gl0[k];
+            const double v = nan_max(isfinite(gu) ? gI - gu : 0.0, isfinite(gl) ? gl - gI : 0.0);
+            mx[7] = nan_max(mx[7], clamp_lo(v, 0.0));
+        }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        double v = s[q], w = mx[q];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            v = v + __shfl_xor(v, o);
+            w = nan_max(w, __shfl_xor(w, o));
+        }
+        if ((t & 63) == 0) {
+            part[q][t >> 6] = v;
+            part[8 + q][t >> 6] = w;
+        }
+    }
+    __syncthreads();
+    if (t != 0) return;
+    double S[8], A[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        S[q] = (part[q][0] + part[q][1]) + (part[q][2] + part[q][3]);
+        A[q] = nan_max(nan_max(part[8 + q][0], part[8 + q][1]), nan_max(part[8 + q][2], part[8 + q][3]));
+    }
+    const double theta = S[6];
+    const double phi = (a.f[b] - mu_h * (S[2] + S[3])) + kd_mu * (S[4] + S[5]);
+    double* out = a.out + b;
+    const long long B = a.B;
+    if (!head) {
+        out[0] = theta;
+        out[B] = phi;
+        return;
+    }
+    const double zsum = S[0] + S[1];
+    const double s_d = clamp_lo((S[7] + zsum) * a.inv_mnb, a.s_max) * a.inv_smax;
+    const double s_c = clamp_lo(zsum * a.inv_nb, a.s_max) * a.inv_smax;
+    const double e_pr = A[5];
+    const double e_d = A[0] / s_d, e_c = A[2] / s_c;
+    const double osc = a.obj_scale[b];
+    out[0] = nan_max(nan_max(e_d, e_pr), e_c);
+    out[B] = e_d;
+    out[2 * B] = e_pr;
+    out[3 * B] = e_c;
+    out[4 * B] = A[4] / osc;
+    out[5 * B] = nan_max(A[6], A[7]);
+    out[6 * B] = A[2] / osc;
+    out[7 * B] = nan_max(nan_max(A[1] / s_d, e_pr), A[3] / s_c);
+    out[8 * B] = theta;
+    out[9 * B] = phi;
+}
+
 extern "C" {
 
 const char* awelu_last_error(void) { return g_err.c_str(); }
@@ -1479,6 +1601,31 @@ int awelu_bmm(int batch, int M, int N, int K, const double* A, long long sAb, lo
         g_err = "output too large for one launch";
         return 1;
     }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// The interior-point measures (ipm_measures_kernel) of a->B instances: a->mode 0 writes the loop
+// head's ten rows out[row][b], mode 1 the merit pair (theta, phi).
+int awelu_ipm_measures(const AweluIpmMeasures* a, void* stream) {
+    if (!a || a->B < 0 || a->ny < 0 || a->n < 0 || a->n > a->ny || a->m < 0 || a->mI < 0 ||
+        a->n + a->mI != a->ny || (a->mode != 0 && a->mode != 1) || !a->out || !a->y || !a->yl || !a->yu ||
+        !a->hl || !a->hu || !a->lo_only || !a->hi_only || !a->f || !a->mu || (a->m > 0 && !a->c)) {
+        g_err = "awelu_ipm_measures: need ny = n + mI, mode 0 or 1 and device pointers";
+        return 1;
+    }
+    if (a->mode == 0 && (!a->grad || !a->jt_lam || !a->zl || !a->zu || !a->obj_scale ||
+                         (a->m > 0 && (!a->lam || !a->c_scale || !a->eq_row)) ||
+                         (a->mI > 0 && (!a->ineq || !a->cs_slack || !a->gl0 || !a->gu0)))) {
+        g_err = "awelu_ipm_measures: mode 0 needs the gradient, J^T lam, multipliers and scalings";
+        return 1;
+    }
+    if (a->B == 0) return 0;
+    ipm_measures_kernel<<<dim3((unsigned)a->B), kIpmThreads, 0, (hipStream_t)stream>>>(*a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

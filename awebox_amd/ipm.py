@@ -42,6 +42,7 @@ import numpy as np
 import torch
 
 from . import det
+from .ipm_measures import Measures
 from . import problem as pb
 
 
@@ -956,16 +957,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
 
     # IPOPT's kappa_d damping: + kappa_d mu (y - y_L) for variables bounded below only, and
     # + kappa_d mu (y_U - y) for those bounded above only, in the barrier function
-    lo_only = (hl & ~hu).to(torch.float64)
-    hi_only = (hu & ~hl).to(torch.float64)
-    damp_dir = lo_only - hi_only
-
-    def barrier_phi(fv, yv, mu_t):
-        dl, du = gaps(yv)
-        lg = det.row_sum(torch.where(hl, torch.log(dl), torch.zeros_like(dl))) + \
-            det.row_sum(torch.where(hu, torch.log(du), torch.zeros_like(du)))
-        dmp = det.row_sum(lo_only * dl) + det.row_sum(hi_only * du)
-        return fv - mu_t * lg + opts.kappa_d * mu_t * dmp
+    damp_dir = ((hl & ~hu).to(torch.float64)) - ((hu & ~hl).to(torch.float64))
 
     def grad_y(gradv):
         return torch.cat([gradv, torch.zeros(B, mI, **f64)], 1)
@@ -975,50 +967,9 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         r[:, n:] -= lamv[:, nlp.ineq_t]
         return r
 
-    nb = int(hl[0].sum().item() + hu[0].sum().item())
-
-    cs_slack = nlp.c_scale[:, nlp.ineq_t]
-    gl0 = torch.tensor(nlp.yl0[n:], **f64)
-    gu0 = torch.tensor(nlp.yu0[n:], **f64)
-
-    def errors(gradv, jvv, cv, yv, lamv, zlv, zuv, mu_t, damped=False, unscaled=False, dev_only=False):
-        """IPOPT's scaled optimality error per instance (host [B] arrays): total, dual, primal,
-        complementarity at barrier parameter mu_t ([B] tensor); ``damped`` adds the kappa_d term
-        (the barrier problem's error).  With ``unscaled`` also the unscaled dual infeasibility,
-        constraint violation (original bounds of the inequality rows) and complementarity that
-        IPOPT's termination tests compare with dual_inf_tol / constr_viol_tol / compl_inf_tol."""
-        dl, du = gaps(yv)
-        dual = grad_y(gradv) + A_T_lam(jvv, lamv) - zlv + zuv
-        if damped:
-            dual = dual + opts.kappa_d * mu_t[:, None] * damp_dir
-        compl_l = torch.where(hl, dl * zlv - mu_t[:, None], torch.zeros_like(yv))
-        compl_u = torch.where(hu, du * zuv - mu_t[:, None], torch.zeros_like(yv))
-        zsum = det.row_sum(zlv.abs()) + det.row_sum(zuv.abs())
-        s_d = torch.clamp((det.row_sum(lamv.abs()) + zsum) / max(1, m + nb), min=opts.s_max) / opts.s_max
-        s_c = torch.clamp(zsum / max(1, nb), min=opts.s_max) / opts.s_max
-        e_dual = dual.abs().amax(1) / s_d
-        e_pr = cv.abs().amax(1) if m else torch.zeros(B, **f64)
-        compl = torch.maximum(compl_l.abs().amax(1), compl_u.abs().amax(1))
-        e_c = compl / s_c
-        parts = [torch.maximum(torch.maximum(e_dual, e_pr), e_c), e_dual, e_pr, e_c]
-        if unscaled:
-            osc = nlp.obj_scale
-            u_dual = torch.maximum(dual[:, :n].abs().amax(1) if n else torch.zeros(B, **f64),
-                                   (dual[:, n:] * cs_slack).abs().amax(1) if mI else torch.zeros(B, **f64)) / osc
-            c_u = cv / nlp.c_scale
-            eq_mask = torch.ones(m, dtype=torch.bool, device=dev)
-            eq_mask[nlp.ineq_t] = False
-            u_pr = torch.where(eq_mask, c_u.abs(), torch.zeros_like(c_u)).amax(1) if m else torch.zeros(B, **f64)
-            if mI:
-                gI = (cv[:, nlp.ineq_t] + yv[:, n:]) / cs_slack         # g of the inequality rows, unscaled
-                vI = torch.maximum(torch.where(torch.isfinite(gu0), gI - gu0, torch.zeros_like(gI)),
-                                   torch.where(torch.isfinite(gl0), gl0 - gI, torch.zeros_like(gI)))
-                u_pr = torch.maximum(u_pr, torch.clamp(vI, min=0.0).amax(1))
-            parts += [u_dual, u_pr, compl / osc]
-        if dev_only:
-            return parts
-        e = torch.stack(parts).cpu().numpy()
-        return tuple(e)
+    # IPOPT's optimality error and the merit pair (theta, phi): one libawelu launch per call on the
+    # device, the torch composition on host tensors (ipm_measures.Measures)
+    meas = Measures(nlp, opts, jt_op, dev, n, mI, m, B)
 
     def ftb_dev(v, dv, mask_pos, tau_t):
         """Fraction-to-the-boundary step per instance on the device: min_i -tau v_i / dv_i ([B])."""
@@ -1173,10 +1124,9 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             with _Phase("eval_fg"):
                 ft, gt = nlp.eval_fg(yt[:, :n])
             ct = nlp.constraints(gt, yt[:, n:])
-            theta_t = det.row_sum(ct.abs())
-            phi_t = barrier_phi(ft, yt, dev_b(mu_t))
+            tp2 = meas.merit(ct, ft, yt, dev_b(mu_t))
             if alpha is None:
-                tp4 = torch.stack([theta_t, phi_t, alpha_dev, gphi_dev]).cpu().numpy()
+                tp4 = torch.cat([tp2, torch.stack([alpha_dev, gphi_dev])]).cpu().numpy()
                 tp, alpha, gphi_d = tp4[:2], tp4[2].copy(), tp4[3].copy()
                 alpha_max = alpha.copy()
                 alpha_min = opts.alpha_min_frac * np.where(
@@ -1193,7 +1143,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                     nback[skipped] += 1
                     first[skipped] = False
             else:
-                tp = torch.stack([theta_t, phi_t]).cpu().numpy()
+                tp = tp2.cpu().numpy()
             start_soc = np.zeros(B, dtype=bool)
             cont_soc = np.zeros(B, dtype=bool)
             for b in np.where(live)[0]:
@@ -1311,7 +1261,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
             lam_r = torch.where(sel, lam_r + dev_b(a_acc)[:, None] * sol[:, ny:], lam_r)
             ft, gt = nlp.eval_fg(yv[:, :n])
             ct = nlp.constraints(gt, yv[:, n:])
-            tp = torch.stack([det.row_sum(ct.abs()), barrier_phi(ft, yv, dev_b(mu_t))]).cpu().numpy()
+            tp = meas.merit(ct, ft, yv, dev_b(mu_t)).cpu().numpy()
             for b in np.where(live)[0]:
                 if tp[0, b] <= 0.9 * theta0_[b] and filter_ok(b, tp[0, b], tp[1, b]):
                     succ[b], live[b] = True, False
@@ -1328,10 +1278,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         # current mu (the first pass of the barrier update below) and theta / phi at the current mu
         # (the line search's reference values, unless mu changes)
         mu_head = dev_b(mu)
-        head = torch.stack(errors(grad, jv, c, y, lam, zl, zu, torch.full((B,), opts.mu_target, **f64),
-                                  unscaled=True, dev_only=True) +
-                           [errors(grad, jv, c, y, lam, zl, zu, mu_head, damped=True, dev_only=True)[0],
-                            det.row_sum(c.abs()), barrier_phi(f, y, mu_head)]).cpu().numpy()
+        head = meas.head(grad, jv, c, y, lam, zl, zu, f, mu_head).cpu().numpy()
         kkt_err, e_d, e_p, e_c, u_d, u_p, u_c = head[:7]
         e_mu_head, theta_head, phi_head = head[7], head[8], head[9]
         # IPOPT's OptimalityErrorConvergenceCheck: the scaled error and the unscaled tests
@@ -1351,7 +1298,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         # barrier update (monotone), per instance
         mu_changed = False
         for pass_ in range(50):
-            e_mu = e_mu_head if pass_ == 0 else errors(grad, jv, c, y, lam, zl, zu, dev_b(mu), damped=True)[0]
+            e_mu = e_mu_head if pass_ == 0 else meas.barrier_error(grad, jv, c, y, lam, zl, zu, f, dev_b(mu))
             upd = active & (e_mu <= opts.kappa_eps * mu) & (mu > mu_floor * 1.0000001)
             if not upd.any():
                 break
@@ -1372,7 +1319,7 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         grad_phi = grad_y(grad) - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
             torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y)) + opts.kappa_d * mu_d[:, None] * damp_dir
         if mu_changed:
-            theta, phi = torch.stack([det.row_sum(c.abs()), barrier_phi(f, y, mu_d)]).cpu().numpy()
+            theta, phi = meas.merit(c, f, y, mu_d).cpu().numpy()
         else:
             theta, phi = theta_head, phi_head
         rhs_top = -(grad_phi + A_T_lam(jv, lam))

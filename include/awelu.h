@@ -68,6 +68,40 @@ int awelu_bmm(int batch, int M, int N, int K, const double* A, long long sAb, lo
               const double* B, long long sBb, long long sBk, long long sBn, double* C, long long sCb, long long sCm,
               long long sCn, void* stream);
 
+/* The interior-point solver's per-iteration measures (awebox_amd/ipm.py solve_batch), one
+ * workgroup per instance, in place of ~130 torch operations per iteration: mode 0 writes out[r][b]
+ * for r = 0..9 (IPOPT's scaled optimality error at mu_target, its dual, primal and complementarity
+ * parts, the unscaled dual infeasibility, constraint violation and complementarity of the
+ * termination test, the barrier problem's error at mu[b], theta = ||c||_1 and the barrier function
+ * phi at mu[b]); mode 1 only theta and phi (rows 0, 1).  Arrays are row-major per instance:
+ * [B][ny] for y, its bounds, masks, zl, zu and jt_lam (J^T lam before the slack rows' -lam_I),
+ * [B][n] grad, [B][m] c, lam, c_scale, [B][mI] cs_slack, [B] f, mu, obj_scale; [ny] lo_only /
+ * hi_only (1.0 where only the lower / upper bound is finite), [m] eq_row, [mI] ineq, gl0, gu0.
+ * Every value rounds as the torch composition ipm.errors_torch / ipm.barrier_phi_torch (sums in
+ * awelu_row_sum's order, no contraction; inv_* are host reciprocals, as torch divides by a host
+ * scalar).  IPOPT's IpIpoptCalculatedQuantities (curr_nlp_error, curr_barrier_obj) for the reference's
+ * solver (opti/preparation.py:285-323). */
+typedef struct AweluIpmMeasures {
+    long long B;
+    int ny, n, m, mI, mode;
+    const double* grad;
+    const double* jt_lam;
+    const double* lam;
+    const long long* ineq;
+    const double *zl, *zu, *y, *yl, *yu;
+    const unsigned char *hl, *hu;
+    const double *lo_only, *hi_only;
+    const double* c;
+    const double* c_scale;
+    const double* cs_slack;
+    const unsigned char* eq_row;
+    const double *gl0, *gu0;
+    const double *obj_scale, *f, *mu;
+    double mu_target, kappa_d, s_max, inv_mnb, inv_nb, inv_smax;
+    double* out;
+} AweluIpmMeasures;
+int awelu_ipm_measures(const AweluIpmMeasures* a, void* stream);
+
 /* Message of the last failed call on this thread. */
 const char* awelu_last_error(void);
 
