@@ -1395,6 +1395,110 @@ __global__ __launch_bounds__(kIpmThreads) void ipm_measures_kernel(AweluIpmMeasu
     out[9 * B] = phi;
 }
 
+// The Newton system's vectors at an iterate (ipm.solve_batch, before the factorisation): the bound
+// gaps dl, du, the barrier diagonal Sigma, grad phi and the right-hand side [-(grad phi + A^T lam); -c],
+// every entry as the torch composition computes it (Measures.newton_torch).  A thread per entry of
+// [ny | m] and instance.
+__global__ __launch_bounds__(256) void ipm_newton_kernel(AweluIpmNewton a) {
+#pragma clang fp contract(off)
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.ny + a.m) return;
+    const size_t oy = (size_t)b * a.ny;
+    if (i >= a.ny) {
+        const int j = i - a.ny;
+        a.rhs[(size_t)b * (a.ny + a.m) + a.ny + j] = -a.c[(size_t)b * a.m + j];
+        return;
+    }
+    const double mu = a.mu[b];
+    const double yv = a.y[oy + i];
+    const bool hl = a.hl[oy + i] != 0, hu = a.hu[oy + i] != 0;
+    const double dl = hl ? yv - a.yl[oy + i] : 1.0;
+    const double du = hu ? a.yu[oy + i] - yv : 1.0;
+    const double sig = (hl ? a.zl[oy + i] / dl : 0.0) + (hu ? a.zu[oy + i] / du : 0.0);
+    const double g = i < a.n ? a.grad[(size_t)b * a.n + i] : 0.0;
+    const double gp = ((g - (hl ? mu / dl : 0.0)) + (hu ? mu / du : 0.0)) + (mu * a.kappa_d) * (a.lo_only[i] - a.hi_only[i]);
+    const double r = a.jt_lam[oy + i];
+    const double at = i < a.n ? r : r - a.lam[(size_t)b * a.m + a.ineq[i - a.n]];
+    a.dl[oy + i] = dl;
+    a.du[oy + i] = du;
+    a.sigma[oy + i] = sig;
+    a.grad_phi[oy + i] = gp;
+    a.rhs[(size_t)b * (a.ny + a.m) + i] = -(gp + at);
+}
+
+__device__ __forceinline__ double nan_min(double a, double b) { return (a != a || a < b) ? a : b; }
+
+// The accepted step (ipm.solve_batch after the line search): the bound multipliers' Newton step
+// dz = mu / gap - z -/+ z / gap dy at the Newton system's gaps (dl_old, du_old), its fraction-to-the-boundary length
+// alpha_z = min(1, min -tau z / dz) (a workgroup per instance: first pass and a block minimum), then
+// y <- y_new where accepted, lam += alpha dlam, z += alpha_z dz, and IPOPT's kappa_sigma safeguard
+// z <- clamp(z, mu / (kappa_sigma gap), kappa_sigma mu / gap) at the new gaps; every entry as the
+// torch composition (Measures.step_torch).  any_acc = 0: no instance stepped (only the safeguard).
+__global__ __launch_bounds__(kIpmThreads) void ipm_step_kernel(AweluIpmStep a) {
+#pragma clang fp contract(off)
+    constexpr int NW = kIpmThreads / 64;
+    __shared__ double part[NW];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const size_t oy = (size_t)b * a.ny;
+    const double mu = a.mu[b];
+    const bool acc = a.acc[b] != 0;
+    double az = 0.0;
+    if (a.any_acc) {
+        const double tau = a.tau[b];
+        double mn = INFINITY;
+        for (int i = t; i < a.ny; i += kIpmThreads) {
+            const bool hl = a.hl[oy + i] != 0, hu = a.hu[oy + i] != 0;
+            const double dl = a.dl_old[oy + i], du = a.du_old[oy + i];
+            const double zl = a.zl[oy + i], zu = a.zu[oy + i], dy = a.dy[oy + i];
+            const double dzl = hl ? (mu / dl - zl) - (zl / dl) * dy : 0.0;
+            const double dzu = hu ? (mu / du - zu) + (zu / du) * dy : 0.0;
+            mn = nan_min(mn, (hl && dzl < 0.0) ? (-tau * zl) / dzl : INFINITY);
+            mn = nan_min(mn, (hu && dzu < 0.0) ? (-tau * zu) / dzu : INFINITY);
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) mn = nan_min(mn, __shfl_xor(mn, o));
+        if ((t & 63) == 0) part[t >> 6] = mn;
+        __syncthreads();
+        mn = part[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) mn = nan_min(mn, part[w]);
+        const double az_b = nan_min(mn, 1.0);
+        az = acc ? az_b : 0.0;
+        if (t == 0) a.alpha_z[b] = az_b;
+    } else if (t == 0) {
+        a.alpha_z[b] = 0.0;
+    }
+    const double al = acc ? a.alpha[b] : 0.0;
+    for (int i = t; i < a.ny; i += kIpmThreads) {
+        const double yold = a.y[oy + i];
+        const bool hl = a.hl[oy + i] != 0, hu = a.hu[oy + i] != 0;
+        double zl = a.zl[oy + i], zu = a.zu[oy + i], yv = yold;
+        if (a.any_acc) {
+            const double dl = a.dl_old[oy + i], du = a.du_old[oy + i];
+            const double dy = a.dy[oy + i];
+            const double dzl = hl ? (mu / dl - zl) - (zl / dl) * dy : 0.0;
+            const double dzu = hu ? (mu / du - zu) + (zu / du) * dy : 0.0;
+            yv = acc ? a.y_new[oy + i] : yold;
+            zl = zl + az * dzl;
+            zu = zu + az * dzu;
+        }
+        const double dl = hl ? yv - a.yl[oy + i] : 1.0;
+        const double du = hu ? a.yu[oy + i] - yv : 1.0;
+        const double ks_mu = mu * a.kappa_sigma;
+        if (hl) zl = (zl != zl) ? zl : fmin(fmax(zl, mu / (dl * a.kappa_sigma)), ks_mu / dl);
+        if (hu) zu = (zu != zu) ? zu : fmin(fmax(zu, mu / (du * a.kappa_sigma)), ks_mu / du);
+        a.y_out[oy + i] = yv;
+        a.zl_out[oy + i] = zl;
+        a.zu_out[oy + i] = zu;
+    }
+    if (a.any_acc)
+        for (int j = t; j < a.m; j += kIpmThreads) {
+            const size_t k = (size_t)b * a.m + j;
+            a.lam_out[k] = a.lam[k] + al * a.dlam[k];
+        }
+}
+
 extern "C" {
 
 const char* awelu_last_error(void) { return g_err.c_str(); }
@@ -1626,6 +1730,43 @@ int awelu_ipm_measures(const AweluIpmMeasures* a, void* stream) {
     }
     if (a->B == 0) return 0;
     ipm_measures_kernel<<<dim3((unsigned)a->B), kIpmThreads, 0, (hipStream_t)stream>>>(*a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// The Newton system's vectors (ipm_newton_kernel) of a->B instances.
+int awelu_ipm_newton(const AweluIpmNewton* a, void* stream) {
+    if (!a || a->B < 0 || a->B > 65535 || a->n < 0 || a->mI < 0 || a->m < 0 || a->ny != a->n + a->mI ||
+        !a->y || !a->yl || !a->yu || !a->hl || !a->hu || !a->zl || !a->zu || !a->lo_only || !a->hi_only ||
+        !a->jt_lam || !a->mu || !a->dl || !a->du || !a->sigma || !a->grad_phi || !a->rhs ||
+        (a->n > 0 && !a->grad) || (a->m > 0 && (!a->c || !a->lam)) || (a->mI > 0 && !a->ineq)) {
+        g_err = "awelu_ipm_newton: need ny = n + mI, B <= 65535 and device pointers";
+        return 1;
+    }
+    if (a->B == 0 || a->ny + a->m == 0) return 0;
+    ipm_newton_kernel<<<dim3((unsigned)((a->ny + a->m + 255) / 256), (unsigned)a->B), 256, 0, (hipStream_t)stream>>>(*a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// The accepted step and the kappa_sigma safeguard (ipm_step_kernel) of a->B instances.
+int awelu_ipm_step(const AweluIpmStep* a, void* stream) {
+    if (!a || a->B < 0 || a->ny < 0 || a->m < 0 || !a->y || !a->yl || !a->yu || !a->hl || !a->hu || !a->zl ||
+        !a->zu || !a->mu || !a->acc || !a->y_out || !a->zl_out || !a->zu_out || !a->alpha_z ||
+        (a->any_acc && (!a->y_new || !a->dy || !a->dl_old || !a->du_old || !a->tau || !a->alpha || (a->m > 0 && (!a->lam || !a->dlam || !a->lam_out))))) {
+        g_err = "awelu_ipm_step: need device pointers";
+        return 1;
+    }
+    if (a->B == 0) return 0;
+    ipm_step_kernel<<<dim3((unsigned)a->B), kIpmThreads, 0, (hipStream_t)stream>>>(*a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

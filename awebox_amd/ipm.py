@@ -955,20 +955,12 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         du = torch.where(hu, yu - yv, torch.ones_like(yv))
         return dl, du
 
-    # IPOPT's kappa_d damping: + kappa_d mu (y - y_L) for variables bounded below only, and
-    # + kappa_d mu (y_U - y) for those bounded above only, in the barrier function
-    damp_dir = ((hl & ~hu).to(torch.float64)) - ((hu & ~hl).to(torch.float64))
-
     def grad_y(gradv):
         return torch.cat([gradv, torch.zeros(B, mI, **f64)], 1)
 
-    def A_T_lam(jvv, lamv):
-        r = jt_op.mv(jvv, lamv)
-        r[:, n:] -= lamv[:, nlp.ineq_t]
-        return r
-
-    # IPOPT's optimality error and the merit pair (theta, phi): one libawelu launch per call on the
-    # device, the torch composition on host tensors (ipm_measures.Measures)
+    # IPOPT's optimality error, the merit pair (theta, phi), the Newton system's vectors and the step
+    # update (with the kappa_d damping of one-sided bounds and the kappa_sigma safeguard): one libawelu
+    # launch each per call on the device, the torch composition on host tensors (ipm_measures.Measures)
     meas = Measures(nlp, opts, jt_op, dev, n, mI, m, B)
 
     def ftb_dev(v, dv, mask_pos, tau_t):
@@ -1313,17 +1305,13 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
         # ---- Newton system ----------------------------------------------------------------------
         with _Phase("hessian"):
             hv = nlp.hess(y[:, :n], lam)
-        dl, du = gaps(y)
         mu_d = dev_b(mu)
-        sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
-        grad_phi = grad_y(grad) - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
-            torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y)) + opts.kappa_d * mu_d[:, None] * damp_dir
+        dl, du, sigma, grad_phi, rhs = meas.newton(grad, jv, c, y, lam, zl, zu, mu_d)
+        rhs_top = rhs[:, :ny]
         if mu_changed:
             theta, phi = meas.merit(c, f, y, mu_d).cpu().numpy()
         else:
             theta, phi = theta_head, phi_head
-        rhs_top = -(grad_phi + A_T_lam(jv, lam))
-        rhs = torch.cat([rhs_top, -c], 1)
         pending = active.copy()
         wd_new = np.zeros(B, dtype=bool)
         if opts.watchdog_shortened_iter_trigger > 0:
@@ -1406,34 +1394,14 @@ def solve_batch(ev, P, x0, lbx, ubx, lbg, ubg, lam0=None, zl0=None, zu0=None, op
                 sel = dev_b(succ)[:, None] > 0
                 y = torch.where(sel, y_r, y)
                 lam = torch.where(sel, lam_r, lam)
-        # ---- accepted steps: primal, multipliers, bound multipliers ------------------------------
-        if acc_all.any():
-            sel = dev_b(acc_all)[:, None] > 0
-            dzl = torch.where(hl, mu_d[:, None] / dl - zl - zl / dl * dy_new, torch.zeros_like(y))
-            dzu = torch.where(hu, mu_d[:, None] / du - zu + zu / du * dy_new, torch.zeros_like(y))
-            # the bound multipliers' step on the device (min(1, steps to the bounds), exact like the
-            # host minimum); its host copy only for the log, with f below
-            az_dev = torch.minimum(torch.minimum(ftb_dev(zl, dzl, hl, tau_d), ftb_dev(zu, dzu, hu, tau_d)),
-                                   torch.ones(B, **f64))
-            az = torch.where(dev_b(acc_all) > 0, az_dev, torch.zeros_like(az_dev))[:, None]
-            y = torch.where(sel, y_new, y)
-            lam = lam + dev_b(np.where(acc_all, alpha_acc, 0.0))[:, None] * dlam_new
-            zl = zl + az * dzl
-            zu = zu + az * dzu
-        else:
-            az_dev = torch.zeros(B, **f64)
-        if wd_restore.any():
-            # the watchdog failed: the iterate returns to its starting point (the next iteration's
-            # direction there is the one the watchdog started with) and skips the full step
-            selr = dev_b(wd_restore)[:, None] > 0
-            y, lam, zl, zu = (torch.where(selr, r, t) for t, r in zip((y, lam, zl, zu), wd_pt))
+        # ---- accepted steps: primal, multipliers, bound multipliers; the kappa_sigma safeguard -------
+        # (a watchdog that failed returns its instances to the watchdog's starting point, whose next
+        # direction is the one the watchdog started with, and skips the full step there)
+        restore = (wd_restore, wd_pt) if wd_restore.any() else None
+        y, lam, zl, zu, az_dev = meas.step(acc_all, y, y_new, dy_new, lam, dlam_new, zl, zu, dl, du, mu_d, tau_d,
+                                           alpha_acc, restore)
+        if restore is not None:
             wd_skip |= wd_restore
-        # kappa_sigma safeguard
-        dl, du = gaps(y)
-        zl = torch.where(hl, torch.clamp(zl, min=mu_d[:, None] / (opts.kappa_sigma * dl),
-                                         max=opts.kappa_sigma * mu_d[:, None] / dl), zl)
-        zu = torch.where(hu, torch.clamp(zu, min=mu_d[:, None] / (opts.kappa_sigma * du),
-                                         max=opts.kappa_sigma * mu_d[:, None] / du), zu)
         with _Phase("eval_all"):
             f, grad, g, jv = nlp.eval_all(y[:, :n])
         if rest_ok.any():

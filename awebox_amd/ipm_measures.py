@@ -16,6 +16,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 from . import det
@@ -29,6 +30,23 @@ class AweluIpmMeasures(ctypes.Structure):
                                         "obj_scale", "f", "mu")] + \
         [(k, ctypes.c_double) for k in ("mu_target", "kappa_d", "s_max", "inv_mnb", "inv_nb", "inv_smax")] + \
         [("out", ctypes.c_void_p)]
+
+
+class AweluIpmNewton(ctypes.Structure):
+    """include/awelu.h AweluIpmNewton."""
+    _fields_ = [(k, ctypes.c_int) for k in ("B", "ny", "n", "m", "mI")] + \
+        [(k, ctypes.c_void_p) for k in ("y", "yl", "yu", "hl", "hu", "zl", "zu", "grad", "jt_lam", "lam", "c", "ineq",
+                                        "lo_only", "hi_only", "mu")] + \
+        [("kappa_d", ctypes.c_double)] + [(k, ctypes.c_void_p) for k in ("dl", "du", "sigma", "grad_phi", "rhs")]
+
+
+class AweluIpmStep(ctypes.Structure):
+    """include/awelu.h AweluIpmStep."""
+    _fields_ = [(k, ctypes.c_int) for k in ("B", "ny", "m", "any_acc")] + \
+        [(k, ctypes.c_void_p) for k in ("y", "y_new", "dy", "lam", "dlam", "zl", "zu", "yl", "yu", "dl_old", "du_old",
+                                        "hl", "hu", "acc", "mu", "tau", "alpha")] + \
+        [("kappa_sigma", ctypes.c_double)] + \
+        [(k, ctypes.c_void_p) for k in ("y_out", "lam_out", "zl_out", "zu_out", "alpha_z")]
 
 
 HEAD_ROWS = 10      # kkt error, e_dual, e_pr, e_c, unscaled dual / primal / compl, barrier error, theta, phi
@@ -75,6 +93,8 @@ class Measures:
             from .batched_lu import load_library
             self._lib = load_library()
             self._lib.awelu_ipm_measures.argtypes = [ctypes.POINTER(AweluIpmMeasures), ctypes.c_void_p]
+            self._lib.awelu_ipm_newton.argtypes = [ctypes.POINTER(AweluIpmNewton), ctypes.c_void_p]
+            self._lib.awelu_ipm_step.argtypes = [ctypes.POINTER(AweluIpmStep), ctypes.c_void_p]
 
     # ---- device kernel ---------------------------------------------------------------------------
     def _launch(self, mode, y, c, f, mu, grad=None, jt_lam=None, lam=None, zl=None, zu=None):
@@ -103,6 +123,22 @@ class Measures:
             raise RuntimeError(f"awelu_ipm_measures: {self._lib.awelu_last_error().decode()}")
         return out
 
+    def _check(self, rc, name):
+        if rc != 0:
+            raise RuntimeError(f"{name}: {self._lib.awelu_last_error().decode()}")
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _dev_mask(self, a):
+        """A host [B] bool array as a device uint8 tensor (pinned, asynchronous)."""
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8))
+        return t.pin_memory().to(self.dev, non_blocking=True)
+
+    def _dev_vec(self, a):
+        t = torch.from_numpy(np.array(a, dtype=np.float64))
+        return t.pin_memory().to(self.dev, non_blocking=True)
+
     # ---- the solver's calls ----------------------------------------------------------------------
     def head(self, grad, jv, c, y, lam, zl, zu, f, mu_head):
         """[10, B] device tensor: the scaled error at mu_target with its parts (rows 0-3), the
@@ -127,7 +163,96 @@ class Measures:
             return self._launch(1, y, c, f, mu)
         return torch.stack([det.row_sum(c.abs()), self.barrier_phi_torch(f, y, mu)])
 
+    def newton(self, grad, jv, c, y, lam, zl, zu, mu):
+        """(dl, du, sigma, grad_phi, rhs) of the Newton system at the iterate, ``mu`` a [B] device
+        tensor: the bound gaps, the barrier diagonal, the barrier gradient and the right-hand side
+        [-(grad phi + A^T lam); -c] ([B, ny + m])."""
+        if not self.fused:
+            return self.newton_torch(grad, jv, c, y, lam, zl, zu, mu)
+        B, ny, m = self.B, self.ny, self.m
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        jt = self.jt_op.mv(jv, lam)
+        y, zl, zu, grad, lam, c, mu = (t.contiguous() for t in (y, zl, zu, grad, lam, c, mu))
+        dl, du, sigma, gp = (torch.empty(B, ny, **f64) for _ in range(4))
+        rhs = torch.empty(B, ny + m, **f64)
+        a = AweluIpmNewton(B=B, ny=ny, n=self.n, m=m, mI=self.mI, y=_ptr(y), yl=_ptr(self.nlp.yl), yu=_ptr(self.nlp.yu),
+                           hl=_ptr(self._hl), hu=_ptr(self._hu), zl=_ptr(zl), zu=_ptr(zu), grad=_ptr(grad),
+                           jt_lam=_ptr(jt), lam=_ptr(lam), c=_ptr(c), ineq=_ptr(self._ineq), lo_only=_ptr(self._lo),
+                           hi_only=_ptr(self._hi), mu=_ptr(mu), kappa_d=self.opts.kappa_d, dl=_ptr(dl), du=_ptr(du),
+                           sigma=_ptr(sigma), grad_phi=_ptr(gp), rhs=_ptr(rhs))
+        self._check(self._lib.awelu_ipm_newton(ctypes.byref(a), self._stream()), "awelu_ipm_newton")
+        return dl, du, sigma, gp, rhs
+
+    def step(self, acc, y, y_new, dy, lam, dlam, zl, zu, dl, du, mu, tau, alpha, restore=None):
+        """The accepted step and the kappa_sigma safeguard: (y, lam, zl, zu, alpha_z) after the
+        iteration.  ``acc`` host [B] bool (stepped instances), ``alpha`` host [B] primal step lengths,
+        ``dl``, ``du`` the Newton system's gaps, ``mu``, ``tau`` [B] device tensors; ``restore`` =
+        (host mask, (y, lam, zl, zu) of the watchdog's start) returns those instances there before
+        the safeguard (the torch composition then)."""
+        if not self.fused or restore is not None:
+            return self.step_torch(acc, y, y_new, dy, lam, dlam, zl, zu, dl, du, mu, tau, alpha, restore)
+        B, ny, m = self.B, self.ny, self.m
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        any_acc = bool(np.any(acc))
+        y, y_new, dy, lam, dlam, zl, zu, mu, tau = (t.contiguous() for t in (y, y_new, dy, lam, dlam, zl, zu, mu, tau))
+        acc_d = self._dev_mask(acc)
+        al = self._dev_vec(alpha)
+        y_o, zl_o, zu_o = (torch.empty(B, ny, **f64) for _ in range(3))
+        lam_o = torch.empty(B, m, **f64) if any_acc else lam
+        az = torch.empty(B, **f64)
+        a = AweluIpmStep(B=B, ny=ny, m=m, any_acc=int(any_acc), y=_ptr(y), y_new=_ptr(y_new), dy=_ptr(dy), lam=_ptr(lam),
+                         dlam=_ptr(dlam), zl=_ptr(zl), zu=_ptr(zu), yl=_ptr(self.nlp.yl), yu=_ptr(self.nlp.yu),
+                         dl_old=_ptr(dl.contiguous()), du_old=_ptr(du.contiguous()), hl=_ptr(self._hl), hu=_ptr(self._hu),
+                         acc=_ptr(acc_d), mu=_ptr(mu), tau=_ptr(tau), alpha=_ptr(al), kappa_sigma=self.opts.kappa_sigma,
+                         y_out=_ptr(y_o), lam_out=_ptr(lam_o), zl_out=_ptr(zl_o), zu_out=_ptr(zu_o), alpha_z=_ptr(az))
+        self._check(self._lib.awelu_ipm_step(ctypes.byref(a), self._stream()), "awelu_ipm_step")
+        return y_o, lam_o, zl_o, zu_o, az
+
     # ---- the torch composition (the CPU harness; the kernel's restatement) --------------------------
+    def newton_torch(self, grad, jv, c, y, lam, zl, zu, mu_d):
+        hl, hu, B, mI = self.hl, self.hu, self.B, self.mI
+        dl, du = self.gaps(y)
+        sigma = torch.where(hl, zl / dl, torch.zeros_like(y)) + torch.where(hu, zu / du, torch.zeros_like(y))
+        grad_y = torch.cat([grad, torch.zeros(B, mI, dtype=torch.float64, device=grad.device)], 1)
+        grad_phi = grad_y - torch.where(hl, mu_d[:, None] / dl, torch.zeros_like(y)) + \
+            torch.where(hu, mu_d[:, None] / du, torch.zeros_like(y)) + self.opts.kappa_d * mu_d[:, None] * self.damp_dir
+        rhs_top = -(grad_phi + self.A_T_lam(jv, lam))
+        return dl, du, sigma, grad_phi, torch.cat([rhs_top, -c], 1)
+
+    def ftb(self, v, dv, mask_pos, tau_t):
+        """Fraction-to-the-boundary step per instance on the device: min_i -tau v_i / dv_i ([B])."""
+        ratio = torch.where(mask_pos & (dv < 0), -tau_t[:, None] * v / dv, torch.full_like(v, float("inf")))
+        return ratio.amin(1) if ratio.shape[1] else torch.full((self.B,), float("inf"), dtype=torch.float64,
+                                                               device=v.device)
+
+    def step_torch(self, acc, y, y_new, dy, lam, dlam, zl, zu, dl, du, mu_d, tau_d, alpha, restore=None):
+        hl, hu, B, opts = self.hl, self.hu, self.B, self.opts
+        f64 = dict(dtype=torch.float64, device=y.device)
+        dev_m = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=bool)).to(y.device)  # noqa: E731
+        if np.any(acc):
+            sel = dev_m(acc)[:, None]
+            dzl = torch.where(hl, mu_d[:, None] / dl - zl - zl / dl * dy, torch.zeros_like(y))
+            dzu = torch.where(hu, mu_d[:, None] / du - zu + zu / du * dy, torch.zeros_like(y))
+            az_dev = torch.minimum(torch.minimum(self.ftb(zl, dzl, hl, tau_d), self.ftb(zu, dzu, hu, tau_d)),
+                                   torch.ones(B, **f64))
+            az = torch.where(dev_m(acc), az_dev, torch.zeros_like(az_dev))[:, None]
+            y = torch.where(sel, y_new, y)
+            lam = lam + torch.tensor(np.where(acc, alpha, 0.0), **f64)[:, None] * dlam
+            zl = zl + az * dzl
+            zu = zu + az * dzu
+        else:
+            az_dev = torch.zeros(B, **f64)
+        if restore is not None:
+            # the watchdog failed: the iterate returns to its starting point
+            selr = dev_m(restore[0])[:, None]
+            y, lam, zl, zu = (torch.where(selr, r, t) for t, r in zip((y, lam, zl, zu), restore[1]))
+        dl, du = self.gaps(y)
+        zl = torch.where(hl, torch.clamp(zl, min=mu_d[:, None] / (opts.kappa_sigma * dl),
+                                         max=opts.kappa_sigma * mu_d[:, None] / dl), zl)
+        zu = torch.where(hu, torch.clamp(zu, min=mu_d[:, None] / (opts.kappa_sigma * du),
+                                         max=opts.kappa_sigma * mu_d[:, None] / du), zu)
+        return y, lam, zl, zu, az_dev
+
     def gaps(self, yv):
         dl = torch.where(self.hl, yv - self.nlp.yl, torch.ones_like(yv))
         du = torch.where(self.hu, self.nlp.yu - yv, torch.ones_like(yv))

@@ -102,6 +102,41 @@ typedef struct AweluIpmMeasures {
 } AweluIpmMeasures;
 int awelu_ipm_measures(const AweluIpmMeasures* a, void* stream);
 
+/* The Newton system's vectors at an iterate (ipm.solve_batch): dl, du (bound gaps, 1 where a bound
+ * is infinite), sigma = z_L / dl + z_U / du, grad phi = grad f - mu / dl + mu / du + kappa_d mu
+ * (lo_only - hi_only) and rhs [B][ny + m] = [-(grad phi + J^T lam - lam_I on the slacks); -c], as
+ * the torch composition ipm_measures.Measures.newton_torch rounds them.  Arrays as in
+ * AweluIpmMeasures; outputs [B][ny] (rhs [B][ny + m]).  IPOPT's PDFullSpaceSolver right-hand side
+ * (IpPDFullSpaceSolver.cpp) for the reference's solver. */
+typedef struct AweluIpmNewton {
+    int B, ny, n, m, mI;
+    const double *y, *yl, *yu;
+    const unsigned char *hl, *hu;
+    const double *zl, *zu, *grad, *jt_lam, *lam, *c;
+    const long long* ineq;
+    const double *lo_only, *hi_only, *mu;
+    double kappa_d;
+    double *dl, *du, *sigma, *grad_phi, *rhs;
+} AweluIpmNewton;
+int awelu_ipm_newton(const AweluIpmNewton* a, void* stream);
+
+/* The accepted step (ipm.solve_batch): dz = mu / gap - z -/+ (z / gap) dy at the Newton system's gaps
+ * dl_old, du_old (awelu_ipm_newton's dl, du), alpha_z[b] =
+ * min(1, min over dz < 0 of -tau z / dz), then per instance with acc[b]: y_out = y_new, lam_out = lam +
+ * alpha[b] dlam, z_out = z + alpha_z dz (instances without acc[b] keep y and add 0 * steps, as the torch
+ * composition does); and for all instances IPOPT's kappa_sigma safeguard at the new gaps,
+ * z <- clamp(z, mu / (kappa_sigma gap), kappa_sigma mu / gap).  any_acc = 0: no instance stepped
+ * (y, lam unchanged; only the safeguard).  Every entry as Measures.step_torch rounds it. */
+typedef struct AweluIpmStep {
+    int B, ny, m, any_acc;
+    const double *y, *y_new, *dy, *lam, *dlam, *zl, *zu, *yl, *yu, *dl_old, *du_old;
+    const unsigned char *hl, *hu, *acc;
+    const double *mu, *tau, *alpha;
+    double kappa_sigma;
+    double *y_out, *lam_out, *zl_out, *zu_out, *alpha_z;
+} AweluIpmStep;
+int awelu_ipm_step(const AweluIpmStep* a, void* stream);
+
 /* Message of the last failed call on this thread. */
 const char* awelu_last_error(void);
 

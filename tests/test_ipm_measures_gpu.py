@@ -91,3 +91,41 @@ def test_measures_kernel_is_the_torch_composition(B, n, mI, m, nnz, poison):
     one = Measures(nlp1, opts, jt_op, torch.device("cuda"), n, mI, m, 1)
     h1 = one.head(*(a[b:b + 1] for a in args))
     assert _same(h1[:, 0], got_head[:, b])
+
+
+@pytest.mark.parametrize("B,n,mI,m,nnz,poison", [(5, 300, 40, 250, 2000, False), (4, 1000, 0, 600, 5000, True),
+                                                 (6, 2900, 120, 2600, 20000, True), (2, 1, 1, 1, 3, False)])
+def test_newton_and_step_kernels_are_the_torch_composition(B, n, mI, m, nnz, poison):
+    """awelu_ipm_newton (gaps, Sigma, grad phi, right-hand side) and awelu_ipm_step (accepted step,
+    alpha_z, kappa_sigma safeguard; stepped and not stepped instances, no instance stepped) bitwise
+    their torch compositions."""
+    _need_gpu()
+    from awebox_amd.ipm_measures import Measures
+    nlp, jt_op, d, opts = _case(B * 7 + n, B, n, mI, m, nnz, poison)
+    opts.kappa_sigma = 1e10
+    dev = torch.device("cuda")
+    meas = Measures(nlp, opts, jt_op, dev, n, mI, m, B)
+    args = (d["grad"], d["jv"], d["c"], d["y"], d["lam"], d["zl"], d["zu"], d["mu"])
+    got = meas.newton(*args)
+    meas.fused = False
+    ref = meas.newton(*args)
+    for name, a, b in zip(("dl", "du", "sigma", "grad_phi", "rhs"), got, ref):
+        assert _same(a, b), name
+    dl, du = ref[0], ref[1]
+    rng = np.random.default_rng(B + n)
+    ny = n + mI
+    t = lambda a: torch.tensor(a, dtype=torch.float64, device=dev)  # noqa: E731
+    dy = t(rng.normal(size=(B, ny)) * 0.01)
+    y_new = d["y"] + 0.5 * dy
+    dlam = t(rng.normal(size=(B, m)))
+    tau = t(np.full(B, 0.99))
+    alpha = rng.uniform(0.1, 1.0, size=B)
+    if poison:
+        dlam[0, 0] = float("inf")          # an instance that does not step: lam + 0 * inf
+    for acc in (np.arange(B) % 2 == 1, np.ones(B, dtype=bool), np.zeros(B, dtype=bool)):
+        meas.fused = True
+        g = meas.step(acc, d["y"], y_new, dy, d["lam"], dlam, d["zl"], d["zu"], dl, du, d["mu"], tau, alpha)
+        meas.fused = False
+        r = meas.step(acc, d["y"], y_new, dy, d["lam"], dlam, d["zl"], d["zu"], dl, du, d["mu"], tau, alpha)
+        for name, a, b in zip(("y", "lam", "zl", "zu", "alpha_z"), g, r):
+            assert _same(a, b), (name, acc)
