@@ -261,10 +261,12 @@ class _ScatterSum:
         while lo < (count.max() if len(count) else 0):
             sel = np.where((count > lo) & (count <= width))[0]
             if len(sel):
+                # row u of the table: the sources of destination uniq[sel[u]] in order, padded
+                cnt, st = count[sel], start[sel]
+                wi = np.arange(width)
+                has = wi[None, :] < cnt[:, None]
                 table = np.full((len(sel), width), len(dst), dtype=np.int64)
-                for w in range(width):
-                    has = count[sel] > w
-                    table[has, w] = order[start[sel][has] + w]
+                table[has] = order[(st[:, None] + wi[None, :])[has]]
                 self.buckets.append((torch.tensor(uniq[sel], device=dev), torch.tensor(table, device=dev)))
                 if width <= self.NATIVE_MAX_W:
                     narrow.append((uniq[sel], table))
@@ -453,19 +455,18 @@ class StructuredKKT:
         n_k, stride, v0, rows = lay.n_k, lay.interval_stride, lay.v_intervals, lay.rows_per_interval
         nx = getattr(lay, "nx", pb.NX)                          # states per shooting node
         owner = np.full(N, -1, dtype=np.int64)                  # interval of an interior unknown
-        for p, v in enumerate(nlp.free):
-            if v >= v0:
-                k, o = divmod(v - v0, stride)
-                if k < n_k and o >= nx:
-                    owner[p] = k
+        free = np.asarray(nlp.free.cpu().numpy() if torch.is_tensor(nlp.free) else nlp.free, dtype=np.int64)
+        kf, of = np.divmod(free - v0, stride)
+        inner = (free >= v0) & (kf < n_k) & (of >= nx)
+        owner[:n][inner] = kf[inner]
         # interval rows start at g0: the MPC NLP leads with nx initial-condition rows
         # (ocp/operation.py:303-326), the periodic NLP has none
         g0 = getattr(lay, "g_int0", 0)
         if g0 > nx:
             raise ValueError("more leading rows than states per node")
-        for i, r in enumerate(nlp.ineq):
-            rr_ = r - g0
-            owner[n + i] = rr_ // rows if 0 <= rr_ < n_k * rows else -1    # global rows (t_f bounds): separators
+        rr_ = np.asarray(nlp.ineq, dtype=np.int64) - g0
+        # global rows (t_f bounds): separators
+        owner[n:n + len(rr_)] = np.where((rr_ >= 0) & (rr_ < n_k * rows), rr_ // rows, -1)
         # interval rows, except the continuity rows: an interval has more rows than interior
         # unknowns (x[k], x[k+1] close the count), so their multipliers join the separators
         rr = np.arange(m) - g0
@@ -475,11 +476,12 @@ class StructuredKKT:
         self.nS = len(sep)
         sep_id = np.full(N, -1, dtype=np.int64)
         sep_id[sep] = np.arange(self.nS)
-        loc = np.full(N, -1, dtype=np.int64)
-        counts = np.zeros(n_k, dtype=np.int64)
-        for p in np.where(owner >= 0)[0]:
-            loc[p] = counts[owner[p]]
-            counts[owner[p]] += 1
+        loc = np.full(N, -1, dtype=np.int64)                    # position within the interval's block
+        ip = np.where(owner >= 0)[0]
+        counts = np.bincount(owner[ip], minlength=n_k).astype(np.int64)
+        by_k = np.argsort(owner[ip], kind="stable")
+        first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        loc[ip[by_k]] = np.arange(len(ip)) - first[owner[ip][by_k]]
         self.nI = int(counts.max())
         self.n_k = n_k
         # KKT pattern in COO (both orientations), in the order of the value vector of factor()
@@ -516,9 +518,9 @@ class StructuredKKT:
         dst_is = oP[isi] * nI * L + loc[P_[isi]] * L + lpos[oP[isi], sep_id[Q_[isi]]]
         self.sel_ss = torch.tensor(np.where(ss)[0], device=dev)
         dst_ss = sep_id[P_[ss]] * (nS + 1) + sep_id[Q_[ss]]
-        pad = [(k, j) for k in range(n_k) for j in range(int(counts[k]), nI)]
-        self.n_pad = len(pad)
-        self.pad_flat = torch.tensor([k * nI * nI + j * nI + j for k, j in pad], dtype=torch.int64, device=dev)
+        pk, pj = np.nonzero(np.arange(nI)[None, :] >= counts[:, None])   # padding rows, by interval
+        self.n_pad = len(pk)
+        self.pad_flat = torch.tensor(pk * nI * nI + pj * nI + pj, dtype=torch.int64, device=dev)
         schur_flat = (lsep_arr[:, :, None] * (nS + 1) + lsep_arr[:, None, :]).reshape(-1)
         int_p = np.where(owner >= 0)[0]
         self.int_p = torch.tensor(int_p, device=dev)
@@ -537,20 +539,22 @@ class StructuredKKT:
         if lu_backend == "awelu" and separators == "btd":
             stage_of = np.full(self.nS, -1, dtype=np.int64)
             pos_of = np.zeros(self.nS, dtype=np.int64)
-            free = np.asarray(nlp.free.cpu().numpy() if torch.is_tensor(nlp.free) else nlp.free)
-            for q, p in enumerate(sep):
-                if p < n:
-                    v = int(free[p])
-                    if v >= v0:
-                        k, o = divmod(v - v0, stride)
-                        if o < nx and k <= n_k:
-                            stage_of[q], pos_of[q] = k, nx + o
-                elif p >= ny:
-                    r = p - ny - g0
-                    if r < 0:                                   # initial-condition rows: stage 0 beside x[0]
-                        stage_of[q], pos_of[q] = 0, r + g0
-                    elif r < n_k * rows and r % rows >= rows - nx:
-                        stage_of[q], pos_of[q] = r // rows + 1, r % rows - (rows - nx)
+            # shooting states x[k] at positions nx.. of stage k
+            xs = sep < n
+            vq = free[sep[xs]]
+            kq, oq = np.divmod(vq - v0, stride)
+            hit = (vq >= v0) & (oq < nx) & (kq <= n_k)
+            qx = np.where(xs)[0][hit]
+            stage_of[qx], pos_of[qx] = kq[hit], nx + oq[hit]
+            # multipliers: initial-condition rows at stage 0 beside x[0], continuity rows of interval k
+            # at positions 0.. of stage k + 1
+            cs = sep >= ny
+            rq = sep[cs] - ny - g0
+            qc = np.where(cs)[0]
+            ic = rq < 0
+            stage_of[qc[ic]], pos_of[qc[ic]] = 0, rq[ic] + g0
+            ct = (rq >= 0) & (rq < n_k * rows) & (rq % rows >= rows - nx)
+            stage_of[qc[ct]], pos_of[qc[ct]] = rq[ct] // rows + 1, rq[ct] % rows - (rows - nx)
             ss_r, ss_c = sep_id[P_[ss]], sep_id[Q_[ss]]
             sch_r, sch_c = lsep_arr[:, :, None].repeat(L, 2), lsep_arr[:, None, :].repeat(L, 1)
             from .btd import BorderedBtd
@@ -782,29 +786,38 @@ _STRUCT_CACHE: dict = {}
 def cached_kkt_structures():
     """The StructuredKKT objects of the recent solves' structure cache (read-only use: bench.py
     times the solver kernels at their block shapes)."""
-    return [e[1] for e in _STRUCT_CACHE.values()]
+    return [e[0] for e in _STRUCT_CACHE.values()]
+
+
+def _layout_key(lay):
+    """What StructuredKKT reads from a layout: two evaluators whose layouts agree here (and whose NLPs
+    have the same patterns) share one structure."""
+    return (type(lay).__name__, lay.n_k, lay.interval_stride, lay.v_intervals, lay.rows_per_interval,
+            getattr(lay, "nx", pb.NX), getattr(lay, "g_int0", 0))
 
 
 def _structure(ev, nlp, dev, opts):
-    """(StructuredKKT, J^T product, H product) for one NLP structure, shared by the solves of the
-    same evaluator and the same fixed-variable / inequality sets (every sampling time of the MPC
-    solves its pre-solve and main solve on one structure): their construction is host work of
-    ~3 ms per solve_batch call.  Only structural data enters them; the per-solve state (the
-    factorisation, the counters, the separator switches) is reset or overwritten by every solve."""
+    """(StructuredKKT, J^T product, H product) for one NLP structure, shared by the solves with the
+    same layout and the same fixed-variable / inequality sets and patterns, whichever evaluator (and
+    batch) runs them: every sampling time of the MPC solves its pre-solve and main solve on one
+    structure, and a sweep shard's batched warm start reuses its homotopy's final structure.  Their
+    construction is host work of ~0.1 s at AP2 N=40.  Only structural data enters them; the per-solve
+    state (the factorisation, the counters, the separator switches) is reset or overwritten by every
+    solve."""
     import hashlib
-    import weakref
     h = hashlib.sha1()
     for a in (nlp.free, nlp.ineq, nlp.j_row.cpu().numpy(), nlp.j_col.cpu().numpy(), nlp.h_r.cpu().numpy(),
               nlp.h_c.cpu().numpy()):
         h.update(np.ascontiguousarray(a, dtype=np.int64).tobytes())
         h.update(b"|")
-    key = (id(ev), h.hexdigest(), str(torch.device(dev)), opts.lu_backend, opts.separators)
+    key = (_layout_key(ev.layout), len(nlp.x_fix), h.hexdigest(),
+           str(torch.device(dev)), opts.lu_backend, opts.separators)
     ent = _STRUCT_CACHE.get(key)
-    if ent is not None and ent[0]() is ev:
-        skkt = ent[1]
+    if ent is not None:
+        skkt = ent[0]
         skkt.n_solve = skkt.n_dense = 0
         skkt.force_btd = skkt.btd_off = False
-        return ent[1], ent[2], ent[3]
+        return ent
     skkt = StructuredKKT(nlp, ev.layout, dev, lu_backend=opts.lu_backend, separators=opts.separators)
     ny, m = nlp.ny, nlp.m
     jt_op = _GatherMv(nlp.j_col.cpu().numpy(), nlp.j_row.cpu().numpy(), (ny, m), dev)
@@ -813,7 +826,7 @@ def _structure(ev, nlp, dev, opts):
     h_op = _GatherMv(np.concatenate([hr_np, hc_np[off_np]]), np.concatenate([hc_np, hr_np[off_np]]), (ny, ny), dev)
     if len(_STRUCT_CACHE) >= 8:
         _STRUCT_CACHE.clear()
-    _STRUCT_CACHE[key] = (weakref.ref(ev), skkt, jt_op, h_op)
+    _STRUCT_CACHE[key] = (skkt, jt_op, h_op)
     return skkt, jt_op, h_op
 
 
