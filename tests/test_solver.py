@@ -261,3 +261,29 @@ def test_watchdog_reaches_the_same_solution_on_cpu_port():
     assert [r["iterations"] for r in ref[1]] != [r["iterations"] for r in got[1]]   # the watchdog ran
     assert abs(got[2]["avg_power_W"] - ref[2]["avg_power_W"]) <= 1e-6 * abs(ref[2]["avg_power_W"])
     assert abs(got[2]["period_s"] - ref[2]["period_s"]) <= 1e-6 * ref[2]["period_s"]
+
+
+def test_kkt_structure_is_shared_by_evaluators_of_one_layout():
+    """ipm._structure caches by layout and pattern: a second evaluator of the same problem (a sweep
+    shard's batched warm start after its homotopy) reuses the StructuredKKT and the J^T / H products;
+    another fixed-variable set gets its own."""
+    from oracle.cpu_device import CpuDeviceEvaluator
+    from awebox_amd.ipm import DeviceNlp, IpmOptions, _structure
+    n_k, d = 4, 3
+    consts = pb.build_constants(pb.Ap2Config(n_k=n_k, d=d))
+    lay = pb.NlpLayout(n_k, d)
+    v0 = initial_guess(consts, lay)
+    sched = hm.schedule(consts, lay, v0)
+    lbg, ubg = lay.g_bounds()
+    opts = IpmOptions()
+
+    def struct(st):
+        ev = CpuDeviceEvaluator(consts)
+        nlp = DeviceNlp(ev, pb.pack_p(lay, consts, v0, step=st.cost_step), st.lbx, st.ubx, lbg, ubg, "cpu")
+        return _structure(ev, nlp, "cpu", opts)
+
+    a, b = struct(sched[-1]), struct(sched[-1])
+    assert all(x is y for x, y in zip(a, b))
+    c = struct(sched[0])
+    if not np.array_equal(sched[0].lbx >= sched[0].ubx, sched[-1].lbx >= sched[-1].ubx):
+        assert c[0] is not a[0]

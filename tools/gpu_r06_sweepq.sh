@@ -1,6 +1,8 @@
 #!/bin/bash
-# Quick: the bench's AP2 and dual sweep blocks only.
+# Quick: the bench's AP2 and dual sweep blocks only, then a kernel-trace summary of the converged
+# MPC block alone.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
 set -o pipefail
 O=gpurun_out/sweepq
 mkdir -p $O
@@ -12,3 +14,6 @@ for k in ('sweep','dual_sweep'):
     v=d.get(k)
     if isinstance(v,dict): print(k, {kk: v.get(kk) for kk in ('value','wall_s','iterations')})
 "
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/pmpc_prof -o run --output-format csv -- python -u bench.py --steps 1 --warmup 0 --batch 8 --no-cpu-baseline --no-hessian --no-latency --dual-batch 0 --mpc-batch 64 --pmpc-loops 64 --sweep-points 0 --dual-sweep-points 0 > $O/pmpc_prof.log 2>&1 || { tail -20 $O/pmpc_prof.log; exit 1; }
+find $O/pmpc_prof -name '*_trace.csv' -delete
+echo SWEEPQ_DONE
