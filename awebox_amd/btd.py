@@ -103,10 +103,14 @@ class BorderedBtd:
             from .batched_lu import btd_factor
             self.Tf = btd_factor(T)
         else:
-            self._factor_blocks(T)
+            # the forward sweep of T^-1 E rides along with the block recursion (see _factor_blocks)
+            Yf = self._factor_blocks(T, E.view(B, nb, m, nG) if nG else None)
         self.Fm = Fm.view(B, nG, n_t)
         if nG:
-            self.Z = self._t_solve(E.view(B, n_t, nG))                     # T^-1 E
+            if self.fused:
+                self.Z = self._t_solve(E.view(B, n_t, nG))                 # T^-1 E
+            else:
+                self.Z = self._t_backward(Yf)
             Cp = C.view(B, nG, nG) - det.bmm(self.Fm, self.Z)
             self.Cp = Cp
             self.Cf = self._lu(Cp)
@@ -136,25 +140,54 @@ class BorderedBtd:
     def dev_is_cuda(self):
         return torch.device(self.dev).type == "cuda"
 
-    def _factor_blocks(self, T):
+    def _factor_blocks(self, T, X=None):
         """The block sweep by a block recursion over batched dense operations (blocks larger than
         the fused kernels' LDS limit, and host tensors): D'_0 = D_0, W_k = D'_k^-1 U_k,
         D'_k = D_k - L_k W_{k-1}, with an LU (partial pivoting) of every pivot block -- the awelu
-        kernels on the device, LAPACK on the host."""
+        kernels on the device, LAPACK on the host.
+
+        With X [B, nb, m, r] (the border columns E) the forward sweep of T^-1 X runs in the same
+        stages, Y_k = D'_k^-1 (X_k - L_k Y_{k-1}): L_k multiplies [W_{k-1} | Y_{k-1}] in one product
+        and D'_k^-1 is applied to [U_k | X_k - L_k Y_{k-1}] in one solve, so the sweep costs no
+        launches of its own.  Every entry is the same sum as in separate calls (products summed over
+        k in sequence, solves column by column), so Y is bitwise _t_solve's forward sweep.  Returns
+        the list of Y_k (None without X)."""
         B, nb, m = T.shape[0], self.nb, self.m
         self.T_blocks = T
-        Dp, LUs, Ws = [], [], []
+        Dp, LUs, Ws, Y = [], [], [], []
         D = T[:, 0, 1]
+        rk = X[:, 0] if X is not None else None
         for k in range(nb):
             if k > 0:
-                D = T[:, k, 1] - det.bmm(T[:, k, 0], Ws[k - 1])
+                if X is None:
+                    D = T[:, k, 1] - det.bmm(T[:, k, 0], Ws[k - 1])
+                else:
+                    P = det.bmm(T[:, k, 0], torch.cat([Ws[k - 1], Y[k - 1]], 2))
+                    D = T[:, k, 1] - P[:, :, :m]
+                    rk = X[:, k] - P[:, :, m:]
             LU = self._lu(D.contiguous())
             Dp.append(D)
             LUs.append(LU)
             if k < nb - 1:
-                Ws.append(self._lu_solve(LU, T[:, k, 2].contiguous()))
+                if X is None:
+                    Ws.append(self._lu_solve(LU, T[:, k, 2].contiguous()))
+                else:
+                    S = self._lu_solve(LU, torch.cat([T[:, k, 2], rk], 2).contiguous())
+                    Ws.append(S[:, :, :m])
+                    Y.append(S[:, :, m:])
+            elif X is not None:
+                Y.append(self._lu_solve(LU, rk.contiguous()))
         self.Dp = torch.stack(Dp, 1)
         self.LUs, self.Ws = LUs, Ws
+        return Y if X is not None else None
+
+    def _t_backward(self, Y):
+        """The backward sweep of T^-1 X from the forward sweep's Y_k: x_k = Y_k - W_k x_{k+1}."""
+        B, nb, m = self.B, self.nb, self.m
+        Y = list(Y)
+        for k in range(nb - 2, -1, -1):
+            Y[k] = Y[k] - det.bmm(self.Ws[k], Y[k + 1])
+        return torch.stack(Y, 1).reshape(B, nb * m, -1)
 
     AWELU_SOLVE = True          # device: the awelu solve kernel (False: rocSOLVER getrs, A/B only)
 
