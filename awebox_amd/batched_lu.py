@@ -31,6 +31,7 @@ def load_library(path: str = _PATH):
         ll, vp = ctypes.c_longlong, ctypes.c_void_p
         lib.awelu_row_sum.argtypes = [ll, ll, vp, ll, vp, vp]
         lib.awelu_bmm.argtypes = [ctypes.c_int] * 4 + [vp, ll, ll, ll] * 3 + [vp]
+        lib.awelu_gather_sum_wide.argtypes = [ctypes.c_int] * 2 + [vp] * 5 + [ll] + [vp] * 2 + [ll, vp, ll, vp]
         lib.awelu_last_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
@@ -142,6 +143,25 @@ def gather_sum(lsrc, lw, ldst, vals, out, rows, x=None, cols=None):
                               x.shape[-1] if x is not None else 0, ptr(out), out.shape[-1], ctypes.c_void_p(s))
     if rc != 0:
         raise RuntimeError(f"awelu_gather_sum: {lib.awelu_last_error().decode()}")
+    return out
+
+
+def gather_sum_wide(wsrc, woff, ww, wdst, vals, out, rows, x=None, cols=None):
+    """The wide lists (more than 64 sources) of ipm._ScatterSum's sums in one launch
+    (awelu_gather_sum_wide): out[r][wdst[l]] += list l's sum of vals[r][wsrc] (times x[r][cols[wsrc]])
+    in det.row_sum's order.  wsrc / woff / ww / wdst int32 device tensors."""
+    import torch
+    nl = wdst.numel()
+    if nl == 0 or rows == 0:
+        return out
+    lib = load_library()
+    s = torch.cuda.current_stream(out.device).cuda_stream
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)  # noqa: E731
+    rc = lib.awelu_gather_sum_wide(nl, rows, ptr(wsrc), ptr(woff), ptr(ww), ptr(wdst), ptr(vals), vals.shape[-1],
+                                   ptr(x), ptr(cols), x.shape[-1] if x is not None else 0, ptr(out), out.shape[-1],
+                                   ctypes.c_void_p(s))
+    if rc != 0:
+        raise RuntimeError(f"awelu_gather_sum_wide: {lib.awelu_last_error().decode()}")
     return out
 
 

@@ -1176,6 +1176,43 @@ __global__ __launch_bounds__(256) void gather_sum_kernel(int L, const int* __res
     if (l < L && d >= 0) out[r * ldo + d] = out[r * ldo + d] + v;
 }
 
+// The lists wider than 64 of the same gather-sums (the few long destination lists, e.g. t_f's
+// column of J): one workgroup per (list, row), the list's sources summed in awelu_row_sum's order over
+// its power-of-two width (thread t adds entries t, t + 256, .. from 0.0, padding entries as 0.0, then
+// the adjacent-pair tree), then added to the destination -- bitwise what ipm._ScatterSum's torch path
+// (gather, det.row_sum, indexed add) computes, in one launch for all wide lists.
+__global__ __launch_bounds__(256) void gather_sum_wide_kernel(const int* __restrict__ wsrc, const int* __restrict__ woff,
+                                                              const int* __restrict__ ww, const int* __restrict__ wdst,
+                                                              const double* __restrict__ vals, long long ldv,
+                                                              const double* __restrict__ x, const int* __restrict__ cols,
+                                                              long long ldx, double* __restrict__ out, long long ldo) {
+#pragma clang fp contract(off)
+    __shared__ double part[4];
+    const int l = blockIdx.x, t = threadIdx.x;
+    const long long r = blockIdx.y;
+    const int* src = wsrc + woff[l];
+    const int W = ww[l];
+    double acc = 0.0;
+    for (int j = t; j < W; j += 256) {
+        const int sj = src[j];
+        double v = 0.0;
+        if (sj >= 0) {
+            v = vals[r * ldv + sj];
+            if (x) v = v * x[r * ldx + cols[sj]];
+        }
+        acc = acc + v;
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) acc = acc + __shfl_xor(acc, o);
+    if ((t & 63) == 0) part[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) {
+        const double sum = (part[0] + part[1]) + (part[2] + part[3]);
+        double* o = out + r * ldo + wdst[l];
+        *o = *o + sum;
+    }
+}
+
 // ---- Batch-invariant reductions and products (awebox_amd/det.py) --------------------------------
 // The interior-point solver's per-instance algebra on [B, n] tensors must round the same way
 // whatever B is: a problem solved alone and the same problem inside a batch of 128 (or inside a
@@ -1779,6 +1816,27 @@ int awelu_ipm_step(const AweluIpmStep* a, void* stream) {
     }
     if (a->B == 0) return 0;
     ipm_step_kernel<<<dim3((unsigned)a->B), kIpmThreads, 0, (hipStream_t)stream>>>(*a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_err = hipGetErrorString(e);
+        return 2;
+    }
+    return 0;
+}
+
+// The wide lists of the gather-sums (gather_sum_wide_kernel): nl lists, list l's sources
+// wsrc[woff[l] .. woff[l] + ww[l]) (-1 = padding), added to out[r * ldo + wdst[l]] for r < rows.
+int awelu_gather_sum_wide(int nl, int rows, const int* wsrc, const int* woff, const int* ww, const int* wdst,
+                          const double* vals, long long ldv, const double* x, const int* cols, long long ldx,
+                          double* out, long long ldo, void* stream) {
+    if (nl < 0 || rows < 0 || rows > 65535 || (nl > 0 && (!wsrc || !woff || !ww || !wdst || !vals || !out)) ||
+        (x && !cols)) {
+        g_err = "need nl >= 0, 0 <= rows <= 65535 and device pointers (cols with x)";
+        return 1;
+    }
+    if (nl == 0 || rows == 0) return 0;
+    gather_sum_wide_kernel<<<dim3((unsigned)nl, (unsigned)rows), 256, 0, (hipStream_t)stream>>>(
+        wsrc, woff, ww, wdst, vals, ldv, x, cols, ldx, out, ldo);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         g_err = hipGetErrorString(e);

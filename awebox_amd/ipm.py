@@ -243,9 +243,9 @@ class _ScatterSum:
 
     On the GPU every bucket up to width 64 goes through one launch of libawelu's gather-sum
     kernel (awelu_gather_sum: lists in lanes, adjacent-pair shuffle trees -- bitwise the gather,
-    row sum and indexed add that torch performs per bucket, ~5 launches each); wider buckets (the
-    few long rows, e.g. t_f's column of J) keep the torch reduction, whose order over more than 64
-    entries the kernel does not reproduce."""
+    row sum and indexed add that torch performs per bucket, ~5 launches each); the wider buckets (the
+    few long rows, e.g. t_f's column of J) go through a second launch (awelu_gather_sum_wide) that sums
+    each list in det.row_sum's order -- bitwise torch's gather, row sum and indexed add for them."""
 
     NATIVE_MAX_W = 64
 
@@ -257,6 +257,7 @@ class _ScatterSum:
         uniq, start, count = np.unique(dst[order], return_index=True, return_counts=True)
         self.buckets = []                                       # (dst, table) on the device, all widths
         narrow = []                                             # host tables of width <= 64
+        wide_h = []                                             # host tables wider than 64
         lo, width = 0, 1
         while lo < (count.max() if len(count) else 0):
             sel = np.where((count > lo) & (count <= width))[0]
@@ -270,6 +271,8 @@ class _ScatterSum:
                 self.buckets.append((torch.tensor(uniq[sel], device=dev), torch.tensor(table, device=dev)))
                 if width <= self.NATIVE_MAX_W:
                     narrow.append((uniq[sel], table))
+                else:
+                    wide_h.append((uniq[sel], table))
             lo, width = width, 2 * width
         self.wide = [(d, t) for d, t in self.buckets if t.shape[1] > self.NATIVE_MAX_W]
         # AWE_NATIVE_GATHER_SUM=0: the torch reduction everywhere (A/B measurements)
@@ -281,6 +284,17 @@ class _ScatterSum:
             self.lsrc = torch.tensor(lsrc.astype(np.int32), device=dev)
             self.lw = torch.tensor(lw, device=dev)
             self.ldst = torch.tensor(ldst.astype(np.int32), device=dev)
+        # the wide lists in one launch too (awelu_gather_sum_wide, det.row_sum's order);
+        # AWE_NATIVE_WIDE=0: torch's gather + row sum for them (A/B measurements)
+        self.native_wide = self.native and bool(wide_h) and os.environ.get("AWE_NATIVE_WIDE", "1") != "0"
+        if self.native_wide:
+            wsrc = np.concatenate([np.where(t == len(dst), -1, t).reshape(-1) for _, t in wide_h])
+            ww = np.concatenate([np.full(t.shape[0], t.shape[1]) for _, t in wide_h])
+            self.wsrc_host = wsrc
+            self.wsrc = torch.tensor(wsrc.astype(np.int32), device=dev)
+            self.ww = torch.tensor(ww.astype(np.int32), device=dev)
+            self.woff = torch.tensor(np.concatenate([[0], np.cumsum(ww)[:-1]]).astype(np.int32), device=dev)
+            self.wdst = torch.tensor(np.concatenate([d for d, _ in wide_h]).astype(np.int32), device=dev)
 
     @staticmethod
     def build_lanes(narrow, n_src):
@@ -322,11 +336,19 @@ class _ScatterSum:
         gather_sum(lsrc, self.lw, self.ldst, vals.contiguous(), out, rows,
                    x=x.contiguous() if x is not None else None, cols=cols)
 
+    def _launch_wide(self, out, vals, wsrc, x=None, cols=None):
+        from .batched_lu import gather_sum_wide
+        rows = out.numel() // max(1, out.shape[-1]) if out.dim() > 1 else 1
+        gather_sum_wide(wsrc, self.woff, self.ww, self.wdst, vals.contiguous(), out, rows,
+                        x=x.contiguous() if x is not None else None, cols=cols)
+
     def add_into(self, out, vals):
         if not self._native_ok(out, vals):
             return self._torch_buckets(out, vals, self.buckets)
         self._launch(out, vals, self.lsrc)
-        if self.wide:
+        if self.native_wide:
+            self._launch_wide(out, vals, self.wsrc)
+        elif self.wide:
             self._torch_buckets(out, vals, self.wide)
         return out
 
@@ -343,14 +365,20 @@ class _ScatterSum:
             s_h = sel.cpu().numpy()
             lsrc = self.lanes_host[0]
             comp = np.where(lsrc >= 0, s_h[np.clip(lsrc, 0, None)], -1)
+            wcomp = None
+            if self.native_wide:
+                ws = self.wsrc_host
+                wcomp = torch.tensor(np.where(ws >= 0, s_h[np.clip(ws, 0, None)], -1).astype(np.int32), device=self.dev)
             lanes = self._sel_lanes
 
             def _drop(r, k=key):                              # the entry dies with its sel tensor
                 if lanes.get(k, (None,))[0] is r:
                     del lanes[k]
-            ent = lanes[key] = (weakref.ref(sel, _drop), torch.tensor(comp.astype(np.int32), device=self.dev))
+            ent = lanes[key] = (weakref.ref(sel, _drop), torch.tensor(comp.astype(np.int32), device=self.dev), wcomp)
         self._launch(out, vals, ent[1])
-        if self.wide:
+        if self.native_wide:
+            self._launch_wide(out, vals, ent[2])
+        elif self.wide:
             self._torch_buckets(out, vals[..., sel], self.wide)
         return out
 
@@ -360,7 +388,9 @@ class _ScatterSum:
         if not self._native_ok(out, vals, x):
             return self.add_into(out, vals * x[..., cols])
         self._launch(out, vals, self.lsrc, x=x, cols=cols32)
-        if self.wide:
+        if self.native_wide:
+            self._launch_wide(out, vals, self.wsrc, x=x, cols=cols32)
+        elif self.wide:
             self._torch_buckets(out, vals * x[..., cols], self.wide)
         return out
 

@@ -51,6 +51,13 @@ int awelu_gather_sum(int L, int rows, const int* lsrc, const unsigned char* lw, 
                      long long ldv, const double* x, const int* cols, long long ldx, double* out, long long ldo,
                      void* stream);
 
+/* The destination lists longer than 64 sources of the same gather-sums, in one launch: list l's
+ * sources wsrc[woff[l] .. woff[l] + ww[l]) (a power-of-two width, -1 = padding) are summed per row in
+ * awelu_row_sum's order and added to out[r * ldo + wdst[l]]; vals / x / cols as in awelu_gather_sum. */
+int awelu_gather_sum_wide(int nl, int rows, const int* wsrc, const int* woff, const int* ww, const int* wdst,
+                          const double* vals, long long ldv, const double* x, const int* cols, long long ldx,
+                          double* out, long long ldo, void* stream);
+
 /* Batch-invariant row sums (awebox_amd/det.py): out[r] = sum of x[r * ldx + j] over j < n, for
  * r < rows.  Thread t of 256 adds x[t], x[t + 256], ... in sequence; the 256 partial sums are added
  * as an adjacent-pair tree.  The order depends on n only, never on rows, so a solver's norms, dot

@@ -80,7 +80,7 @@ def test_awelu_exports_every_header_symbol():
     hdr = os.path.join(os.path.dirname(HEADER), "awelu.h")
     declared = set(re.findall(r"^(?:int|const char\*)\s+(awelu_\w+)\(", open(hdr).read(), re.M))
     assert declared == {"awelu_factor_batched", "awelu_solve_batched", "awelu_btd_factor_batched", "awelu_btd_solve_batched",
-                        "awelu_sym_inertia_batched", "awelu_gather_sum", "awelu_row_sum", "awelu_bmm",
+                        "awelu_sym_inertia_batched", "awelu_gather_sum", "awelu_gather_sum_wide", "awelu_row_sum", "awelu_bmm",
                         "awelu_ipm_measures", "awelu_ipm_newton", "awelu_ipm_step",
                         "awelu_last_error"}
     out = subprocess.run(["nm", "-D", "--defined-only", LIB_LU], capture_output=True, text=True, check=True).stdout
