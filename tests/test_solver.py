@@ -287,3 +287,30 @@ def test_kkt_structure_is_shared_by_evaluators_of_one_layout():
     c = struct(sched[0])
     if not np.array_equal(sched[0].lbx >= sched[0].ubx, sched[-1].lbx >= sched[-1].ubx):
         assert c[0] is not a[0]
+
+
+def test_btd_merged_forward_sweep_matches_separate_solve():
+    """btd.BorderedBtd._factor_blocks with the border columns E (the forward sweep of T^-1 E inside
+    the factorisation's stages, then _t_backward) gives T^-1 E as the separate block solve does
+    (host LAPACK path; on the device the two are bitwise equal)."""
+    import torch
+    from awebox_amd.btd import BorderedBtd
+    rng = np.random.default_rng(5)
+    B, nb, m, r = 2, 6, 7, 3
+    T = torch.tensor(rng.normal(size=(B, nb, 3, m, m)) * 0.2)
+    T[:, :, 1] += 3.0 * torch.eye(m, dtype=torch.float64)
+    E = torch.tensor(rng.normal(size=(B, nb * m, r)))
+    bt = BorderedBtd.__new__(BorderedBtd)
+    bt.nb, bt.m, bt.B = nb, m, B
+    Y = bt._factor_blocks(T, E.view(B, nb, m, r))
+    merged = bt._t_backward(Y)
+    bt.fused = False
+    separate = bt._t_solve(E)
+    np.testing.assert_allclose(merged.numpy(), separate.numpy(), rtol=1e-12, atol=1e-13)
+    # and T^-1 E is what a dense solve of the block-tridiagonal matrix gives
+    A = torch.zeros(B, nb * m, nb * m, dtype=torch.float64)
+    for k in range(nb):
+        for s_, dk in ((0, -1), (1, 0), (2, 1)):
+            if 0 <= k + dk < nb:
+                A[:, k * m:(k + 1) * m, (k + dk) * m:(k + dk + 1) * m] = T[:, k, s_]
+    np.testing.assert_allclose(merged.numpy(), torch.linalg.solve(A, E).numpy(), rtol=1e-10, atol=1e-12)
