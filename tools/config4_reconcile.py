@@ -42,12 +42,13 @@ def main():
     ap.add_argument("--points", type=int, default=64)
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "config4_reconcile.json"))
+    ap.add_argument("--no-watchdog", action="store_true", help="IPOPT's watchdog off (A/B against records before it)")
     args = ap.parse_args()
     from awebox_amd.dual_homotopy import make_evaluator
     from awebox_amd.ipm import IpmOptions
     from awebox_amd.sweep import reconcile_shard, run_sweep, speculate, warm_point_solver
     grid = np.linspace(5.0, 8.0, 64)[:args.points]
-    opts = IpmOptions(max_iter=3000)
+    opts = IpmOptions(max_iter=3000, watchdog_shortened_iter_trigger=0 if args.no_watchdog else 10)
     mk = lambda c, b=1: make_evaluator(c, batch=b)  # noqa: E731
     t0 = time.perf_counter()
     glob = run_sweep(grid, n_k=args.n_k, d=4, make_evaluator=mk, device="cuda", opts=opts, arch="dual",
